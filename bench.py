@@ -1,0 +1,295 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident rx parse + checksum throughput (BASELINE.json metric).
+
+Headline workload (BASELINE.json configs[1]): 1M synthetic 64 B IPv4/UDP frames resident in
+HBM, protocol.CheckSumEnable = true, parsed Ethernet -> IPv4 -> UDP with both checksums
+verified, one 32 B result record per frame. A step is one launch of the hot-path kernel over
+one batch of 1M frames. Batches rotate over --rotate distinct slices of the synthetic stream
+so the working set (8 x 102 MB) exceeds the 256 MB Infinity Cache and every step streams
+from HBM.
+
+Multi-GPU (torchrun, one process per GPU): every rank parses its own shard of the global
+frame stream (weak scaling, no data-path collective; the gloo group only carries the
+barrier and the max-over-ranks timing). value = frames all ranks parsed / max wall time.
+
+Extra fields: roofline (dominant kernel, algorithmic bytes / HIP-event kernel time vs the
+8 TB/s HBM3E spec peak), cpu_baseline (the C oracle, a scalar port of the Go path, timed on
+this host's cores on a bounded sample), secondary (1500 B, IMIX, 9000 B jumbo, and the
+cache-resident variant of the headline; N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpps + Gbit/s device-resident parse+cksum, 64B & 1500B frames, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+RESULT_BYTES = 32
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse_args():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--frames", type=int, default=1 << 20, help="frames per batch per GPU")
+    p.add_argument("--rotate", type=int, default=8, help="distinct batches cycled through")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-secondary", action="store_true")
+    return p.parse_args()
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.pg = dist
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.pg:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+def make_batches(dev, netif, *, n, rotate, rank, length=64, size_mode=0, proto_mode=0, strided=False):
+    from halo_amd import synth
+
+    batches = []
+    for b in range(rotate):
+        first = (rank * rotate + b) * n
+        lay = synth.layout(n, length=length, size_mode=size_mode, proto_mode=proto_mode, first_index=first,
+                           ragged=not strided)
+        fr = synth.frames_device(lay, netif, device=dev, stride=length if strided else 0)
+        fr["layout"] = lay
+        batches.append(fr)
+    return batches
+
+
+def frame_bytes(fr) -> int:
+    return int(fr["layout"]["lens"].astype("int64").sum())
+
+
+def time_kernel(launch, steps, warmup, d: Dist):
+    """Wall time of `steps` launches (barrier + sync both sides) and per-launch HIP-event
+    kernel time on the launch stream (torch's current stream, which the C ABI is given)."""
+    import torch
+
+    for i in range(warmup):
+        launch(i)
+    torch.cuda.synchronize()
+    d.barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record()
+        launch(i)
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    d.barrier()
+    kern = sorted(a.elapsed_time(b) for a, b in ev)
+    return d.max(wall), sum(kern) / len(kern), kern[len(kern) // 2]
+
+
+def ragged_launcher(batches, out, netif, hint, flags=1):
+    from halo_amd import _lib
+    import torch
+
+    L = _lib.lib
+
+    def launch(i):
+        fr = batches[i % len(batches)]
+        rc = L.halo_rx_parse_batch_device(fr["bytes"].data_ptr(), fr["offsets_dw"].data_ptr(),
+                                          fr["lens"].data_ptr(), fr["layout"]["n"], flags, netif, hint,
+                                          out.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+        if rc:
+            raise _lib.HaloError("halo_rx_parse_batch_device", rc)
+    return launch
+
+
+def strided_launcher(batches, out, netif, length, flags):
+    from halo_amd import _lib
+    import torch
+
+    L = _lib.lib
+
+    def launch(i):
+        fr = batches[i % len(batches)]
+        rc = L.halo_rx_parse_strided_device(fr["bytes"].data_ptr(), length, None, length, fr["layout"]["n"], flags,
+                                            netif, out.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+        if rc:
+            raise _lib.HaloError("halo_rx_parse_strided_device", rc)
+    return launch
+
+
+def roofline(alg_bytes_per_launch, kernel_ms, traffic=None):
+    achieved = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get(workload, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(fr, seconds: float):
+    """The C oracle (scalar restatement of the Go path) on the host, 1 thread, then all cores."""
+    import numpy as np
+
+    from oracle import oracle
+
+    oracle.build()
+    lay = fr["layout"]
+    host = fr["bytes"].cpu().numpy()
+    netif = oracle.NetIf.make()
+    res = {}
+    for threads in (1, min(os.cpu_count() or 1, 16)):
+        oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads)  # warm
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 2 or (threads > 1 and el >= 2.0):
+                break
+        res[threads] = (passes * lay["n"] / el / 1e6, passes, el)
+    one, mt = res[1], res[max(res)]
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(one[0], 3), "unit": "Mpps", "cores": 1, "kind": "port",
+            "sample": f"{lay['n']} x {int(lay['lens'][0])}B UDP frames (batch 0 of the workload), "
+                      f"{one[1]} passes in {one[2]:.1f}s, oracle/halo_rx_oracle.c -O2, one thread "
+                      f"(the reference's one goroutine per NetIf); cpu={model}",
+            "multi_thread": {"value": round(mt[0], 3), "threads": max(res), "passes": mt[1]}}
+
+
+def main():
+    args = parse_args()
+    import numpy as np  # noqa: F401
+    import torch
+
+    d = Dist()
+    torch.cuda.set_device(d.local)
+    dev = torch.device("cuda", d.local)
+    from halo_amd import _lib
+    from halo_amd._lib import NetIf
+
+    _lib.check("halo_rx_init", _lib.lib.halo_rx_init(d.local))
+    netif = NetIf.make()  # eth0 of example.UsePcapDev (example/example.go:768-773)
+    n = args.frames
+
+    log(f"[rank {d.rank}] generating {args.rotate} x {n} frames of 64 B")
+    batches = make_batches(dev, netif, n=n, rotate=args.rotate, rank=d.rank)
+    out = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    wall, kern_ms, kern_med = time_kernel(ragged_launcher(batches, out, netif, 64), args.steps, args.warmup, d)
+    frames_total = n * args.steps * d.world
+    mpps = frames_total / wall / 1e6
+    fbytes = frame_bytes(batches[0])
+    gbit = fbytes * args.steps * d.world * 8 / wall / 1e9
+    alg = fbytes + n * (4 + 2 + RESULT_BYTES)  # frames + dword offset + u16 len + record
+    line = {
+        "metric": METRIC, "value": round(mpps, 2), "unit": "Mpps", "n_gpus": d.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "config2: 1M x 64B IPv4/UDP frames resident in HBM, CheckSumEnable=true, "
+                               "ragged ring-record layout (u32 dword offsets + u16 lens), 32B record/frame",
+                   "frames_per_gpu_per_step": n, "frame_bytes": 64, "rotating_batches": args.rotate,
+                   "parallelism": f"index-sharded x{d.world}, no collective"},
+        "gbit_s": round(gbit, 2),
+        "kernel_ms": round(kern_ms, 5), "kernel_ms_median": round(kern_med, 5),
+        "kernel": "rx_parse_kernel<G=4,ragged>",
+        "roofline": roofline(alg, kern_ms, load_traffic("config2")),
+        "alg_bytes_per_launch": alg,
+        "cpu_baseline": None,
+    }
+    line["roofline"]["note"] = ("achieved = (frame bytes + 6 B metadata + 32 B record) per launch / HIP-event "
+                                "kernel time; peak = HBM3E spec")
+
+    if d.world == 1 and not args.no_secondary:
+        sec = {}
+        # cache-resident variant of the headline (one batch, 102 MB < 256 MB Infinity Cache)
+        w1, k1, _ = time_kernel(ragged_launcher(batches[:1], out, netif, 64), args.steps, args.warmup, d)
+        sec["config2_mall_resident"] = {"mpps": round(n * args.steps / w1 / 1e6, 1), "kernel_ms": round(k1, 5),
+                                        "roofline": roofline(alg, k1)}
+        del batches
+        torch.cuda.empty_cache()
+        for name, kw, hint, strided_len, flags in [
+            ("1500B_udp_1M", dict(length=1500), 1500, 0, 1),
+            ("config3_imix_16M", dict(size_mode=1, proto_mode=3), 1500, 0, 1),
+            ("config5_jumbo_9000B_tcp_4M_ext", dict(length=9000, proto_mode=1, strided=True), 0, 9000, 3),
+        ]:
+            nn = (16 << 20) if "imix" in name else ((4 << 20) if "jumbo" in name else n)
+            rot = 2 if nn * (kw.get("length", 352)) < (1 << 31) else 1
+            log(f"[secondary] {name}: {rot} x {nn} frames")
+            bs = make_batches(dev, netif, n=nn, rotate=rot, rank=0, **kw)
+            o2 = torch.empty((nn, RESULT_BYTES), dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            steps = max(5, args.steps // 5)
+            launch = (strided_launcher(bs, o2, netif, strided_len, flags) if strided_len
+                      else ragged_launcher(bs, o2, netif, hint, flags))
+            w2, k2, _ = time_kernel(launch, steps, 2, d)
+            fb = frame_bytes(bs[0])
+            meta = 0 if strided_len else 6
+            a2 = fb + nn * (meta + RESULT_BYTES)
+            sec[name] = {"frames": nn, "mpps": round(nn * steps / w2 / 1e6, 1),
+                         "gbit_s": round(fb * steps * 8 / w2 / 1e9, 1), "kernel_ms": round(k2, 4),
+                         "roofline": roofline(a2, k2, load_traffic(name))}
+            del bs, o2
+            torch.cuda.empty_cache()
+        line["secondary"] = sec
+    if d.world == 1 and not args.no_cpu:  # rank 0 at N=1 only
+        bs = make_batches(dev, netif, n=n, rotate=1, rank=0)
+        torch.cuda.synchronize()
+        log("[cpu baseline] timing the oracle on the host")
+        line["cpu_baseline"] = cpu_baseline(bs[0], args.cpu_seconds)
+    d.close()
+    if d.rank == 0:
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+"""ctypes binding of libhalo_rx.so — the C ABI declared in include/halo_rx.h.
+
+The shared library is built in-tree (``__graft_entry__.build()`` or
+``python -m halo_amd.build``) and loaded from ``halo_amd/lib/``. There is no CPU
+fallback: if the library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libhalo_rx.so")
+
+# ---- constants mirrored from include/halo_rx.h ---------------------------------------
+HALO_OK = 0
+HALO_E_INVAL = -1
+HALO_E_NODEV = -2
+HALO_E_ARCH = -3
+HALO_E_HIP = -4
+HALO_E_NOMEM = -5
+HALO_E_RANGE = -6
+
+HALO_RX_CSUM_ENABLE = 0x1
+HALO_RX_JUMBO_EXT = 0x2
+
+STATUS_NAMES = (
+    "OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_PROTO", "IP_HDR_CKSUM",
+    "IP_TOTLEN_UNDERFLOW", "IP_TOTLEN_OVERRUN", "L4_LEN", "ICMP_TYPE", "ICMP_CODE", "L4_CKSUM",
+)
+STATUS = {name: code for code, name in enumerate(STATUS_NAMES)}
+HALO_RX_STATUS_COUNT = len(STATUS_NAMES)
+
+F_MAC_MATCH = 0x01
+F_IP_BCAST = 0x02
+F_DST_IS_OWN = 0x04
+
+ACTION_NAMES = (
+    "DROP_ETH", "IGNORE_MAC", "ARP", "IGNORE_TYPE", "DROP_IP", "BCAST_UDP", "DROP_BCAST_UDP",
+    "IGNORE_BCAST", "FORWARD", "LOCAL_ICMP", "LOCAL_UDP", "LOCAL_TCP", "DROP_L4",
+)
+ACTION = {name: code for code, name in enumerate(ACTION_NAMES)}
+HALO_RX_ACT_COUNT = len(ACTION_NAMES)
+
+# halo_rx_result_t (32 bytes, little-endian)
+RESULT_DTYPE = np.dtype([
+    ("status", "u1"), ("flags", "u1"), ("ethertype", "<u2"),
+    ("ip_proto", "u1"), ("l4_aux", "u1"), ("ip_total_len", "<u2"),
+    ("src_ip", "<u4"), ("dst_ip", "<u4"),
+    ("sport", "<u2"), ("dport", "<u2"),
+    ("payload_off", "<u2"), ("payload_len", "<u2"),
+    ("l4_seq", "<u4"), ("l4_ack", "<u4"),
+])
+assert RESULT_DTYPE.itemsize == 32
+
+
+class NetIf(ctypes.Structure):
+    """halo_rx_netif_t — engine.NetIfConfig's MacAddr / IpAddr / NatEnable."""
+
+    _fields_ = [
+        ("mac", ctypes.c_uint8 * 6),
+        ("pad", ctypes.c_uint8 * 2),
+        ("ip", ctypes.c_uint32),
+        ("nat_enable", ctypes.c_uint32),
+    ]
+
+    @classmethod
+    def make(cls, mac: str = "AA:AA:AA:AA:AA:AA", ip: str = "192.168.100.100", nat_enable: bool = False):
+        """Parse addresses like protocol.ParseMacAddr / ParseIpAddr (protocol/utils.go:57-82)."""
+        n = cls()
+        for i, part in enumerate(mac.split(":")[:6]):
+            n.mac[i] = int(part, 16)
+        a = [int(x) for x in ip.split(".")[:4]]
+        n.ip = (a[0] << 24) | (a[1] << 16) | (a[2] << 8) | a[3]  # IpAddrToU (utils.go:34-44)
+        n.nat_enable = 1 if nat_enable else 0
+        return n
+
+
+_u8p = ctypes.c_void_p
+_PROTOS = {
+    "halo_rx_version": (ctypes.c_char_p, []),
+    "halo_rx_init": (ctypes.c_int, [ctypes.c_int]),
+    "halo_rx_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "halo_rx_status_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "halo_rx_parse_batch_device": (ctypes.c_int, [
+        _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf), ctypes.c_uint32,
+        _u8p, _u8p, ctypes.c_void_p]),
+    "halo_rx_parse_strided_device": (ctypes.c_int, [
+        _u8p, ctypes.c_uint64, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+        ctypes.POINTER(NetIf), _u8p, _u8p, ctypes.c_void_p]),
+    "halo_rx_host_ctx_create": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    "halo_rx_host_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "halo_rx_parse_batch_host": (ctypes.c_int, [
+        ctypes.c_void_p, _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf),
+        _u8p, _u8p]),
+    "halo_rx_dispatch": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
+    "halo_synth_layout": (ctypes.c_int, [
+        ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+        ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint64)]),
+    "halo_synth_frames_device": (ctypes.c_int, [
+        ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, _u8p, _u8p, ctypes.c_uint64, _u8p,
+        ctypes.POINTER(NetIf), _u8p, ctypes.c_void_p]),
+}
+
+
+class HaloError(RuntimeError):
+    def __init__(self, fn: str, code: int):
+        super().__init__(f"{fn} failed: {code} ({strerror(code)})")
+        self.code = code
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP library first "
+            "(python -c 'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def strerror(code: int) -> str:
+    return lib.halo_rx_strerror(code).decode()
+
+
+def check(fn: str, code: int) -> None:
+    if code != HALO_OK:
+        raise HaloError(fn, code)
+
+
+def ptr(x) -> int | None:
+    """Device/host address of a torch tensor or numpy array (None for None)."""
+    if x is None:
+        return None
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return x.ctypes.data

@@ -1,0 +1,59 @@
+// halo_common.h — constants and helpers shared by the HIP kernels and the host side of
+// libhalo_rx.so. Device code is written for gfx950 (CDNA4) only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "halo_rx.h"
+
+namespace halo {
+
+// Reference limits (protocol/ethernet.go:31, protocol/ipv4.go:49, protocol/udp.go:22,
+// protocol/tcp.go:37, protocol/icmp.go:34) and the build-defined jumbo extension.
+constexpr uint32_t kEthMin = 42, kEthMax = 1514, kIpMax = 1500, kL4Max = 1480;
+constexpr uint32_t kEthMaxJumbo = 9014, kIpMaxJumbo = 9000, kL4MaxJumbo = 8980;
+
+// EtherTypes (protocol/ethernet.go:16-22), IP protocol ids (protocol/ipv4.go:27-32),
+// ICMP types (protocol/icmp.go:25-30).
+constexpr uint16_t kEthIeee8023 = 0x05DC, kEthIpv4 = 0x0800, kEthArp = 0x0806,
+                   kEthIpv6 = 0x86DD, kEthUnknown = 0xFFFF;
+constexpr uint8_t kIpIcmp = 0x01, kIpTcp = 0x06, kIpUdp = 0x11, kIpUnknown = 0xFF;
+constexpr uint8_t kIcmpRequest = 0x08, kIcmpReply = 0x00, kIcmpTtl = 0x0B;
+
+// Kernel parameter block (passed by value; one per launch).
+struct RxParams {
+    const uint8_t* bytes;
+    const uint32_t* offsets_dw;  // ragged layout (LAYOUT 0)
+    const uint16_t* lens;        // per-frame lengths (LAYOUT 0, 1)
+    uint64_t stride;             // strided layouts (LAYOUT 1, 2)
+    uint32_t len;                // uniform length (LAYOUT 2)
+    uint32_t n;
+    uint32_t flags;
+    uint32_t mac_lo;  // own MAC bytes 0..3, little-endian packed
+    uint32_t mac_hi;  // own MAC bytes 4..5
+    uint32_t own_ip;  // IpAddrToU(NetIf.IpAddr)
+    halo_rx_result_t* out;
+    uint32_t* hist;
+};
+
+// splitmix64 finaliser — the synthetic-traffic generator's only randomness source.
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ inline uint64_t synth_key(uint64_t seed, uint64_t index) {
+    return mix64(seed ^ mix64(index));
+}
+__host__ __device__ inline uint64_t synth_draw(uint64_t key, uint64_t slot) {
+    return mix64(key + slot * 0xD6E8FEB86659FD93ull);
+}
+enum SynthSlot : uint32_t {
+    kSlotSize = 1, kSlotProto = 2, kSlotMutate = 3, kSlotMutPos = 4, kSlotMac = 5,
+    kSlotIp = 6, kSlotPorts = 7, kSlotSeq = 8, kSlotWin = 9, kSlotPayload = 64
+};
+
+int check_device();  // 0 if the current device is gfx950, else HALO_E_*
+
+}  // namespace halo

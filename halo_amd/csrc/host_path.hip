@@ -1,0 +1,251 @@
+// host_path.hip — device selection, the host-memory batch path (SURVEY.md §8f row f1:
+// drain host frames into pinned chunks, double-buffered H2D -> kernel -> D2H) and the
+// reference engine's per-frame decision over the kernel's records.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <atomic>
+#include <new>
+
+#include "halo_common.h"
+
+namespace halo {
+
+int check_device() {
+    static std::atomic<int> verdict[64];  // 0 = unknown, 1 = gfx950, <0 = HALO_E_*
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return HALO_E_NODEV;
+    if (dev < 64) {
+        const int v = verdict[dev].load(std::memory_order_relaxed);
+        if (v == 1) return HALO_OK;
+        if (v < 0) return v;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return HALO_E_NODEV;
+    const int v = strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : HALO_E_ARCH;
+    if (dev < 64) verdict[dev].store(v, std::memory_order_relaxed);
+    return v == 1 ? HALO_OK : v;
+}
+
+}  // namespace halo
+
+extern "C" HALO_API const char* halo_rx_version(void) { return "halo_rx 0.1 (gfx950)"; }
+
+extern "C" HALO_API int halo_rx_init(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return HALO_E_NODEV;
+    if (device < 0 || device >= count) return HALO_E_NODEV;
+    if (hipSetDevice(device) != hipSuccess) return HALO_E_NODEV;
+    return halo::check_device();
+}
+
+extern "C" HALO_API const char* halo_rx_strerror(int code) {
+    switch (code) {
+        case HALO_OK: return "ok";
+        case HALO_E_INVAL: return "invalid argument";
+        case HALO_E_NODEV: return "no HIP device";
+        case HALO_E_ARCH: return "device is not gfx950";
+        case HALO_E_HIP: return "HIP runtime error";
+        case HALO_E_NOMEM: return "out of memory";
+        case HALO_E_RANGE: return "batch exceeds addressing range";
+        default: return "unknown error";
+    }
+}
+
+extern "C" HALO_API const char* halo_rx_status_name(int status) {
+    static const char* const names[HALO_RX_STATUS_COUNT] = {
+        "OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_PROTO", "IP_HDR_CKSUM",
+        "IP_TOTLEN_UNDERFLOW", "IP_TOTLEN_OVERRUN", "L4_LEN", "ICMP_TYPE", "ICMP_CODE", "L4_CKSUM"};
+    return (status >= 0 && status < HALO_RX_STATUS_COUNT) ? names[status] : "UNKNOWN";
+}
+
+// ---- engine decision (engine/ethernet_engine.go:13-31, engine/ipv4_engine.go:18-47) -----
+extern "C" HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32_t n, const halo_rx_netif_t* netif,
+                                         uint8_t* actions, uint32_t* action_hist) {
+    if (n && (!results || !netif || !actions)) return HALO_E_INVAL;
+    for (uint32_t i = 0; i < n; ++i) {
+        const halo_rx_result_t& r = results[i];
+        uint8_t a;
+        if (r.status == HALO_RX_ETH_LEN || r.status == HALO_RX_ETH_TYPE) {
+            a = HALO_RX_ACT_DROP_ETH;                        // ethernet_engine.go:18-21
+        } else if (!(r.flags & HALO_RX_F_MAC_MATCH)) {
+            a = HALO_RX_ACT_IGNORE_MAC;                      // ethernet_engine.go:22
+        } else if (r.ethertype == halo::kEthArp) {
+            a = HALO_RX_ACT_ARP;                             // ethernet_engine.go:24-25
+        } else if (r.ethertype != halo::kEthIpv4) {
+            a = HALO_RX_ACT_IGNORE_TYPE;                     // ethernet_engine.go:28
+        } else if (r.status >= HALO_RX_IP_LEN && r.status <= HALO_RX_IP_TOTLEN_OVERRUN) {
+            a = HALO_RX_ACT_DROP_IP;                         // ipv4_engine.go:19-23
+        } else if (r.flags & HALO_RX_F_IP_BCAST) {           // ipv4_engine.go:24-30
+            if (r.ip_proto == halo::kIpUdp)
+                a = r.status == HALO_RX_OK ? HALO_RX_ACT_BCAST_UDP : HALO_RX_ACT_DROP_BCAST_UDP;
+            else
+                a = HALO_RX_ACT_IGNORE_BCAST;
+        } else if (!(r.flags & HALO_RX_F_DST_IS_OWN) || netif->nat_enable) {
+            a = HALO_RX_ACT_FORWARD;                         // ipv4_engine.go:31-37
+        } else if (r.status != HALO_RX_OK) {
+            a = HALO_RX_ACT_DROP_L4;                         // {udp,tcp,icmp}_engine.go Rx*
+        } else {
+            a = r.ip_proto == halo::kIpIcmp ? HALO_RX_ACT_LOCAL_ICMP
+              : r.ip_proto == halo::kIpUdp  ? HALO_RX_ACT_LOCAL_UDP
+                                            : HALO_RX_ACT_LOCAL_TCP;  // ipv4_engine.go:38-46
+        }
+        actions[i] = a;
+        if (action_hist) ++action_hist[a];
+    }
+    return HALO_OK;
+}
+
+// ---- host-memory batch path ---------------------------------------------------------------
+struct halo_rx_host_ctx {
+    int device;
+    uint32_t chunk_frames;
+    uint64_t chunk_bytes;
+    struct Slot {
+        hipStream_t stream = nullptr;
+        uint8_t* h_bytes = nullptr;   // pinned staging
+        uint32_t* h_off = nullptr;
+        uint16_t* h_len = nullptr;
+        halo_rx_result_t* h_res = nullptr;
+        uint8_t* d_bytes = nullptr;
+        uint32_t* d_off = nullptr;
+        uint16_t* d_len = nullptr;
+        halo_rx_result_t* d_res = nullptr;
+        uint32_t* d_hist = nullptr;
+        // chunk currently in flight in this slot
+        bool busy = false;
+        uint64_t first = 0;
+        uint32_t count = 0;
+    } slot[2];
+};
+
+namespace {
+void free_ctx(halo_rx_host_ctx* c) {
+    for (auto& s : c->slot) {
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        if (s.h_bytes) (void)hipHostFree(s.h_bytes);
+        if (s.h_off) (void)hipHostFree(s.h_off);
+        if (s.h_len) (void)hipHostFree(s.h_len);
+        if (s.h_res) (void)hipHostFree(s.h_res);
+        if (s.d_bytes) (void)hipFree(s.d_bytes);
+        if (s.d_off) (void)hipFree(s.d_off);
+        if (s.d_len) (void)hipFree(s.d_len);
+        if (s.d_res) (void)hipFree(s.d_res);
+        if (s.d_hist) (void)hipFree(s.d_hist);
+    }
+    delete c;
+}
+}  // namespace
+
+extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frames, uint64_t chunk_bytes,
+                                                halo_rx_host_ctx_t** out) {
+    if (!out) return HALO_E_INVAL;
+    *out = nullptr;
+    int rc = halo_rx_init(device);
+    if (rc) return rc;
+    if (chunk_frames == 0) chunk_frames = 1u << 18;
+    if (chunk_bytes == 0) chunk_bytes = 64ull << 20;
+    if (chunk_bytes < 65536) return HALO_E_INVAL;
+    auto* c = new (std::nothrow) halo_rx_host_ctx;
+    if (!c) return HALO_E_NOMEM;
+    c->device = device;
+    c->chunk_frames = chunk_frames;
+    c->chunk_bytes = chunk_bytes;
+    bool ok = true;
+    for (auto& s : c->slot) {
+        ok = ok && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess;
+        ok = ok && hipHostMalloc((void**)&s.h_bytes, chunk_bytes, hipHostMallocDefault) == hipSuccess;
+        ok = ok && hipHostMalloc((void**)&s.h_off, 4ull * chunk_frames, hipHostMallocDefault) == hipSuccess;
+        ok = ok && hipHostMalloc((void**)&s.h_len, 2ull * chunk_frames, hipHostMallocDefault) == hipSuccess;
+        ok = ok && hipHostMalloc((void**)&s.h_res, sizeof(halo_rx_result_t) * chunk_frames,
+                                 hipHostMallocDefault) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_bytes, chunk_bytes) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_off, 4ull * chunk_frames) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_len, 2ull * chunk_frames) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_res, sizeof(halo_rx_result_t) * chunk_frames) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_hist, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
+        ok = ok && hipMemset(s.d_hist, 0, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
+    }
+    if (!ok) {
+        free_ctx(c);
+        return HALO_E_NOMEM;
+    }
+    *out = c;
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_host_ctx_destroy(halo_rx_host_ctx_t* ctx) {
+    if (!ctx) return HALO_E_INVAL;
+    (void)hipSetDevice(ctx->device);
+    for (auto& s : ctx->slot)
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+    free_ctx(ctx);
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* bytes,
+                                                 const uint64_t* offsets, const uint16_t* lens, uint32_t n,
+                                                 uint32_t flags, const halo_rx_netif_t* netif,
+                                                 halo_rx_result_t* out, uint32_t* status_hist) {
+    if (!ctx || !netif) return HALO_E_INVAL;
+    if (n == 0) return HALO_OK;
+    if (!bytes || !offsets || !lens || !out) return HALO_E_INVAL;
+    if (hipSetDevice(ctx->device) != hipSuccess) return HALO_E_NODEV;
+    const uint32_t cap = (flags & HALO_RX_JUMBO_EXT) ? halo::kEthMaxJumbo : halo::kEthMax;
+    int rc = HALO_OK;
+    auto drain = [&](halo_rx_host_ctx::Slot& s) -> int {
+        if (!s.busy) return HALO_OK;
+        s.busy = false;
+        if (hipStreamSynchronize(s.stream) != hipSuccess) return HALO_E_HIP;
+        memcpy(out + s.first, s.h_res, sizeof(halo_rx_result_t) * s.count);
+        return HALO_OK;
+    };
+    uint64_t next = 0;
+    uint32_t k = 0;
+    while (next < n && rc == HALO_OK) {
+        auto& s = ctx->slot[k & 1];
+        if ((rc = drain(s))) break;
+        // pack frames [next, ...) into the pinned slot, 4-byte aligned (ring-record style)
+        uint64_t used = 0;
+        uint32_t cnt = 0;
+        while (next + cnt < n && cnt < ctx->chunk_frames) {
+            const uint32_t L = lens[next + cnt];
+            const uint64_t need = L <= cap ? ((L + 3u) & ~3u) : 0;  // over-long frames are never read
+            if (used + need > ctx->chunk_bytes) break;
+            if (need) memcpy(s.h_bytes + used, bytes + offsets[next + cnt], L);
+            s.h_off[cnt] = (uint32_t)(used >> 2);
+            s.h_len[cnt] = (uint16_t)L;
+            used += need;
+            ++cnt;
+        }
+        hipError_t e = hipSuccess;
+        if (used) e = hipMemcpyAsync(s.d_bytes, s.h_bytes, used, hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, 4ull * cnt, hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(s.d_len, s.h_len, 2ull * cnt, hipMemcpyHostToDevice, s.stream);
+        if (e != hipSuccess) { rc = HALO_E_HIP; break; }
+        rc = halo_rx_parse_batch_device(s.d_bytes, s.d_off, s.d_len, cnt, flags, netif, 0, s.d_res,
+                                        status_hist ? s.d_hist : nullptr, s.stream);
+        if (rc) break;
+        if (hipMemcpyAsync(s.h_res, s.d_res, sizeof(halo_rx_result_t) * cnt, hipMemcpyDeviceToHost, s.stream) !=
+            hipSuccess) { rc = HALO_E_HIP; break; }
+        s.busy = true;
+        s.first = next;
+        s.count = cnt;
+        next += cnt;
+        ++k;
+    }
+    for (auto& s : ctx->slot) {
+        int r2 = drain(s);
+        if (!rc) rc = r2;
+    }
+    if (rc == HALO_OK && status_hist) {
+        for (auto& s : ctx->slot) {
+            uint32_t h[HALO_RX_STATUS_COUNT];
+            if (hipMemcpy(h, s.d_hist, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemset(s.d_hist, 0, sizeof h) != hipSuccess)
+                return HALO_E_HIP;
+            for (int j = 0; j < HALO_RX_STATUS_COUNT; ++j) status_hist[j] += h[j];
+        }
+    }
+    return rc;
+}

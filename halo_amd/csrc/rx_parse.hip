@@ -1,0 +1,384 @@
+// rx_parse.hip — the hot path: batched Ethernet -> IPv4 -> UDP/TCP/ICMP parse and
+// 16-bit one's-complement Internet checksum verification on gfx950 (MI355X).
+//
+// Restates, per frame and bit-exactly:
+//   protocol.GetCheckSum        protocol/utils.go:11-31
+//   protocol.ParseEthFrm        protocol/ethernet.go:29-55
+//   protocol.ParseIpv4Pkt       protocol/ipv4.go:48-86
+//   protocol.ParseUdpPkt        protocol/udp.go:21-49
+//   protocol.ParseTcpPkt        protocol/tcp.go:36-70
+//   protocol.ParseIcmpPkt       protocol/icmp.go:33-63
+//   protocol.NatGetSrcDstPort   protocol/ipv4.go:229-246
+//   NetIf.RxEthernet / RxIpv4 branch inputs  engine/ethernet_engine.go:22, ipv4_engine.go:24,31
+//
+// Execution shape (DESIGN.md "Kernels"): a group of G lanes of one 64-wide wavefront owns a
+// frame; 64/G frames per wave. Lane j of the group loads dwords [4j, 4j+4) + k*4G of the frame
+// with one 16-byte load per step, so a wave-instruction covers 64/G frames' consecutive bytes
+// (coalesced). The 48-byte header (dwords 0..11) sits in group lanes 0..2 after the first load
+// and is broadcast to the group with 12 ds_bpermute shuffles; every lane then runs the header
+// checks redundantly (no divergence, no second broadcast). Only the L4 segment sum needs a
+// cross-lane reduction (log2 G xor-shuffles).
+//
+// Checksum arithmetic (DESIGN.md "Checksum in the little-endian domain"): the frame is summed
+// as little-endian dwords. A one's-complement sum of byte-swapped 16-bit words is the byte
+// swap of the sum (RFC 1071 §2B); swapping maps 0xFFFF to itself, and 2^16 == 1 (mod 0xFFFF),
+// so "GetCheckSum(region) == 0" <=> fold16(sum of the LE dwords of the region) == 0xFFFF.
+// Every region on the path starts at an even frame offset (14, 26, 34), so region edges fall
+// on half-dwords and an odd trailing byte lands in the low byte of its half, which is the
+// HIGH byte of its big-endian word: exactly protocol/utils.go:21-24.
+#include <hip/hip_runtime.h>
+
+#include "halo_common.h"
+
+namespace halo {
+namespace {
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
+
+// fold a 32-bit sum to 16 bits, as protocol/utils.go:26-28 (two steps suffice for 32 bits)
+__device__ __forceinline__ uint32_t fold16(uint32_t s) {
+    s = (s & 0xFFFFu) + (s >> 16);
+    return (s & 0xFFFFu) + (s >> 16);
+}
+// fold a 64-bit sum to < 2^18 keeping its value mod 0xFFFF and its zero-ness
+__device__ __forceinline__ uint32_t fold64(uint64_t s) {
+    uint64_t t = (s & 0xFFFFFFFFull) + (s >> 32);
+    return (uint32_t)((t & 0xFFFFull) + (t >> 16));
+}
+__device__ __forceinline__ uint32_t hsum(uint32_t w) { return (w & 0xFFFFu) + (w >> 16); }
+
+// Load dwords [d0, d0+4) of a frame that has ndw readable dwords; zero beyond. Never touches a
+// dword past the one holding the frame's last byte (halo_rx.h layout contract).
+__device__ __forceinline__ void load4(const uint8_t* frame, uint32_t d0, uint32_t ndw, uint32_t (&w)[4]) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(frame) + d0;
+    if (d0 + 4 <= ndw) {
+        uint4 v;
+        __builtin_memcpy(&v, p, 16);  // 4-byte aligned 16-byte load: global_load_dwordx4
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (d0 + j < ndw) ? p[j] : 0u;
+    }
+}
+
+// Accumulate the L4-segment bytes [34, seg_end) held in dwords [d0, d0+4).
+__device__ __forceinline__ void acc_segment(const uint32_t (&w)[4], uint32_t d0, uint32_t seg_end, uint64_t& c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t d = d0 + j;
+        const int32_t rel = (int32_t)seg_end - (int32_t)(4u * d);  // segment bytes left in this dword
+        uint32_t keep = rel >= 4 ? 0xFFFFFFFFu : (rel <= 0 ? 0u : ((1u << (rel * 8)) - 1u));
+        keep &= d >= 9 ? 0xFFFFFFFFu : (d == 8 ? 0xFFFF0000u : 0u);  // segment starts at byte 34
+        c += (uint64_t)(w[j] & keep);
+    }
+}
+
+struct Verdict {
+    uint32_t status, flags, ethertype, ip_proto, ip_total_len, src_ip, dst_ip, sport, dport;
+    uint32_t pay_off, pay_len, l4_aux, l4_seq, l4_ack;
+    uint32_t seg_end;   // end of the L4 segment whose sum is needed (0: none)
+    uint32_t l4_extra;  // pseudo-header + header-field part of the L4 sum, LE domain
+    bool check_l4;      // L4 checksum decides the verdict after the reduction
+};
+
+#define HB(b) ((h[(b) >> 2] >> (((b)&3) * 8)) & 0xFFu)
+
+// Header checks, in reference order, up to (not including) the L4 checksum.
+__device__ __forceinline__ Verdict parse_header(const uint32_t (&h)[12], uint32_t L, bool present,
+                                                const RxParams& p) {
+    Verdict v;
+    v.status = HALO_RX_OK; v.flags = 0; v.ethertype = kEthUnknown; v.ip_proto = kIpUnknown;
+    v.ip_total_len = 0; v.src_ip = 0; v.dst_ip = 0; v.sport = 0; v.dport = 0;
+    v.pay_off = 0; v.pay_len = 0; v.l4_aux = 0; v.l4_seq = 0; v.l4_ack = 0;
+    v.seg_end = 0; v.l4_extra = 0; v.check_l4 = false;
+    const bool jumbo = (p.flags & HALO_RX_JUMBO_EXT) != 0;
+    const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
+    const uint32_t eth_max = jumbo ? kEthMaxJumbo : kEthMax;
+    const uint32_t ip_max = jumbo ? kIpMaxJumbo : kIpMax;
+    const uint32_t l4_max = jumbo ? kL4MaxJumbo : kL4Max;
+
+    // ---- ParseEthFrm (protocol/ethernet.go:29-55)
+    if (!present || L < kEthMin || L > eth_max) { v.status = HALO_RX_ETH_LEN; return v; }
+    const uint32_t et = bswap16(h[3] & 0xFFFFu);
+    if (et != kEthIeee8023 && et != kEthIpv4 && et != kEthArp && et != kEthIpv6) {
+        v.status = HALO_RX_ETH_TYPE; return v;
+    }
+    v.ethertype = et;
+    v.pay_off = 14; v.pay_len = L - 14;
+    // RxEthernet's filter (engine/ethernet_engine.go:22)
+    const uint32_t dm_lo = h[0], dm_hi = h[1] & 0xFFFFu;
+    if ((dm_lo == p.mac_lo && dm_hi == p.mac_hi) || (dm_lo == 0xFFFFFFFFu && dm_hi == 0xFFFFu))
+        v.flags |= HALO_RX_F_MAC_MATCH;
+    if (et != kEthIpv4) return v;
+
+    // ---- ParseIpv4Pkt (protocol/ipv4.go:48-86) on pkt = frm[14:L]
+    const uint32_t iplen = L - 14;
+    if (iplen < 20 || iplen > ip_max) { v.status = HALO_RX_IP_LEN; return v; }
+    if (HB(14) != 0x45u) { v.status = HALO_RX_IP_VER; return v; }
+    if ((HB(20) != 0x40u && HB(20) != 0x00u) || HB(21) != 0x00u) { v.status = HALO_RX_IP_FRAG; return v; }
+    const uint32_t proto = HB(23);
+    if (proto != kIpIcmp && proto != kIpTcp && proto != kIpUdp) { v.status = HALO_RX_IP_PROTO; return v; }
+    // pseudo-header src+dst (frame bytes 26..33), LE domain
+    const uint32_t sum_b = (h[6] >> 16) + hsum(h[7]) + (h[8] & 0xFFFFu);
+    if (csum) {
+        const uint32_t sum_a = (h[3] >> 16) + hsum(h[4]) + hsum(h[5]) + (h[6] & 0xFFFFu);
+        if (fold16(sum_a + sum_b) != 0xFFFFu) { v.status = HALO_RX_IP_HDR_CKSUM; return v; }
+    }
+    const uint32_t total_len = bswap16(h[4] & 0xFFFFu);
+    // pkt[20:totalLen] (protocol/ipv4.go:84): Go panics below 20 and reads stale bytes or
+    // panics past len(pkt); both are reported as build-defined statuses.
+    if (total_len < 20) { v.status = HALO_RX_IP_TOTLEN_UNDERFLOW; return v; }
+    if (total_len > iplen) { v.status = HALO_RX_IP_TOTLEN_OVERRUN; return v; }
+    v.ip_proto = proto;
+    v.ip_total_len = total_len;
+    v.src_ip = (HB(26) << 24) | (HB(27) << 16) | (HB(28) << 8) | HB(29);
+    v.dst_ip = (HB(30) << 24) | (HB(31) << 16) | (HB(32) << 8) | HB(33);
+    if (HB(33) == 255u) v.flags |= HALO_RX_F_IP_BCAST;
+    if (v.dst_ip == p.own_ip) v.flags |= HALO_RX_F_DST_IS_OWN;
+    // NatGetSrcDstPort (protocol/ipv4.go:229-246) on the untrimmed packet (len >= 26 here)
+    if (proto == kIpIcmp) {
+        v.sport = v.dport = (HB(38) << 8) | HB(39);
+    } else {
+        v.sport = (HB(34) << 8) | HB(35);
+        v.dport = (HB(36) << 8) | HB(37);
+    }
+    v.pay_off = 34; v.pay_len = total_len - 20;
+
+    // ---- L4 pre-checksum checks on pkt = ipPayload (len = totalLen - 20)
+    const uint32_t l4len = total_len - 20;
+    const uint32_t seg_end = total_len + 14;
+    if (proto == kIpUdp) {        // protocol/udp.go:21-49
+        if (l4len < 8 || l4len > l4_max) { v.status = HALO_RX_L4_LEN; return v; }
+        if (csum) {  // pseudo length = the UDP header's own length field (udp.go:30,38)
+            v.check_l4 = true; v.seg_end = seg_end;
+            v.l4_extra = sum_b + 0x1100u + (h[9] >> 16);
+        }
+    } else if (proto == kIpTcp) { // protocol/tcp.go:36-70
+        if (l4len < 20 || l4len > l4_max) { v.status = HALO_RX_L4_LEN; return v; }
+        if (csum) {  // pseudo length = len(pkt) (tcp.go:54-59)
+            v.check_l4 = true; v.seg_end = seg_end;
+            v.l4_extra = sum_b + 0x0600u + bswap16(l4len);
+        }
+    } else {                      // ICMP, protocol/icmp.go:33-63: checksum ALWAYS verified
+        if (l4len < 8 || l4len > l4_max) { v.status = HALO_RX_L4_LEN; return v; }
+        const uint32_t type = HB(34);
+        if (type != kIcmpRequest && type != kIcmpReply && type != kIcmpTtl) { v.status = HALO_RX_ICMP_TYPE; return v; }
+        if (HB(35) != 0u) { v.status = HALO_RX_ICMP_CODE; return v; }
+        v.check_l4 = true; v.seg_end = seg_end; v.l4_extra = 0;
+    }
+    return v;
+}
+
+// L4 outputs once the whole chain succeeded.
+__device__ __forceinline__ void finish_l4(const uint32_t (&h)[12], Verdict& v) {
+    const uint32_t l4len = v.ip_total_len - 20;
+    if (v.ip_proto == kIpUdp) {
+        v.pay_off = 42; v.pay_len = l4len - 8;                          // udp.go:47
+    } else if (v.ip_proto == kIpTcp) {
+        v.l4_aux = HB(47);                                             // tcp.go:50
+        v.l4_seq = (HB(38) << 24) | (HB(39) << 16) | (HB(40) << 8) | HB(41);
+        v.l4_ack = (HB(42) << 24) | (HB(43) << 16) | (HB(44) << 8) | HB(45);
+        const uint32_t hl = HB(46) >> 4;                               // tcp.go:49 (words used as bytes)
+        v.pay_off = 34 + hl; v.pay_len = l4len - hl;                   // tcp.go:68
+    } else {
+        v.l4_aux = HB(34);                                             // icmp.go:38
+        v.l4_seq = (HB(38) << 24) | (HB(39) << 16) | (HB(40) << 8) | HB(41);
+        v.pay_off = 42; v.pay_len = l4len - 8;                          // icmp.go:62
+    }
+}
+#undef HB
+
+template <int LAYOUT>
+__device__ __forceinline__ void frame_at(const RxParams& p, uint64_t i, const uint8_t*& frame, uint32_t& L) {
+    if constexpr (LAYOUT == 0) {
+        frame = p.bytes + ((uint64_t)p.offsets_dw[i] << 2);
+        L = p.lens[i];
+    } else if constexpr (LAYOUT == 1) {
+        frame = p.bytes + i * p.stride;
+        L = p.lens[i];
+    } else {
+        frame = p.bytes + i * p.stride;
+        L = p.len;
+    }
+}
+
+// G lanes per frame (G in {4,8,16,32,64}); LAYOUT 0 ragged, 1 strided+lens, 2 strided uniform.
+template <int G, int LAYOUT>
+__global__ void __launch_bounds__(256) rx_parse_kernel(const RxParams p) {
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
+    constexpr uint32_t FPW = 64 / G;  // frames per wave
+    constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
+    __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
+    if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp_base = lane & ~(uint32_t)(G - 1);
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const bool jumbo = (p.flags & HALO_RX_JUMBO_EXT) != 0;
+    const uint32_t eth_max = jumbo ? kEthMaxJumbo : kEthMax;
+    uint32_t ok_count = 0;
+
+    for (uint64_t base = wave * FPW; base < p.n; base += nwaves * FPW) {
+        const uint64_t i = base + lane / G;
+        const bool present = i < p.n;
+        const uint8_t* frame = p.bytes;
+        uint32_t L = 0;
+        if (present) frame_at<LAYOUT>(p, i, frame, L);
+        // frames failing the length check are never read (ParseEthFrm looks at no byte)
+        const uint32_t ndw = (present && L >= kEthMin && L <= eth_max) ? (L + 3) >> 2 : 0;
+
+        uint32_t w[4];
+        load4(frame, gl * 4, ndw, w);
+
+        uint32_t h[12];
+#pragma unroll
+        for (int d = 0; d < 12; ++d) h[d] = __shfl(w[d & 3], (int)(grp_base + (d >> 2)), 64);
+
+        Verdict v = parse_header(h, L, present, p);
+
+        // L4 segment sum over [34, seg_end): first step from registers, then the rest
+        uint64_t c = 0;
+        if (v.seg_end) {
+            acc_segment(w, gl * 4, v.seg_end, c);
+            const uint32_t seg_dw = (v.seg_end + 3) >> 2;
+            for (uint32_t d0 = STEP + gl * 4; d0 < seg_dw; d0 += STEP) {
+                uint32_t x[4];
+                load4(frame, d0, seg_dw, x);
+                acc_segment(x, d0, v.seg_end, c);
+            }
+        }
+        uint32_t c32 = fold64(c);
+#pragma unroll
+        for (int m = 1; m < G; m <<= 1) c32 += __shfl_xor(c32, m, 64);
+
+        if (v.status == HALO_RX_OK && v.check_l4 && fold16(c32 + v.l4_extra) != 0xFFFFu)
+            v.status = HALO_RX_L4_CKSUM;
+        if (v.status == HALO_RX_OK && v.ip_proto != kIpUnknown) finish_l4(h, v);
+
+        if (present && gl < 2) {
+            uint4 r;
+            if (gl == 0) {
+                r.x = v.status | (v.flags << 8) | (v.ethertype << 16);
+                r.y = v.ip_proto | (v.l4_aux << 8) | (v.ip_total_len << 16);
+                r.z = v.src_ip;
+                r.w = v.dst_ip;
+            } else {
+                r.x = v.sport | (v.dport << 16);
+                r.y = v.pay_off | (v.pay_len << 16);
+                r.z = v.l4_seq;
+                r.w = v.l4_ack;
+            }
+            reinterpret_cast<uint4*>(p.out + i)[gl] = r;
+            if (gl == 0) {
+                if (v.status == HALO_RX_OK) ++ok_count;
+                else if (p.hist) atomicAdd(&s_hist[v.status], 1u);
+            }
+        }
+    }
+    if (p.hist) {
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) ok_count += __shfl_xor(ok_count, m, 64);
+        if (lane == 0 && ok_count) atomicAdd(&s_hist[HALO_RX_OK], ok_count);
+        __syncthreads();
+        if (threadIdx.x < HALO_RX_STATUS_COUNT && s_hist[threadIdx.x])
+            atomicAdd(&p.hist[threadIdx.x], s_hist[threadIdx.x]);
+    }
+}
+
+template <int G>
+hipError_t launch_g(const RxParams& p, int layout, hipStream_t s) {
+    constexpr uint32_t FPW = 64 / G;
+    const uint64_t waves = (p.n + FPW - 1) / FPW;
+    uint64_t blocks = (waves + 3) / 4;
+    const uint64_t kMaxBlocks = 256ull * 8 * 8;  // 256 CUs x 8 resident blocks x 8 rounds
+    if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+    const dim3 grid((uint32_t)blocks), block(256);
+    switch (layout) {
+        case 0: hipLaunchKernelGGL((rx_parse_kernel<G, 0>), grid, block, 0, s, p); break;
+        case 1: hipLaunchKernelGGL((rx_parse_kernel<G, 1>), grid, block, 0, s, p); break;
+        default: hipLaunchKernelGGL((rx_parse_kernel<G, 2>), grid, block, 0, s, p); break;
+    }
+    return hipGetLastError();
+}
+
+// lanes per frame from the longest frame: one 16-byte load per lane covers the frame
+int pick_group(uint32_t max_len) {
+    if (max_len == 0) return 16;
+    if (max_len <= 64) return 4;
+    if (max_len <= 128) return 8;
+    if (max_len <= 256) return 16;
+    if (max_len <= 512) return 32;
+    return 64;
+}
+
+int launch_parse(const RxParams& p, int layout, uint32_t max_len, hipStream_t s) {
+    hipError_t e;
+    switch (pick_group(max_len)) {
+        case 4: e = launch_g<4>(p, layout, s); break;
+        case 8: e = launch_g<8>(p, layout, s); break;
+        case 16: e = launch_g<16>(p, layout, s); break;
+        case 32: e = launch_g<32>(p, layout, s); break;
+        default: e = launch_g<64>(p, layout, s); break;
+    }
+    return e == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+
+int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
+                halo_rx_result_t* d_out, uint32_t* d_hist) {
+    if (!netif || !d_out) return HALO_E_INVAL;
+    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT)) return HALO_E_INVAL;
+    if (reinterpret_cast<uintptr_t>(d_out) & 15u) return HALO_E_INVAL;
+    p.n = n;
+    p.flags = flags;
+    p.mac_lo = (uint32_t)netif->mac[0] | ((uint32_t)netif->mac[1] << 8) | ((uint32_t)netif->mac[2] << 16) |
+               ((uint32_t)netif->mac[3] << 24);
+    p.mac_hi = (uint32_t)netif->mac[4] | ((uint32_t)netif->mac[5] << 8);
+    p.own_ip = netif->ip;
+    p.out = d_out;
+    p.hist = d_hist;
+    return HALO_OK;
+}
+
+}  // namespace
+}  // namespace halo
+
+extern "C" HALO_API int halo_rx_parse_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                                   const uint16_t* d_lens, uint32_t n, uint32_t flags,
+                                                   const halo_rx_netif_t* netif, uint32_t max_len_hint,
+                                                   halo_rx_result_t* d_out, uint32_t* d_status_hist,
+                                                   halo_stream_t stream) {
+    halo::RxParams p{};
+    int rc = halo::fill_common(p, n, flags, netif, d_out, d_status_hist);
+    if (rc) return rc;
+    if (n == 0) return HALO_OK;
+    if (!d_bytes || !d_offsets_dw || !d_lens) return HALO_E_INVAL;
+    if ((rc = halo::check_device())) return rc;
+    p.bytes = d_bytes;
+    p.offsets_dw = d_offsets_dw;
+    p.lens = d_lens;
+    return halo::launch_parse(p, 0, max_len_hint, static_cast<hipStream_t>(stream));
+}
+
+extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uint64_t stride,
+                                                     const uint16_t* d_lens, uint32_t len, uint32_t n,
+                                                     uint32_t flags, const halo_rx_netif_t* netif,
+                                                     halo_rx_result_t* d_out, uint32_t* d_status_hist,
+                                                     halo_stream_t stream) {
+    halo::RxParams p{};
+    int rc = halo::fill_common(p, n, flags, netif, d_out, d_status_hist);
+    if (rc) return rc;
+    if (n == 0) return HALO_OK;
+    if (!d_bytes || (stride & 3u) || (n > 1 && stride == 0)) return HALO_E_INVAL;
+    if (!d_lens && n > 1 && len > stride) return HALO_E_INVAL;
+    if ((rc = halo::check_device())) return rc;
+    p.bytes = d_bytes;
+    p.lens = d_lens;
+    p.stride = stride;
+    p.len = len;
+    // the longest frame bounds the group width: uniform length is known, lens[] is not
+    const uint32_t max_len = d_lens ? (uint32_t)(stride < 65535 ? stride : 65535) : len;
+    return halo::launch_parse(p, d_lens ? 1 : 2, max_len, static_cast<hipStream_t>(stream));
+}

@@ -1,0 +1,138 @@
+"""Batched mirror of halo's receive engine (engine/engine.go:339-385 and its callees).
+
+The reference's ``NetIf.PacketHandle`` pulls one frame per iteration from
+``NetIfConfig.EthRxFunc`` (engine/engine.go:76,348) and runs ``RxEthernet`` -> ``RxIpv4``
+-> ``Rx{Udp,Tcp,Icmp}`` on it. ``NetIf.packet_handle_batch`` drains up to ``batch`` frames
+from the same kind of ``eth_rx_func`` (a callable returning ``bytes`` or ``None``), parses
+and verifies the whole batch on the GPU through ``halo_rx_parse_batch_host`` (pinned
+staging, double-buffered H2D -> kernel -> D2H), maps every record to the reference
+engine's decision with ``halo_rx_dispatch`` and invokes the registered UDP / TCP service
+handlers in frame order, with the same session and payload arguments as
+engine/udp_engine.go:16-20 and engine/tcp_engine.go:79-88.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import ACTION, ACTION_NAMES, RESULT_DTYPE, NetIf as NetIfAbi
+from .protocol import flags_word
+
+
+def dispatch(results: np.ndarray, netif: NetIfAbi) -> np.ndarray:
+    """Reference engine decision per record (halo_rx_dispatch), as uint8 action codes."""
+    results = np.ascontiguousarray(results).view(RESULT_DTYPE).reshape(-1)
+    actions = np.empty(results.shape[0], dtype=np.uint8)
+    rc = _lib.lib.halo_rx_dispatch(_lib.ptr(results), results.shape[0], netif, _lib.ptr(actions), None)
+    _lib.check("halo_rx_dispatch", rc)
+    return actions
+
+
+@dataclass
+class UdpSession:  # engine/udp_engine.go:47-50
+    RemoteIp: int
+    RemotePort: int
+
+
+@dataclass
+class TcpSession:  # engine/tcp_engine.go:103-106
+    RemoteIp: int
+    RemotePort: int
+
+
+class HostBatcher:
+    """Owns a halo_rx_host_ctx (pinned staging + two streams) on one device."""
+
+    def __init__(self, device: int = 0, chunk_frames: int = 0, chunk_bytes: int = 0):
+        h = ctypes.c_void_p()
+        _lib.check("halo_rx_host_ctx_create",
+                   _lib.lib.halo_rx_host_ctx_create(device, chunk_frames, chunk_bytes, ctypes.byref(h)))
+        self._ctx = h
+
+    def close(self):
+        if self._ctx:
+            _lib.lib.halo_rx_host_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def parse(self, data: np.ndarray, offsets: np.ndarray, lens: np.ndarray, netif: NetIfAbi, flags: int,
+              hist: Optional[np.ndarray] = None) -> np.ndarray:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        n = lens.shape[0]
+        out = np.empty(n, dtype=RESULT_DTYPE)
+        if hist is not None:
+            assert hist.dtype == np.uint32 and hist.flags.c_contiguous
+        rc = _lib.lib.halo_rx_parse_batch_host(self._ctx, _lib.ptr(data), _lib.ptr(offsets), _lib.ptr(lens), n,
+                                               flags, netif, _lib.ptr(out), _lib.ptr(hist))
+        _lib.check("halo_rx_parse_batch_host", rc)
+        return out
+
+
+@dataclass
+class NetIf:
+    """engine.NetIf / NetIfConfig (engine/engine.go:65-121), receive side only."""
+
+    Name: str
+    MacAddr: str
+    IpAddr: str
+    EthRxFunc: Callable[[], Optional[bytes]]
+    NatEnable: bool = False
+    CheckSumEnable: bool = True  # protocol.CheckSumEnable for this interface's batches
+    UdpServiceMap: dict = field(default_factory=dict)
+    TcpServiceMap: dict = field(default_factory=dict)
+    device: int = 0
+
+    def __post_init__(self):
+        self.abi = NetIfAbi.make(self.MacAddr, self.IpAddr, self.NatEnable)
+        self._batcher: Optional[HostBatcher] = None
+        self.action_counts = np.zeros(len(ACTION_NAMES), dtype=np.int64)
+
+    def RecvUdp(self, port: int, handle: Callable):  # engine/udp_engine.go:56-58
+        self.UdpServiceMap[port] = handle
+
+    def RecvTcp(self, port: int, handle: Callable):  # engine/tcp_engine.go:112-114
+        self.TcpServiceMap[port] = handle
+
+    def packet_handle_batch(self, batch: int = 4096):
+        """One batched iteration of PacketHandle: drain, parse on GPU, dispatch.
+
+        Returns (results, actions) for the frames drained this iteration.
+        """
+        frames = []
+        for _ in range(batch):
+            f = self.EthRxFunc()
+            if f is None:
+                break
+            frames.append(bytes(f))
+        if not frames:
+            return np.empty(0, RESULT_DTYPE), np.empty(0, np.uint8)
+        lens = np.fromiter((len(f) for f in frames), dtype=np.uint16, count=len(frames))
+        offsets = np.zeros(len(frames), dtype=np.uint64)
+        np.cumsum(lens[:-1], out=offsets[1:])
+        data = np.frombuffer(b"".join(frames), dtype=np.uint8)
+        if self._batcher is None:
+            self._batcher = HostBatcher(self.device)
+        res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable))
+        actions = dispatch(res, self.abi)
+        np.add.at(self.action_counts, actions, 1)
+        for i in np.nonzero((actions == ACTION["LOCAL_UDP"]) | (actions == ACTION["LOCAL_TCP"]))[0]:
+            r = res[i]
+            payload = frames[i][int(r["payload_off"]):int(r["payload_off"]) + int(r["payload_len"])]
+            if actions[i] == ACTION["LOCAL_UDP"]:
+                h = self.UdpServiceMap.get(int(r["dport"]))
+                if h is not None:
+                    h(UdpSession(int(r["src_ip"]), int(r["sport"])), payload)
+            else:
+                h = self.TcpServiceMap.get(int(r["dport"]))
+                if h is not None:
+                    h(TcpSession(int(r["src_ip"]), int(r["sport"])), payload, int(r["l4_seq"]),
+                      int(r["l4_ack"]), int(r["l4_aux"]))
+        return res, actions

@@ -1,0 +1,132 @@
+"""Batch mirror of halo's ``protocol`` package on the receive path.
+
+The reference parses one frame per call (``protocol.ParseEthFrm`` -> ``ParseIpv4Pkt`` ->
+``ParseUdpPkt`` / ``ParseTcpPkt`` / ``ParseIcmpPkt``, gated by the package global
+``protocol.CheckSumEnable``). Here one call parses a whole device-resident batch through the
+C ABI (``halo_rx_parse_batch_device``); the per-frame Go return values become one 32-byte
+``halo_rx_result_t`` record per frame (see ``include/halo_rx.h`` for the field contract).
+
+Names and constants follow the reference so code reads like its own:
+``check_sum_enable`` is ``CheckSumEnable`` (protocol/utils.go:8), the EtherType / IP
+protocol / ICMP constants are those of protocol/ethernet.go:16-22, protocol/ipv4.go:27-32,
+protocol/icmp.go:25-30 and protocol/tcp.go:26-33, and ``ERROR_TEXT`` maps each status to the
+error string the reference returns for it.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import HALO_RX_CSUM_ENABLE, HALO_RX_JUMBO_EXT, RESULT_DTYPE, STATUS, STATUS_NAMES, NetIf
+
+# protocol/ethernet.go:16-22
+IEEE_802_3 = 0x05DC
+ETH_PROTO_IPV4 = 0x0800
+ETH_PROTO_ARP = 0x0806
+ETH_PROTO_IPV6 = 0x86DD
+ETH_PROTO_UNKNOWN = 0xFFFF
+BROADCAST_MAC_ADDR = b"\xff" * 6
+# protocol/ipv4.go:27-32
+IPH_PROTO_ICMP = 0x01
+IPH_PROTO_TCP = 0x06
+IPH_PROTO_UDP = 0x11
+IPH_PROTO_UNKNOWN = 0xFF
+# protocol/icmp.go:25-30
+ICMP_REQUEST = 0x08
+ICMP_REPLY = 0x00
+ICMP_TTL = 0x0B
+ICMP_UNKNOWN = 0xFF
+# protocol/tcp.go:26-33
+TCP_FLAGS_URG = 0x20
+TCP_FLAGS_ACK = 0x10
+TCP_FLAGS_PSH = 0x08
+TCP_FLAGS_RST = 0x04
+TCP_FLAGS_SYN = 0x02
+TCP_FLAGS_FIN = 0x01
+
+# status -> the error the reference returns at that check (None: no error / build-defined)
+ERROR_TEXT = {
+    "OK": None,
+    "ETH_LEN": "ethernet frame len must >= 42 and <= 1514 bytes",   # ethernet.go:32
+    "ETH_TYPE": "unknown ethernet protocol",                        # ethernet.go:49
+    "IP_LEN": "ip packet len must >= 20 and <= 1500 bytes",         # ipv4.go:50
+    "IP_VER": "not support type of ip packet",                      # ipv4.go:53
+    "IP_FRAG": "not support ip frg",                                # ipv4.go:60
+    "IP_PROTO": "unknown ip protocol",                              # ipv4.go:71
+    "IP_HDR_CKSUM": "header check sum error",                       # ipv4.go:76
+    "IP_TOTLEN_UNDERFLOW": None,  # Go: slice-bounds panic (ipv4.go:84)
+    "IP_TOTLEN_OVERRUN": None,    # Go: stale bytes or slice-bounds panic (ipv4.go:84)
+    "L4_LEN": "udp/tcp/icmp packet len out of range",               # udp.go:23 / tcp.go:38 / icmp.go:35
+    "ICMP_TYPE": "not support type of icmp packet",                 # icmp.go:46
+    "ICMP_CODE": "not support type of icmp packet",                 # icmp.go:50
+    "L4_CKSUM": "check sum error",                                  # udp.go:43 / tcp.go:55 / icmp.go:54
+}
+
+
+def flags_word(check_sum_enable: bool = True, jumbo: bool = False) -> int:
+    """The ABI ``flags`` word that replaces the ``CheckSumEnable`` package global."""
+    return (HALO_RX_CSUM_ENABLE if check_sum_enable else 0) | (HALO_RX_JUMBO_EXT if jumbo else 0)
+
+
+def _stream_handle(stream):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _check_out(out, n: int):
+    import torch
+
+    assert out.dtype == torch.uint8 and out.is_cuda and out.numel() >= 32 * n, "out: cuda uint8[n*32]"
+
+
+def parse_frames_batch(frames, offsets_dw, lens, *, netif: NetIf, check_sum_enable: bool = True,
+                       jumbo: bool = False, max_len_hint: int = 0, out=None, hist=None, stream=None):
+    """Parse + verify a ragged, device-resident batch (ParseEthFrm..ParseIcmpPkt per frame).
+
+    frames: cuda uint8 tensor; offsets_dw: cuda int32 tensor (frame i at 4*offsets_dw[i]);
+    lens: cuda int16 tensor (u16 lengths). Returns the cuda uint8 [n, 32] result tensor.
+    ``hist`` (cuda int32[14]) is incremented per status. Asynchronous on ``stream``.
+    """
+    import torch
+
+    n = int(lens.numel())
+    if out is None:
+        out = torch.empty((n, 32), dtype=torch.uint8, device=frames.device)
+    _check_out(out, n)
+    rc = _lib.lib.halo_rx_parse_batch_device(
+        _lib.ptr(frames), _lib.ptr(offsets_dw), _lib.ptr(lens), n,
+        flags_word(check_sum_enable, jumbo), netif, max_len_hint, _lib.ptr(out), _lib.ptr(hist),
+        _stream_handle(stream))
+    _lib.check("halo_rx_parse_batch_device", rc)
+    return out
+
+
+def parse_frames_strided(frames, stride: int, n: int, *, netif: NetIf, length: int = 0, lens=None,
+                         check_sum_enable: bool = True, jumbo: bool = False, out=None, hist=None,
+                         stream=None):
+    """Same as parse_frames_batch for frames at i*stride (uniform ``length`` or ``lens``)."""
+    import torch
+
+    if out is None:
+        out = torch.empty((n, 32), dtype=torch.uint8, device=frames.device)
+    _check_out(out, n)
+    rc = _lib.lib.halo_rx_parse_strided_device(
+        _lib.ptr(frames), stride, _lib.ptr(lens), length, n, flags_word(check_sum_enable, jumbo), netif,
+        _lib.ptr(out), _lib.ptr(hist), _stream_handle(stream))
+    _lib.check("halo_rx_parse_strided_device", rc)
+    return out
+
+
+def records(out) -> np.ndarray:
+    """View a result buffer (cuda or host, uint8 [n,32]) as a numpy structured array."""
+    a = out.cpu().numpy() if hasattr(out, "cpu") else np.asarray(out)
+    return np.ascontiguousarray(a).reshape(-1).view(RESULT_DTYPE)
+
+
+def status_name(code: int) -> str:
+    return STATUS_NAMES[code] if 0 <= code < len(STATUS_NAMES) else "UNKNOWN"
+
+
+__all__ = [name for name in dir() if not name.startswith("_")] + ["STATUS"]

@@ -1,0 +1,229 @@
+/*
+ * halo_rx.h — C ABI of the MI355X-native receive parse-and-checksum engine.
+ *
+ * This is the drop-in boundary for halo's software receive path.
+ * The reference has no FFI on this path: the parsers are plain Go functions that
+ * engine.(*NetIf).PacketHandle calls once per frame. This ABI replaces that per-frame
+ * chain with one call per BATCH of frames:
+ *
+ *   reference (one frame at a time)                       replaced by
+ *   -----------------------------------------------------  -------------------------------
+ *   protocol.ParseEthFrm        protocol/ethernet.go:29-55 \
+ *   protocol.ParseIpv4Pkt       protocol/ipv4.go:48-86      |
+ *   protocol.ParseUdpPkt        protocol/udp.go:21-49       |  halo_rx_parse_batch_device()
+ *   protocol.ParseTcpPkt        protocol/tcp.go:36-70       |  halo_rx_parse_strided_device()
+ *   protocol.ParseIcmpPkt       protocol/icmp.go:33-63      |  (one halo_rx_result_t per frame)
+ *   protocol.GetCheckSum        protocol/utils.go:11-31     |
+ *   protocol.NatGetSrcDstPort   protocol/ipv4.go:229-246    |
+ *   protocol.IpAddrToU          protocol/utils.go:34-44    /
+ *   protocol.CheckSumEnable     protocol/utils.go:8         -> HALO_RX_CSUM_ENABLE bit of `flags`
+ *   NetIf.RxEthernet filter     engine/ethernet_engine.go:22 -> HALO_RX_F_MAC_MATCH
+ *   NetIf.RxIpv4 branch inputs  engine/ipv4_engine.go:24,31  -> HALO_RX_F_IP_BCAST / _DST_IS_OWN
+ *   NetIf.PacketHandle loop     engine/engine.go:339-385    -> halo_rx_parse_batch_host() (pinned H2D,
+ *                                                              kernel, D2H) + halo_rx_dispatch()
+ *
+ * Conventions (SURVEY.md §8b "Error convention"):
+ *   - Every entry point returns int: 0 (HALO_OK) or a negative HALO_E_* code. A malformed
+ *     frame is DATA (its status code in halo_rx_result_t), never a call failure.
+ *   - The caller owns every buffer. No globals: `flags` replaces protocol.CheckSumEnable.
+ *   - Calls are thread-safe per (device, stream).
+ *   - There is no CPU fallback: without a gfx950 device every compute entry point
+ *     returns HALO_E_NODEV / HALO_E_ARCH.
+ *
+ * Frame layout in device memory (DESIGN.md "Data layout in HBM"):
+ *   - ragged:  frame i starts at bytes + 4*offsets_dw[i] (4-byte aligned starts, as the
+ *              reference's ring records are: mem/ring_buffer.go:47-50) and is lens[i] bytes
+ *              long. u32 dword offsets address 16 GiB per call.
+ *   - strided: frame i starts at bytes + i*stride (stride a multiple of 4), length
+ *              lens[i] or, when lens == NULL, the uniform length `len`.
+ *   The kernel never reads past the 4-byte word that holds a frame's last byte.
+ */
+#ifndef HALO_RX_H
+#define HALO_RX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define HALO_API __attribute__((visibility("default")))
+#else
+#define HALO_API
+#endif
+
+/* ---- return codes ------------------------------------------------------------------ */
+#define HALO_OK 0
+#define HALO_E_INVAL (-1)   /* bad argument (null pointer, bad stride/flags)              */
+#define HALO_E_NODEV (-2)   /* no HIP device / device index out of range                  */
+#define HALO_E_ARCH (-3)    /* device is not gfx950 (MI355X)                              */
+#define HALO_E_HIP (-4)     /* a HIP runtime call or kernel launch failed                 */
+#define HALO_E_NOMEM (-5)   /* device or pinned host allocation failed                    */
+#define HALO_E_RANGE (-6)   /* batch too large for the addressing mode                    */
+
+/* ---- flags (replaces the protocol.CheckSumEnable package global, protocol/utils.go:8) - */
+#define HALO_RX_CSUM_ENABLE 0x1u /* verify IPv4 header + UDP/TCP checksums (ICMP: always)  */
+#define HALO_RX_JUMBO_EXT 0x2u   /* build-defined extension: lift the 1514/1500/1480 caps   */
+                                 /* to 9014/9000/8980 (MTU 9000); arithmetic unchanged      */
+
+/* ---- per-frame status: the FIRST failing check in reference order, 0 = OK ---------- */
+typedef enum halo_rx_status {
+    HALO_RX_OK = 0,
+    HALO_RX_ETH_LEN = 1,              /* len<42 || len>1514        protocol/ethernet.go:31    */
+    HALO_RX_ETH_TYPE = 2,             /* EtherType not whitelisted protocol/ethernet.go:39-50 */
+    HALO_RX_IP_LEN = 3,               /* len<20 || len>1500        protocol/ipv4.go:49        */
+    HALO_RX_IP_VER = 4,               /* pkt[0] != 0x45            protocol/ipv4.go:52        */
+    HALO_RX_IP_FRAG = 5,              /* flags/offset not DF|0     protocol/ipv4.go:59        */
+    HALO_RX_IP_PROTO = 6,             /* proto not ICMP/TCP/UDP    protocol/ipv4.go:63-72     */
+    HALO_RX_IP_HDR_CKSUM = 7,         /* GetCheckSum(hdr) != 0     protocol/ipv4.go:74-78     */
+    HALO_RX_IP_TOTLEN_UNDERFLOW = 8,  /* totalLen < 20: Go panics  protocol/ipv4.go:84 (build-defined) */
+    HALO_RX_IP_TOTLEN_OVERRUN = 9,    /* totalLen > len(pkt): Go reads stale bytes or panics (build-defined) */
+    HALO_RX_L4_LEN = 10,              /* udp.go:22 / tcp.go:37 / icmp.go:34                   */
+    HALO_RX_ICMP_TYPE = 11,           /* type not 8/0/11           protocol/icmp.go:38-47     */
+    HALO_RX_ICMP_CODE = 12,           /* code != 0                 protocol/icmp.go:49        */
+    HALO_RX_L4_CKSUM = 13,            /* udp.go:42 / tcp.go:54 / icmp.go:53                   */
+    HALO_RX_STATUS_COUNT = 14
+} halo_rx_status_t;
+
+/* ---- per-frame flags: what engine/{ethernet,ipv4}_engine.go branch on ---------------- */
+#define HALO_RX_F_MAC_MATCH 0x01u  /* dst MAC == own || broadcast   engine/ethernet_engine.go:22 */
+#define HALO_RX_F_IP_BCAST 0x02u   /* dst IP byte 3 == 255           engine/ipv4_engine.go:24     */
+#define HALO_RX_F_DST_IS_OWN 0x04u /* dst IP == own IP               engine/ipv4_engine.go:31     */
+
+/* ---- per-frame result record (32 B, written once per frame) ---------------------------
+ * Each field is the output of the reference layer that produced it, filled only when that
+ * layer returned without error (Go returns zero values / nil slices on error):
+ *   ethertype     ParseEthFrm ethProto (0xFFFF on error: ETH_PROTO_UNKNOWN)
+ *   ip_proto      ParseIpv4Pkt ipHeadProto (0xFF when not IPv4 or on error: IPH_PROTO_UNKNOWN)
+ *   src_ip/dst_ip IpAddrToU(srcAddr/dstAddr)   (0 when ParseIpv4Pkt did not succeed)
+ *   ip_total_len  IPv4 totalLen field           (0 when ParseIpv4Pkt did not succeed)
+ *   sport/dport   NatGetSrcDstPort(ethPayload)  (ICMP: echo id twice; 0 when IP failed)
+ *   l4_aux        TCP flags (tcp.go:50) or ICMP type (icmp.go:38)   (0 unless L4 succeeded)
+ *   l4_seq        TCP seqNum, or ICMP id<<16 | seq                   (0 unless L4 succeeded)
+ *   l4_ack        TCP ackNum                                         (0 unless L4 succeeded)
+ *   payload_off/payload_len  the innermost successfully returned payload slice, in frame
+ *                 coordinates: Ethernet frm[14:], IPv4 pkt[20:totalLen], UDP pkt[8:],
+ *                 TCP pkt[headerLen:] (headerLen = data-offset nibble used as BYTES,
+ *                 protocol/tcp.go:49,68), ICMP pkt[8:]. 0/0 on an Ethernet error.
+ * The kernel evaluates the L4 parser selected by ip_proto for EVERY IPv4 frame; which of
+ * those verdicts the reference engine would actually have evaluated follows from `flags`
+ * (see halo_rx_dispatch).                                                               */
+typedef struct halo_rx_result {
+    uint8_t status;        /* halo_rx_status_t */
+    uint8_t flags;         /* HALO_RX_F_*      */
+    uint16_t ethertype;
+    uint8_t ip_proto;
+    uint8_t l4_aux;
+    uint16_t ip_total_len;
+    uint32_t src_ip;
+    uint32_t dst_ip;
+    uint16_t sport;
+    uint16_t dport;
+    uint16_t payload_off;
+    uint16_t payload_len;
+    uint32_t l4_seq;
+    uint32_t l4_ack;
+} halo_rx_result_t;
+
+/* ---- the interface a frame is received on (engine.NetIfConfig, engine/engine.go:65-81) - */
+typedef struct halo_rx_netif {
+    uint8_t mac[6];  /* NetIf.MacAddr                              */
+    uint8_t pad[2];
+    uint32_t ip;     /* IpAddrToU(NetIf.IpAddr), host integer      */
+    uint32_t nat_enable; /* NetIfConfig.NatEnable (only halo_rx_dispatch reads it) */
+} halo_rx_netif_t;
+
+typedef void* halo_stream_t; /* a hipStream_t (NULL = the device's null stream) */
+
+/* ---- device / library -------------------------------------------------------------- */
+HALO_API const char* halo_rx_version(void);
+/* Selects `device` for the calling thread and checks that it is a gfx950 part. */
+HALO_API int halo_rx_init(int device);
+HALO_API const char* halo_rx_strerror(int code);
+HALO_API const char* halo_rx_status_name(int status);
+
+/* ---- device-resident batch parse (the hot path) --------------------------------------
+ * All pointers are device pointers. `d_out` receives n records. `d_status_hist`, if not
+ * NULL, receives HALO_RX_STATUS_COUNT u32 counters that are INCREMENTED (the caller
+ * zeroes them). `max_len_hint` (0 = unknown) selects the lanes-per-frame variant.
+ * Asynchronous on `stream`.                                                              */
+HALO_API int halo_rx_parse_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                        const uint16_t* d_lens, uint32_t n, uint32_t flags,
+                                        const halo_rx_netif_t* netif, uint32_t max_len_hint,
+                                        halo_rx_result_t* d_out, uint32_t* d_status_hist,
+                                        halo_stream_t stream);
+
+HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uint64_t stride,
+                                          const uint16_t* d_lens, uint32_t len, uint32_t n,
+                                          uint32_t flags, const halo_rx_netif_t* netif,
+                                          halo_rx_result_t* d_out, uint32_t* d_status_hist,
+                                          halo_stream_t stream);
+
+/* ---- host-memory batch parse -----------------------------------
+ * Frames in HOST memory (any alignment, ragged byte offsets). Stages them into pinned
+ * buffers, copies H2D, runs the kernel and copies results D2H, double-buffered in chunks
+ * of `chunk_frames` (0 = default). Synchronous: returns when `out` is filled.           */
+typedef struct halo_rx_host_ctx halo_rx_host_ctx_t;
+HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frames, uint64_t chunk_bytes,
+                                     halo_rx_host_ctx_t** ctx);
+HALO_API int halo_rx_host_ctx_destroy(halo_rx_host_ctx_t* ctx);
+HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* bytes,
+                                      const uint64_t* offsets, const uint16_t* lens, uint32_t n,
+                                      uint32_t flags, const halo_rx_netif_t* netif,
+                                      halo_rx_result_t* out, uint32_t* status_hist);
+
+/* ---- the reference engine's per-frame decision (engine/ethernet_engine.go:13-31,
+ *      engine/ipv4_engine.go:18-47, engine/{udp,tcp,icmp}_engine.go) ------------------ */
+typedef enum halo_rx_action {
+    HALO_RX_ACT_DROP_ETH = 0,      /* ParseEthFrm error: logged and dropped              */
+    HALO_RX_ACT_IGNORE_MAC = 1,    /* not for this NetIf (dst MAC filter)                */
+    HALO_RX_ACT_ARP = 2,           /* -> HandleArp                                       */
+    HALO_RX_ACT_IGNORE_TYPE = 3,   /* 802.3 / IPv6: silently ignored                     */
+    HALO_RX_ACT_DROP_IP = 4,       /* ParseIpv4Pkt error (incl. build-defined totalLen)   */
+    HALO_RX_ACT_BCAST_UDP = 5,     /* RxUdpBroadcast, UDP parse+verify OK (-> DHCP)      */
+    HALO_RX_ACT_DROP_BCAST_UDP = 6,/* RxUdpBroadcast, UDP parse error                    */
+    HALO_RX_ACT_IGNORE_BCAST = 7,  /* x.x.x.255 and not UDP                              */
+    HALO_RX_ACT_FORWARD = 8,       /* Ipv4RouteForward (no L4 verification)              */
+    HALO_RX_ACT_LOCAL_ICMP = 9,    /* RxIcmp OK                                          */
+    HALO_RX_ACT_LOCAL_UDP = 10,    /* RxUdp OK -> UdpServiceMap                          */
+    HALO_RX_ACT_LOCAL_TCP = 11,    /* RxTcp OK -> TcpServiceMap                          */
+    HALO_RX_ACT_DROP_L4 = 12,      /* local L4 parse error: logged and dropped           */
+    HALO_RX_ACT_COUNT = 13
+} halo_rx_action_t;
+
+/* Host-side: maps n results to the action the reference engine takes (u8 per frame).
+ * Pure host code over the kernel's records; no GPU needed. `action_hist` (optional)
+ * receives HALO_RX_ACT_COUNT counters (incremented).                                    */
+HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32_t n,
+                              const halo_rx_netif_t* netif, uint8_t* actions,
+                              uint32_t* action_hist);
+
+/* ---- synthetic traffic (bench + tests; SURVEY.md §8d generator) ----------------------
+ * Every field of frame i is a pure function of (seed, i), so any shard of the global
+ * stream [first_index, first_index + n) is generated independently.
+ * halo_synth_layout (host): per-frame length, kind byte and ragged 4-byte-aligned dword
+ * offsets (frames packed back to back, each rounded up to 4 bytes).
+ *   size_mode : 0 = uniform `len`, 1 = IMIX 64/570/1500 at 7:4:1
+ *   proto_mode: 0 = UDP, 1 = TCP, 2 = ICMP, 3 = mix UDP 50 / TCP 40 / ICMP 10
+ *   mutate_shift: frame mutated with probability 2^-mutate_shift (0 = never)
+ *   kinds[i]  : bits 0-1 protocol (0 UDP, 1 TCP, 2 ICMP), bit 7 = mutated
+ *   *total_bytes = bytes the ragged layout spans.
+ * halo_synth_frames_device: writes the frame bytes for a layout into d_bytes (ragged
+ * dword offsets, or i*stride when d_offsets_dw == NULL). A mutated frame has one bit
+ * flipped in [14, len) after its checksums were filled.                                 */
+HALO_API int halo_synth_layout(uint64_t seed, uint64_t first_index, uint32_t n,
+                               uint32_t size_mode, uint32_t len, uint32_t proto_mode,
+                               uint32_t mutate_shift, uint16_t* lens, uint32_t* offsets_dw,
+                               uint8_t* kinds, uint64_t* total_bytes);
+HALO_API int halo_synth_frames_device(uint64_t seed, uint64_t first_index, uint32_t n,
+                                      const uint16_t* d_lens, const uint32_t* d_offsets_dw,
+                                      uint64_t stride, const uint8_t* d_kinds,
+                                      const halo_rx_netif_t* netif, uint8_t* d_bytes,
+                                      halo_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HALO_RX_H */

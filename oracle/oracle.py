@@ -1,0 +1,150 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of oracle/liboracle.so (halo_rx_oracle.c).
+
+The C restatement of protocol.Parse* / GetCheckSum / engine.RxEthernet->RxIpv4->Rx* (see
+the file header of halo_rx_oracle.c for the reference lines it follows). Used as the
+parity checker in tests/ and smoke(), and timed as bench.py's cpu_baseline.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+RESULT_DTYPE = np.dtype([
+    ("status", "u1"), ("flags", "u1"), ("ethertype", "<u2"),
+    ("ip_proto", "u1"), ("l4_aux", "u1"), ("ip_total_len", "<u2"),
+    ("src_ip", "<u4"), ("dst_ip", "<u4"),
+    ("sport", "<u2"), ("dport", "<u2"),
+    ("payload_off", "<u2"), ("payload_len", "<u2"),
+    ("l4_seq", "<u4"), ("l4_ack", "<u4"),
+])
+STATUS_COUNT = 14
+
+
+class NetIf(ctypes.Structure):
+    _fields_ = [("mac", ctypes.c_uint8 * 6), ("pad", ctypes.c_uint8 * 2), ("ip", ctypes.c_uint32),
+                ("nat_enable", ctypes.c_uint32)]
+
+    @classmethod
+    def make(cls, mac="AA:AA:AA:AA:AA:AA", ip="192.168.100.100", nat_enable=False):
+        n = cls()
+        for i, p in enumerate(mac.split(":")[:6]):
+            n.mac[i] = int(p, 16)
+        a = [int(x) for x in ip.split(".")]
+        n.ip = (a[0] << 24) | (a[1] << 16) | (a[2] << 8) | a[3]
+        n.nat_enable = int(nat_enable)
+        return n
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "halo_rx_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        L.ora_get_checksum.restype = ctypes.c_uint16
+        L.ora_get_checksum.argtypes = [vp, ctypes.c_size_t]
+        L.ora_rx_frame.restype = None
+        L.ora_rx_frame.argtypes = [vp, u32, u32, ctypes.POINTER(NetIf), vp]
+        L.ora_engine_rx.restype = ctypes.c_int
+        L.ora_engine_rx.argtypes = [vp, u32, u32, ctypes.POINTER(NetIf)]
+        L.ora_rx_batch.restype = ctypes.c_int
+        L.ora_rx_batch.argtypes = [vp, vp, vp, u64, u32, u32, u32, ctypes.POINTER(NetIf), vp, vp, ctypes.c_int]
+        L.ora_engine_batch.restype = None
+        L.ora_engine_batch.argtypes = [vp, vp, vp, u64, u32, u32, u32, ctypes.POINTER(NetIf), vp]
+        L.ora_synth_kind.restype = None
+        L.ora_synth_kind.argtypes = [u64, u64, u32, u32, u32, u32, vp, vp]
+        L.ora_synth_frame.restype = None
+        L.ora_synth_frame.argtypes = [u64, u64, u32, ctypes.c_uint8, ctypes.POINTER(NetIf), vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def get_checksum(data: bytes) -> int:
+    b = np.frombuffer(bytes(data), dtype=np.uint8)
+    return lib().ora_get_checksum(_p(b) if len(b) else None, len(b))
+
+
+def rx_frame(frame: bytes, netif: NetIf, flags: int = 1) -> np.ndarray:
+    b = np.frombuffer(bytes(frame) + b"\0", dtype=np.uint8)
+    out = np.zeros(1, dtype=RESULT_DTYPE)
+    lib().ora_rx_frame(_p(b), len(frame), flags, netif, _p(out))
+    return out[0]
+
+
+def engine_rx(frame: bytes, netif: NetIf, flags: int = 1) -> int:
+    b = np.frombuffer(bytes(frame) + b"\0", dtype=np.uint8)
+    return lib().ora_engine_rx(_p(b), len(frame), flags, netif)
+
+
+def rx_batch(data: np.ndarray, lens: np.ndarray, netif: NetIf, flags: int = 1, offsets_dw=None, stride: int = 0,
+             length: int = 0, threads: int = 1):
+    """Returns (records, status histogram)."""
+    n = int(lens.shape[0]) if lens is not None else int(data.shape[0] // stride)
+    out = np.zeros(n, dtype=RESULT_DTYPE)
+    hist = np.zeros(STATUS_COUNT, dtype=np.uint32)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    lens_c = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
+    offs_c = None if offsets_dw is None else np.ascontiguousarray(offsets_dw, dtype=np.uint32)
+    rc = lib().ora_rx_batch(_p(data), _p(offs_c), _p(lens_c), stride, length, n, flags, netif, _p(out), _p(hist),
+                            threads)
+    assert rc == 0
+    return out, hist
+
+
+def engine_batch(data, lens, netif, flags=1, offsets_dw=None, stride=0, length=0) -> np.ndarray:
+    n = int(lens.shape[0])
+    acts = np.zeros(n, dtype=np.uint8)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    lens_c = np.ascontiguousarray(lens, dtype=np.uint16)
+    offs_c = None if offsets_dw is None else np.ascontiguousarray(offsets_dw, dtype=np.uint32)
+    lib().ora_engine_batch(_p(data), _p(offs_c), _p(lens_c), stride, length, n, flags, netif, _p(acts))
+    return acts
+
+
+def synth_kind(seed, index, size_mode=0, length=64, proto_mode=0, mutate_shift=0):
+    L = np.zeros(1, np.uint16)
+    k = np.zeros(1, np.uint8)
+    lib().ora_synth_kind(seed, index, size_mode, length, proto_mode, mutate_shift, _p(L), _p(k))
+    return int(L[0]), int(k[0])
+
+
+def synth_frame(seed: int, index: int, length: int, kind: int, netif: NetIf) -> bytes:
+    f = np.zeros(length, dtype=np.uint8)
+    lib().ora_synth_frame(seed, index, length, kind, netif, _p(f))
+    return f.tobytes()
+
+
+def synth_batch(seed, first_index, lens, kinds, netif, offsets_dw=None, stride=0, fill=0) -> np.ndarray:
+    """Host twin of halo_synth_frames_device: the same bytes laid out the same way."""
+    n = len(lens)
+    if offsets_dw is not None:
+        total = (int(offsets_dw[-1]) * 4 + ((int(lens[-1]) + 3) & ~3)) if n else 0
+    else:
+        total = stride * n
+    buf = np.full(max(16, (total + 15) & ~15), fill, dtype=np.uint8)
+    for k in range(n):
+        start = int(offsets_dw[k]) * 4 if offsets_dw is not None else k * stride
+        L = int(lens[k])
+        buf[start:start + L] = np.frombuffer(synth_frame(seed, first_index + k, L, int(kinds[k]), netif), np.uint8)
+    return buf

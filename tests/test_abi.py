@@ -1,0 +1,154 @@
+"""CPU: the C-ABI library loads, exports every symbol include/halo_rx.h declares, agrees
+with the header on struct layout, refuses bad arguments, and has no CPU compute fallback.
+Also the pure-host pieces of the ABI: halo_rx_dispatch and halo_synth_layout."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "halo_rx.h")
+
+
+def _declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"HALO_API\s+[\w\s\*]+?\b(halo_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from halo_amd import _lib
+
+    syms = _declared_symbols()
+    assert len(syms) >= 12
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    for s in syms:
+        assert hasattr(_lib.lib, s)
+
+
+def test_result_struct_layout_matches_header(tmp_path):
+    from halo_amd._lib import RESULT_DTYPE, NetIf
+
+    src = tmp_path / "layout.c"
+    fields = list(RESULT_DTYPE.names)
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "halo_rx.h"\nint main(void){\n'
+        + "".join(f'printf("%zu\\n", offsetof(halo_rx_result_t, {f}));\n' for f in fields)
+        + 'printf("%zu\\n%zu\\n%zu\\n", sizeof(halo_rx_result_t), sizeof(halo_rx_netif_t), '
+          'offsetof(halo_rx_netif_t, ip));\nreturn 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[:len(fields)] == [RESULT_DTYPE.fields[f][1] for f in fields]
+    assert vals[len(fields)] == RESULT_DTYPE.itemsize == 32
+    assert vals[len(fields) + 1] == ctypes.sizeof(NetIf)
+    assert vals[len(fields) + 2] == NetIf.ip.offset
+
+
+def test_status_and_error_names():
+    from halo_amd import _lib
+
+    for code, name in enumerate(_lib.STATUS_NAMES):
+        assert _lib.lib.halo_rx_status_name(code).decode() == name
+    assert _lib.lib.halo_rx_status_name(99).decode() == "UNKNOWN"
+    assert _lib.strerror(_lib.HALO_E_ARCH) == "device is not gfx950"
+    assert b"gfx950" in _lib.lib.halo_rx_version()
+
+
+def test_argument_validation_without_gpu():
+    from halo_amd import _lib
+
+    L, n = _lib.lib, _lib.NetIf.make()
+    buf = np.zeros(64, np.uint8)
+    out = np.zeros(64, np.uint8)
+    # empty batch is a no-op success; a null netif / output is always INVAL
+    assert L.halo_rx_parse_batch_device(None, None, None, 0, 1, n, 0, out.ctypes.data, None, None) == 0
+    assert L.halo_rx_parse_batch_device(None, None, None, 0, 1, None, 0, out.ctypes.data, None, None) == -1
+    assert L.halo_rx_parse_batch_device(None, None, None, 1, 1, n, 0, out.ctypes.data, None, None) == -1
+    assert L.halo_rx_parse_batch_device(buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 1, 0x10, n, 0,
+                                        out.ctypes.data, None, None) == -1  # unknown flag bit
+    assert L.halo_rx_parse_batch_device(buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 1, 1, n, 0,
+                                        out.ctypes.data + 4, None, None) == -1  # misaligned output
+    assert L.halo_rx_parse_strided_device(buf.ctypes.data, 6, None, 60, 2, 1, n, out.ctypes.data, None,
+                                          None) == -1  # stride not a multiple of 4
+    assert L.halo_rx_parse_strided_device(buf.ctypes.data, 60, None, 64, 2, 1, n, out.ctypes.data, None,
+                                          None) == -1  # overlapping uniform frames
+
+
+def test_no_cpu_fallback_without_device():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from halo_amd import _lib
+
+    L, n = _lib.lib, _lib.NetIf.make()
+    buf = np.zeros(128, np.uint8)
+    out = np.zeros(64, np.uint8)
+    offs = np.zeros(1, np.uint32)
+    lens = np.full(1, 64, np.uint16)
+    assert L.halo_rx_init(0) == _lib.HALO_E_NODEV
+    rc = L.halo_rx_parse_batch_device(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, 1, 1, n, 0,
+                                      out.ctypes.data, None, None)
+    assert rc == _lib.HALO_E_NODEV
+
+
+def test_dispatch_matches_oracle_engine(golden, oracle_lib):
+    """halo_rx_dispatch (records -> engine action) == the oracle's independent re-derivation."""
+    from halo_amd import engine
+    from halo_amd._lib import NetIf
+    from tests.helpers import golden_arrays
+
+    meta, blob = golden
+    data, offs, lens, names = golden_arrays(meta, blob)
+    for nat in (False, True):
+        on = oracle_lib.NetIf.make(nat_enable=nat)
+        hn = NetIf.make(nat_enable=nat)
+        for fl in (0, 1, 2, 3):
+            recs, _ = oracle_lib.rx_batch(data, lens, on, fl, offsets_dw=offs)
+            got = engine.dispatch(recs, hn)
+            want = oracle_lib.engine_batch(data, lens, on, fl, offsets_dw=offs)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, [(names[i], got[i], want[i]) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("size_mode,proto_mode", [(0, 0), (0, 1), (0, 2), (1, 3)])
+def test_synth_layout_matches_oracle_twin(oracle_lib, size_mode, proto_mode):
+    from halo_amd import synth
+
+    lay = synth.layout(3000, length=128, size_mode=size_mode, proto_mode=proto_mode, mutate_shift=4,
+                       first_index=777)
+    offs = lay["offsets_dw"].astype(np.int64) * 4
+    assert offs[0] == 0 and np.all(np.diff(offs) == ((lay["lens"][:-1].astype(np.int64) + 3) & ~3))
+    assert lay["total_bytes"] == offs[-1] + ((int(lay["lens"][-1]) + 3) & ~3)
+    for k in range(0, 3000, 37):
+        L, kind = oracle_lib.synth_kind(synth.SEED, 777 + k, size_mode, 128, proto_mode, 4)
+        assert (L, kind) == (int(lay["lens"][k]), int(lay["kinds"][k]))
+    if size_mode == 1:
+        big = synth.layout(120000, size_mode=1, proto_mode=3)
+        frac = np.bincount(np.searchsorted([64, 570, 1500], big["lens"]), minlength=3) / 120000
+        assert np.allclose(frac, [7 / 12, 4 / 12, 1 / 12], atol=0.01)
+        pf = np.bincount(big["kinds"] & 3, minlength=3) / 120000
+        assert np.allclose(pf, [0.5, 0.4, 0.1], atol=0.01)
+
+
+def test_synth_twin_frames_verify(oracle_lib):
+    """Frames of the generator spec (host twin) verify clean, and every mutated frame fails."""
+    from halo_amd import synth
+
+    n = oracle_lib.NetIf.make()
+    lay = synth.layout(600, size_mode=1, proto_mode=3, mutate_shift=2)
+    data = oracle_lib.synth_batch(synth.SEED, 0, lay["lens"], lay["kinds"], n, offsets_dw=lay["offsets_dw"])
+    recs, _ = oracle_lib.rx_batch(data, lay["lens"], n, 1, offsets_dw=lay["offsets_dw"])
+    mutated = (lay["kinds"] & 0x80) != 0
+    assert mutated.sum() > 50
+    assert np.all(recs["status"][~mutated] == 0)
+    assert np.all(recs["status"][mutated] != 0)

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU-box session: each GPU step under its own time limit; stop at the first crash,
+# abort, fault or timeout (pytest's "tests failed" exit code 1 does not stop the session).
+# Usage: bash tools/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-run}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+step() {
+  local name=$1 limit=$2; shift 2
+  echo "[$(date +%T)] start $name" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    test)  step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 900 python bench.py ;;
+    benchq) step benchq 600 python bench.py --no-secondary --cpu-seconds 4 ;;
+    prof)  step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --steps 20 ;;
+    pmcf)  step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
+    pmcw)  step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo done
