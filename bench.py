@@ -81,12 +81,18 @@ class Dist:
             self.pg.destroy_process_group()
 
 
+def shard_first_index(rank: int, batch: int, n: int, rotate: int) -> int:
+    """Global index of the first frame of `batch` on `rank`: ranks own disjoint, contiguous
+    slices of the synthetic stream (index sharding) and never exchange data."""
+    return (rank * rotate + batch) * n
+
+
 def make_batches(dev, netif, *, n, rotate, rank, length=64, size_mode=0, proto_mode=0, strided=False):
     from halo_amd import synth
 
     batches = []
     for b in range(rotate):
-        first = (rank * rotate + b) * n
+        first = shard_first_index(rank, b, n, rotate)
         lay = synth.layout(n, length=length, size_mode=size_mode, proto_mode=proto_mode, first_index=first,
                            ragged=not strided)
         fr = synth.frames_device(lay, netif, device=dev, stride=length if strided else 0)
