@@ -1,4 +1,7 @@
-"""Build libhalo_rx.so (hipcc, gfx950) in-tree: ``python -m halo_amd.build``."""
+"""Build libhalo_rx.so (hipcc, gfx950) in-tree: ``python halo_amd/build.py [--force]``.
+
+Standalone on purpose: importing the halo_amd package requires the library this builds.
+"""
 from __future__ import annotations
 
 import os

@@ -15,9 +15,11 @@
 // frame; 64/G frames per wave. Lane j of the group loads dwords [4j, 4j+4) + k*4G of the frame
 // with one 16-byte load per step, so a wave-instruction covers 64/G frames' consecutive bytes
 // (coalesced). The 48-byte header (dwords 0..11) sits in group lanes 0..2 after the first load
-// and is broadcast to the group with 12 ds_bpermute shuffles; every lane then runs the header
-// checks redundantly (no divergence, no second broadcast). Only the L4 segment sum needs a
-// cross-lane reduction (log2 G xor-shuffles).
+// and is broadcast to the group (DPP quad_perm / row_newbcast for G = 4 / 16, v_readlane for
+// G = 64, ds_bpermute otherwise); every lane then runs the header checks redundantly (no
+// divergence, no second broadcast). Only the L4 segment sum needs a cross-lane reduction
+// (DPP butterflies). G = 1 (small frames): each lane owns a whole frame, reads its header with
+// its own three 16-byte loads and needs no cross-lane traffic at all.
 //
 // Checksum arithmetic (DESIGN.md "Checksum in the little-endian domain"): the frame is summed
 // as little-endian dwords. A one's-complement sum of byte-swapped 16-bit words is the byte
@@ -27,6 +29,8 @@
 // on half-dwords and an odd trailing byte lands in the low byte of its half, which is the
 // HIGH byte of its big-endian word: exactly protocol/utils.go:21-24.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 
 #include "halo_common.h"
 
@@ -46,6 +50,36 @@ __device__ __forceinline__ uint32_t fold64(uint64_t s) {
     return (uint32_t)((t & 0xFFFFull) + (t >> 16));
 }
 __device__ __forceinline__ uint32_t hsum(uint32_t w) { return (w & 0xFFFFu) + (w >> 16); }
+
+// DPP controls (gfx9 encoding): quad_perm, row_half_mirror, row_mirror, row_newbcast
+constexpr int kDppQuadBcast(int k) { return k | (k << 2) | (k << 4) | (k << 6); }
+constexpr int kDppHalfMirror = 0x141, kDppMirror = 0x140, kDppRowNewBcast0 = 0x150;
+
+// value of `x` in lane k of this lane's group of G lanes
+template <int G, int K>
+__device__ __forceinline__ uint32_t group_bcast(uint32_t x, uint32_t grp_base) {
+    if constexpr (G == 4) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppQuadBcast(K), 0xF, 0xF, false);
+    } else if constexpr (G == 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppRowNewBcast0 + K, 0xF, 0xF, false);
+    } else if constexpr (G == 64) {
+        return (uint32_t)__builtin_amdgcn_readlane((int)x, K);
+    } else {
+        return (uint32_t)__shfl((int)x, (int)(grp_base + K), 64);
+    }
+}
+
+// sum of `x` over this lane's group of G lanes, in every lane of the group
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+    if constexpr (G >= 2) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    if constexpr (G >= 4) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    if constexpr (G >= 8) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppHalfMirror, 0xF, 0xF, false);
+    if constexpr (G >= 16) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppMirror, 0xF, 0xF, false);
+    if constexpr (G >= 32) x += (uint32_t)__shfl_xor((int)x, 16, 64);
+    if constexpr (G >= 64) x += (uint32_t)__shfl_xor((int)x, 32, 64);
+    return x;
+}
 
 // Load dwords [d0, d0+4) of a frame that has ndw readable dwords; zero beyond. Never touches a
 // dword past the one holding the frame's last byte (halo_rx.h layout contract).
@@ -202,10 +236,10 @@ __device__ __forceinline__ void frame_at(const RxParams& p, uint64_t i, const ui
     }
 }
 
-// G lanes per frame (G in {4,8,16,32,64}); LAYOUT 0 ragged, 1 strided+lens, 2 strided uniform.
+// G lanes per frame (G in {1,4,8,16,32,64}); LAYOUT 0 ragged, 1 strided+lens, 2 strided uniform.
 template <int G, int LAYOUT>
 __global__ void __launch_bounds__(256) rx_parse_kernel(const RxParams p) {
-    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two in [4,64]");
+    static_assert(G == 1 || (G >= 4 && G <= 64 && (G & (G - 1)) == 0), "G must be 1 or a power of two in [4,64]");
     constexpr uint32_t FPW = 64 / G;  // frames per wave
     constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
@@ -230,48 +264,73 @@ __global__ void __launch_bounds__(256) rx_parse_kernel(const RxParams p) {
         // frames failing the length check are never read (ParseEthFrm looks at no byte)
         const uint32_t ndw = (present && L >= kEthMin && L <= eth_max) ? (L + 3) >> 2 : 0;
 
-        uint32_t w[4];
-        load4(frame, gl * 4, ndw, w);
-
         uint32_t h[12];
-#pragma unroll
-        for (int d = 0; d < 12; ++d) h[d] = __shfl(w[d & 3], (int)(grp_base + (d >> 2)), 64);
-
-        Verdict v = parse_header(h, L, present, p);
-
-        // L4 segment sum over [34, seg_end): first step from registers, then the rest
         uint64_t c = 0;
-        if (v.seg_end) {
-            acc_segment(w, gl * 4, v.seg_end, c);
-            const uint32_t seg_dw = (v.seg_end + 3) >> 2;
-            for (uint32_t d0 = STEP + gl * 4; d0 < seg_dw; d0 += STEP) {
-                uint32_t x[4];
-                load4(frame, d0, seg_dw, x);
-                acc_segment(x, d0, v.seg_end, c);
+        Verdict v;
+        if constexpr (G == 1) {
+            // lane per frame: the header is the lane's own first three 16-byte loads
+            uint32_t a[4], b[4], x[4];
+            load4(frame, 0, ndw, a);
+            load4(frame, 4, ndw, b);
+            load4(frame, 8, ndw, x);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { h[j] = a[j]; h[4 + j] = b[j]; h[8 + j] = x[j]; }
+            v = parse_header(h, L, present, p);
+            if (v.seg_end) {
+                acc_segment(x, 8, v.seg_end, c);
+                const uint32_t seg_dw = (v.seg_end + 3) >> 2;
+                for (uint32_t d0 = 12; d0 < seg_dw; d0 += 4) {
+                    uint32_t y[4];
+                    load4(frame, d0, seg_dw, y);
+                    acc_segment(y, d0, v.seg_end, c);
+                }
+            }
+        } else {
+            uint32_t w[4];
+            load4(frame, gl * 4, ndw, w);
+            // header dwords 0..11 sit in group lanes 0..2 (4 dwords each)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                h[j] = group_bcast<G, 0>(w[j], grp_base);
+                h[4 + j] = group_bcast<G, 1>(w[j], grp_base);
+                h[8 + j] = group_bcast<G, 2>(w[j], grp_base);
+            }
+            v = parse_header(h, L, present, p);
+            // L4 segment sum over [34, seg_end): first step from registers, then the rest
+            if (v.seg_end) {
+                acc_segment(w, gl * 4, v.seg_end, c);
+                const uint32_t seg_dw = (v.seg_end + 3) >> 2;
+                for (uint32_t d0 = STEP + gl * 4; d0 < seg_dw; d0 += STEP) {
+                    uint32_t x[4];
+                    load4(frame, d0, seg_dw, x);
+                    acc_segment(x, d0, v.seg_end, c);
+                }
             }
         }
-        uint32_t c32 = fold64(c);
-#pragma unroll
-        for (int m = 1; m < G; m <<= 1) c32 += __shfl_xor(c32, m, 64);
+        const uint32_t c32 = group_sum<G>(fold64(c));
 
         if (v.status == HALO_RX_OK && v.check_l4 && fold16(c32 + v.l4_extra) != 0xFFFFu)
             v.status = HALO_RX_L4_CKSUM;
         if (v.status == HALO_RX_OK && v.ip_proto != kIpUnknown) finish_l4(h, v);
 
         if (present && gl < 2) {
-            uint4 r;
-            if (gl == 0) {
-                r.x = v.status | (v.flags << 8) | (v.ethertype << 16);
-                r.y = v.ip_proto | (v.l4_aux << 8) | (v.ip_total_len << 16);
-                r.z = v.src_ip;
-                r.w = v.dst_ip;
-            } else {
-                r.x = v.sport | (v.dport << 16);
-                r.y = v.pay_off | (v.pay_len << 16);
-                r.z = v.l4_seq;
-                r.w = v.l4_ack;
+            uint4 lo, hi;
+            lo.x = v.status | (v.flags << 8) | (v.ethertype << 16);
+            lo.y = v.ip_proto | (v.l4_aux << 8) | (v.ip_total_len << 16);
+            lo.z = v.src_ip;
+            lo.w = v.dst_ip;
+            hi.x = v.sport | (v.dport << 16);
+            hi.y = v.pay_off | (v.pay_len << 16);
+            hi.z = v.l4_seq;
+            hi.w = v.l4_ack;
+            uint4* rec = reinterpret_cast<uint4*>(p.out + i);
+            if constexpr (G == 1) {
+                rec[0] = lo;
+                rec[1] = hi;
+            } else {  // lane 0 writes bytes 0..15, lane 1 bytes 16..31 (per-component select: no scratch)
+                const bool h1 = gl != 0;
+                rec[gl] = make_uint4(h1 ? hi.x : lo.x, h1 ? hi.y : lo.y, h1 ? hi.z : lo.z, h1 ? hi.w : lo.w);
             }
-            reinterpret_cast<uint4*>(p.out + i)[gl] = r;
             if (gl == 0) {
                 if (v.status == HALO_RX_OK) ++ok_count;
                 else if (p.hist) atomicAdd(&s_hist[v.status], 1u);
@@ -304,11 +363,14 @@ hipError_t launch_g(const RxParams& p, int layout, hipStream_t s) {
     return hipGetLastError();
 }
 
-// lanes per frame from the longest frame: one 16-byte load per lane covers the frame
+std::atomic<int> g_force_group{0};  // tuning hook (halo_rx_tune_group); 0 = automatic
+
+// lanes per frame from the longest frame (DESIGN.md "Choosing G")
 int pick_group(uint32_t max_len) {
+    const int forced = g_force_group.load(std::memory_order_relaxed);
+    if (forced) return forced;
     if (max_len == 0) return 16;
-    if (max_len <= 64) return 4;
-    if (max_len <= 128) return 8;
+    if (max_len <= 128) return 1;
     if (max_len <= 256) return 16;
     if (max_len <= 512) return 32;
     return 64;
@@ -317,6 +379,7 @@ int pick_group(uint32_t max_len) {
 int launch_parse(const RxParams& p, int layout, uint32_t max_len, hipStream_t s) {
     hipError_t e;
     switch (pick_group(max_len)) {
+        case 1: e = launch_g<1>(p, layout, s); break;
         case 4: e = launch_g<4>(p, layout, s); break;
         case 8: e = launch_g<8>(p, layout, s); break;
         case 16: e = launch_g<16>(p, layout, s); break;
@@ -381,4 +444,12 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
     // the longest frame bounds the group width: uniform length is known, lens[] is not
     const uint32_t max_len = d_lens ? (uint32_t)(stride < 65535 ? stride : 65535) : len;
     return halo::launch_parse(p, d_lens ? 1 : 2, max_len, static_cast<hipStream_t>(stream));
+}
+
+extern "C" HALO_API int halo_rx_tune_group(int lanes_per_frame) {
+    if (lanes_per_frame != 0 && lanes_per_frame != 1 && lanes_per_frame != 4 && lanes_per_frame != 8 &&
+        lanes_per_frame != 16 && lanes_per_frame != 32 && lanes_per_frame != 64)
+        return HALO_E_INVAL;
+    halo::g_force_group.store(lanes_per_frame, std::memory_order_relaxed);
+    return HALO_OK;
 }

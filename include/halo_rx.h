@@ -161,6 +161,10 @@ HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uint64_t strid
                                           halo_rx_result_t* d_out, uint32_t* d_status_hist,
                                           halo_stream_t stream);
 
+/* Tuning hook: force the lanes-per-frame variant (1, 4, 8, 16, 32 or 64; 0 = choose from
+ * max_len_hint). Process-wide; results are identical for every value, only speed changes. */
+HALO_API int halo_rx_tune_group(int lanes_per_frame);
+
 /* ---- host-memory batch parse -----------------------------------
  * Frames in HOST memory (any alignment, ragged byte offsets). Stages them into pinned
  * buffers, copies H2D, runs the kernel and copies results D2H, double-buffered in chunks

@@ -53,17 +53,55 @@ def _parse_ragged(dev, data, offs_dw, lens, flags, hint=0, netif=None):
     return protocol.records(out), hist.cpu().numpy().astype(np.int64)
 
 
+@pytest.fixture
+def lanes_per_frame(request):
+    """Force the kernel variant (G lanes per frame) for one test, restore automatic after."""
+    from halo_amd import _lib
+
+    _lib.check("halo_rx_tune_group", _lib.lib.halo_rx_tune_group(request.param))
+    yield request.param
+    _lib.lib.halo_rx_tune_group(0)
+
+
 @pytest.mark.parametrize("flags", [0, 1, 2, 3])
-@pytest.mark.parametrize("hint", [0, 64, 128, 256, 512, 1514])
-def test_golden_ragged_all_group_widths(dev, golden, flags, hint):
+@pytest.mark.parametrize("lanes_per_frame", [1, 4, 8, 16, 32, 64], indirect=True)
+def test_golden_ragged_all_group_widths(dev, golden, flags, lanes_per_frame):
     from halo_amd._lib import RESULT_DTYPE
 
     meta, blob = golden
     data, offs, lens, names = golden_arrays(meta, blob)
-    got, hist = _parse_ragged(dev, data, offs, lens, flags, hint)
+    got, hist = _parse_ragged(dev, data, offs, lens, flags, 0)
     want = expected_records(meta, flags, RESULT_DTYPE)
-    assert_records_equal(got, want, names, f"GPU ragged flags={flags} hint={hint}")
+    assert_records_equal(got, want, names, f"GPU ragged flags={flags} G={lanes_per_frame}")
     assert np.array_equal(hist, np.bincount(want["status"], minlength=14))
+
+
+@pytest.mark.parametrize("hint", [0, 64, 128, 256, 512, 1514, 9014])
+def test_golden_ragged_auto_variant(dev, golden, hint):
+    from halo_amd._lib import RESULT_DTYPE
+
+    meta, blob = golden
+    data, offs, lens, names = golden_arrays(meta, blob)
+    got, _ = _parse_ragged(dev, data, offs, lens, 3, hint)
+    assert_records_equal(got, expected_records(meta, 3, RESULT_DTYPE), names, f"GPU ragged hint={hint}")
+
+
+@pytest.mark.parametrize("lanes_per_frame", [1, 4, 8, 16, 32, 64], indirect=True)
+def test_random_imix_every_group_width(dev, oracle_lib, lanes_per_frame):
+    """30k IMIX frames, mixed protocols, 1/4 mutated: each kernel variant vs the oracle."""
+    import torch
+
+    from halo_amd import protocol, synth
+    from halo_amd._lib import NetIf
+
+    n = 30_000
+    lay = synth.layout(n, size_mode=1, proto_mode=3, mutate_shift=2, first_index=77_000_000)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev, fill=0x3C)
+    out = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make())
+    torch.cuda.synchronize()
+    want, _ = oracle_lib.rx_batch(fr["bytes"].cpu().numpy(), lay["lens"], oracle_lib.NetIf.make(), 1,
+                                  offsets_dw=lay["offsets_dw"], threads=8)
+    assert_records_equal(protocol.records(out), want, None, f"IMIX G={lanes_per_frame}")
 
 
 def test_golden_gap_bytes_are_ignored(dev, golden):

@@ -27,6 +27,8 @@ for s in "$@"; do
     prof)  step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu --steps 20 ;;
     pmcf)  step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
     pmcw)  step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
+    tune)  step tune 900 python tools/tune.py ;;
+    tuneq) step tuneq 600 python tools/tune.py --quick ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Sweep lanes-per-frame (G) per workload on the GPU: kernel time (HIP events), GB/s of
+algorithmic bytes, and a bit-identity check of every variant against the first one.
+
+    python tools/tune.py [--quick]
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+
+    import bench
+    from halo_amd import _lib
+    from halo_amd._lib import NetIf
+
+    quick = "--quick" in sys.argv
+    _lib.check("init", _lib.lib.halo_rx_init(0))
+    dev = torch.device("cuda:0")
+    netif = NetIf.make()
+    d = bench.Dist()
+    workloads = [
+        ("64B", dict(length=64), 1 << 20, 8, [1, 4, 8, 16]),
+        ("128B", dict(length=128), 1 << 20, 8, [1, 4, 8, 16]),
+        ("570B", dict(length=570), 1 << 20, 2, [1, 8, 16, 32, 64]),
+        ("1500B", dict(length=1500), 1 << 20, 2, [4, 8, 16, 32, 64]),
+        ("imix", dict(size_mode=1, proto_mode=3), 16 << 20, 1, [1, 4, 8, 16, 32, 64]),
+        ("jumbo9000", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, [16, 32, 64]),
+    ]
+    if quick:
+        workloads = workloads[:2] + workloads[3:5]
+    res = {}
+    for name, kw, n, rot, gs in workloads:
+        bs = bench.make_batches(dev, netif, n=n, rotate=rot, rank=0, **kw)
+        out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        strided = kw.get("strided", False)
+        flags = 3 if strided else 1
+        meta = 0 if strided else 6
+        alg = bench.frame_bytes(bs[0]) + n * (meta + 32)
+        ref = None
+        res[name] = {}
+        for g in gs:
+            _lib.check("tune", _lib.lib.halo_rx_tune_group(g))
+            launch = (bench.strided_launcher(bs, out, netif, kw["length"], flags) if strided
+                      else bench.ragged_launcher(bs, out, netif, 0, flags))
+            wall, kms, kmed = bench.time_kernel(launch, 20, 3, d)
+            launch(0)
+            torch.cuda.synchronize()
+            h = torch.sum(out.view(torch.int64).view(-1, 4) * torch.arange(1, 5, device=dev)).item()
+            if ref is None:
+                ref = h
+            ok = h == ref
+            res[name][g] = {"kernel_ms": round(kms, 4), "median_ms": round(kmed, 4),
+                            "GBps": round(alg / kms / 1e6, 1), "Mpps": round(n / kms / 1e3, 1), "same": ok}
+            print(f"{name:10s} G={g:2d} {kms*1e3:9.1f} us  {alg / kms / 1e6:8.1f} GB/s  "
+                  f"{n / kms / 1e3:9.1f} Mpps  {'ok' if ok else 'MISMATCH'}", flush=True)
+        _lib.lib.halo_rx_tune_group(0)
+        del bs, out
+        torch.cuda.empty_cache()
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "tune.json"), "w") as fh:
+        json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
