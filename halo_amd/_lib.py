@@ -90,7 +90,7 @@ _PROTOS = {
     "halo_rx_parse_strided_device": (ctypes.c_int, [
         _u8p, ctypes.c_uint64, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.POINTER(NetIf), _u8p, _u8p, ctypes.c_void_p]),
-    "halo_rx_tune_group": (ctypes.c_int, [ctypes.c_int]),
+    "halo_rx_tune_variant": (ctypes.c_int, [ctypes.c_int]),
     "halo_rx_host_ctx_create": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "halo_rx_host_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),

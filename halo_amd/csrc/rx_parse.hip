@@ -236,155 +236,208 @@ __device__ __forceinline__ void frame_at(const RxParams& p, uint64_t i, const ui
     }
 }
 
-// G lanes per frame (G in {1,4,8,16,32,64}); LAYOUT 0 ragged, 1 strided+lens, 2 strided uniform.
+// Per-block status histogram: OK frames are counted per lane, the rest in LDS.
+struct Hist {
+    uint32_t* s;  // __shared__ [HALO_RX_STATUS_COUNT]
+    uint32_t ok;
+    __device__ __forceinline__ void add(uint32_t status) {
+        if (status == HALO_RX_OK) ++ok;
+        else atomicAdd(&s[status], 1u);
+    }
+};
+
+// The whole chain for frame i on a group of G lanes (G = 1: one lane, no cross-lane traffic).
+// Every lane of the group must call it with the same i / present (lanes of other groups may
+// be doing the same for other frames); `present` false means "no frame": nothing is read or
+// written, but the group still executes the collective steps.
 template <int G, int LAYOUT>
-__global__ void __launch_bounds__(256) rx_parse_kernel(const RxParams p) {
-    static_assert(G == 1 || (G >= 4 && G <= 64 && (G & (G - 1)) == 0), "G must be 1 or a power of two in [4,64]");
-    constexpr uint32_t FPW = 64 / G;  // frames per wave
+__device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, bool present, uint32_t gl,
+                                              uint32_t grp_base, Hist& hist) {
     constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
+    constexpr int U = 4;              // 16-byte chunks in flight per lane per round
+    const uint32_t eth_max = (p.flags & HALO_RX_JUMBO_EXT) ? kEthMaxJumbo : kEthMax;
+    const uint8_t* frame = p.bytes;
+    uint32_t L = 0;
+    if (present) frame_at<LAYOUT>(p, i, frame, L);
+    // frames failing the length check are never read (ParseEthFrm looks at no byte)
+    const uint32_t ndw = (present && L >= kEthMin && L <= eth_max) ? (L + 3) >> 2 : 0;
+
+    // Round 0: U 16-byte chunks per lane issued back to back, bounded by the frame length (the
+    // L4 end is not known before the header is parsed, and never exceeds the frame length).
+    uint32_t buf[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load4(frame, (u * G + gl) * 4, ndw, buf[u]);
+    uint32_t h[12];
+    if constexpr (G == 1) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) h[j] = buf[j >> 2][j & 3];  // the lane's own frame
+    } else {
+        // header dwords 0..11 sit in chunk 0 of group lanes 0..2
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            h[j] = group_bcast<G, 0>(buf[0][j], grp_base);
+            h[4 + j] = group_bcast<G, 1>(buf[0][j], grp_base);
+            h[8 + j] = group_bcast<G, 2>(buf[0][j], grp_base);
+        }
+    }
+    Verdict v = parse_header(h, L, present, p);
+
+    // L4 segment sum over [34, seg_end): round 0 from registers, then U chunks per round
+    uint64_t c = 0;
+    if (v.seg_end) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc_segment(buf[u], (u * G + gl) * 4, v.seg_end, c);
+        const uint32_t seg_dw = (v.seg_end + 3) >> 2;
+        for (uint32_t r0 = U * STEP; r0 < seg_dw; r0 += U * STEP) {
+            uint32_t x[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load4(frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc_segment(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
+        }
+    }
+    const uint32_t c32 = group_sum<G>(fold64(c));
+    if (v.status == HALO_RX_OK && v.check_l4 && fold16(c32 + v.l4_extra) != 0xFFFFu) v.status = HALO_RX_L4_CKSUM;
+    if (v.status == HALO_RX_OK && v.ip_proto != kIpUnknown) finish_l4(h, v);
+
+    if (present && gl < 2) {
+        uint4 lo, hi;
+        lo.x = v.status | (v.flags << 8) | (v.ethertype << 16);
+        lo.y = v.ip_proto | (v.l4_aux << 8) | (v.ip_total_len << 16);
+        lo.z = v.src_ip;
+        lo.w = v.dst_ip;
+        hi.x = v.sport | (v.dport << 16);
+        hi.y = v.pay_off | (v.pay_len << 16);
+        hi.z = v.l4_seq;
+        hi.w = v.l4_ack;
+        uint4* rec = reinterpret_cast<uint4*>(p.out + i);
+        if constexpr (G == 1) {
+            rec[0] = lo;
+            rec[1] = hi;
+        } else {  // lane 0 writes bytes 0..15, lane 1 bytes 16..31 (per-component select: no scratch)
+            const bool h1 = gl != 0;
+            rec[gl] = make_uint4(h1 ? hi.x : lo.x, h1 ? hi.y : lo.y, h1 ? hi.z : lo.z, h1 ? hi.w : lo.w);
+        }
+        if (gl == 0 && p.hist) hist.add(v.status);
+    }
+}
+
+__device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
+    if (!p.hist) return;
+    uint32_t ok = hist.ok;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) ok += __shfl_xor(ok, m, 64);
+    if ((threadIdx.x & 63u) == 0 && ok) atomicAdd(&hist.s[HALO_RX_OK], ok);
+    __syncthreads();
+    if (threadIdx.x < HALO_RX_STATUS_COUNT && hist.s[threadIdx.x]) atomicAdd(&p.hist[threadIdx.x], hist.s[threadIdx.x]);
+}
+
+// Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
+template <int G, int LAYOUT>
+__global__ void __launch_bounds__(256) rx_group_kernel(const RxParams p) {
+    static_assert(G == 1 || G == 4 || G == 8 || G == 16, "G must be 1, 4, 8 or 16");
+    constexpr uint32_t FPW = 64 / G;  // frames per wave
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
-
+    Hist hist{s_hist, 0};
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp_base = lane & ~(uint32_t)(G - 1);
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const bool jumbo = (p.flags & HALO_RX_JUMBO_EXT) != 0;
-    const uint32_t eth_max = jumbo ? kEthMaxJumbo : kEthMax;
-    uint32_t ok_count = 0;
-
     for (uint64_t base = wave * FPW; base < p.n; base += nwaves * FPW) {
         const uint64_t i = base + lane / G;
-        const bool present = i < p.n;
-        const uint8_t* frame = p.bytes;
-        uint32_t L = 0;
-        if (present) frame_at<LAYOUT>(p, i, frame, L);
-        // frames failing the length check are never read (ParseEthFrm looks at no byte)
-        const uint32_t ndw = (present && L >= kEthMin && L <= eth_max) ? (L + 3) >> 2 : 0;
-
-        uint32_t h[12];
-        uint64_t c = 0;
-        Verdict v;
-        if constexpr (G == 1) {
-            // lane per frame: the header is the lane's own first three 16-byte loads
-            uint32_t a[4], b[4], x[4];
-            load4(frame, 0, ndw, a);
-            load4(frame, 4, ndw, b);
-            load4(frame, 8, ndw, x);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) { h[j] = a[j]; h[4 + j] = b[j]; h[8 + j] = x[j]; }
-            v = parse_header(h, L, present, p);
-            if (v.seg_end) {
-                acc_segment(x, 8, v.seg_end, c);
-                const uint32_t seg_dw = (v.seg_end + 3) >> 2;
-                for (uint32_t d0 = 12; d0 < seg_dw; d0 += 4) {
-                    uint32_t y[4];
-                    load4(frame, d0, seg_dw, y);
-                    acc_segment(y, d0, v.seg_end, c);
-                }
-            }
-        } else {
-            uint32_t w[4];
-            load4(frame, gl * 4, ndw, w);
-            // header dwords 0..11 sit in group lanes 0..2 (4 dwords each)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                h[j] = group_bcast<G, 0>(w[j], grp_base);
-                h[4 + j] = group_bcast<G, 1>(w[j], grp_base);
-                h[8 + j] = group_bcast<G, 2>(w[j], grp_base);
-            }
-            v = parse_header(h, L, present, p);
-            // L4 segment sum over [34, seg_end): first step from registers, then the rest
-            if (v.seg_end) {
-                acc_segment(w, gl * 4, v.seg_end, c);
-                const uint32_t seg_dw = (v.seg_end + 3) >> 2;
-                for (uint32_t d0 = STEP + gl * 4; d0 < seg_dw; d0 += STEP) {
-                    uint32_t x[4];
-                    load4(frame, d0, seg_dw, x);
-                    acc_segment(x, d0, v.seg_end, c);
-                }
-            }
-        }
-        const uint32_t c32 = group_sum<G>(fold64(c));
-
-        if (v.status == HALO_RX_OK && v.check_l4 && fold16(c32 + v.l4_extra) != 0xFFFFu)
-            v.status = HALO_RX_L4_CKSUM;
-        if (v.status == HALO_RX_OK && v.ip_proto != kIpUnknown) finish_l4(h, v);
-
-        if (present && gl < 2) {
-            uint4 lo, hi;
-            lo.x = v.status | (v.flags << 8) | (v.ethertype << 16);
-            lo.y = v.ip_proto | (v.l4_aux << 8) | (v.ip_total_len << 16);
-            lo.z = v.src_ip;
-            lo.w = v.dst_ip;
-            hi.x = v.sport | (v.dport << 16);
-            hi.y = v.pay_off | (v.pay_len << 16);
-            hi.z = v.l4_seq;
-            hi.w = v.l4_ack;
-            uint4* rec = reinterpret_cast<uint4*>(p.out + i);
-            if constexpr (G == 1) {
-                rec[0] = lo;
-                rec[1] = hi;
-            } else {  // lane 0 writes bytes 0..15, lane 1 bytes 16..31 (per-component select: no scratch)
-                const bool h1 = gl != 0;
-                rec[gl] = make_uint4(h1 ? hi.x : lo.x, h1 ? hi.y : lo.y, h1 ? hi.z : lo.z, h1 ? hi.w : lo.w);
-            }
-            if (gl == 0) {
-                if (v.status == HALO_RX_OK) ++ok_count;
-                else if (p.hist) atomicAdd(&s_hist[v.status], 1u);
-            }
-        }
+        process_frame<G, LAYOUT>(p, i, i < p.n, gl, grp_base, hist);
     }
-    if (p.hist) {
-#pragma unroll
-        for (int m = 1; m < 64; m <<= 1) ok_count += __shfl_xor(ok_count, m, 64);
-        if (lane == 0 && ok_count) atomicAdd(&s_hist[HALO_RX_OK], ok_count);
-        __syncthreads();
-        if (threadIdx.x < HALO_RX_STATUS_COUNT && s_hist[threadIdx.x])
-            atomicAdd(&p.hist[threadIdx.x], s_hist[threadIdx.x]);
-    }
+    flush_hist(p, hist);
 }
 
-template <int G>
-hipError_t launch_g(const RxParams& p, int layout, hipStream_t s) {
-    constexpr uint32_t FPW = 64 / G;
-    const uint64_t waves = (p.n + FPW - 1) / FPW;
+// Mixed-size batches (IMIX): each wave takes a tile of 64 consecutive frames. Frames of at most
+// 64 bytes (or failing the length check) are done lane-per-frame in place; the tile's longer
+// frames are then compacted (ballot rank -> LDS) and done 8 at a time by 8-lane groups, so no
+// lane idles behind a 1500-byte neighbour and no global workspace is needed.
+template <int LAYOUT>
+__global__ void __launch_bounds__(256) rx_tile_kernel(const RxParams p) {
+    constexpr int GL = 8;  // lanes per long frame
+    __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
+    __shared__ uint8_t s_slot[4][64];  // per wave: tile-local index of the k-th long frame
+    if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    Hist hist{s_hist, 0};
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wib = threadIdx.x >> 6;  // wave in block
+    const uint32_t eth_max = (p.flags & HALO_RX_JUMBO_EXT) ? kEthMaxJumbo : kEthMax;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t base = wave * 64; base < p.n; base += nwaves * 64) {
+        const uint64_t i = base + lane;
+        const bool present = i < p.n;
+        uint32_t L = 0;
+        if (present) L = LAYOUT == 2 ? p.len : p.lens[i];
+        const bool is_long = present && L > 64 && L <= eth_max;
+        if (!is_long) process_frame<1, LAYOUT>(p, i, present, 0, lane, hist);
+        const uint64_t long_mask = __ballot(is_long);
+        if (long_mask == 0) continue;
+        const uint32_t nlong = (uint32_t)__popcll(long_mask);
+        if (is_long) s_slot[wib][__builtin_amdgcn_mbcnt_hi((uint32_t)(long_mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)long_mask, 0u))] = (uint8_t)lane;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (uint32_t k0 = 0; k0 < nlong; k0 += 64 / GL) {
+            const uint32_t k = k0 + lane / GL;
+            const bool has = k < nlong;
+            const uint32_t t = has ? s_slot[wib][k] : 0u;
+            process_frame<GL, LAYOUT>(p, base + t, has, lane & (GL - 1), lane & ~(uint32_t)(GL - 1), hist);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    flush_hist(p, hist);
+}
+
+constexpr int kVariantTile = -1;
+std::atomic<int> g_force_variant{0};  // tuning hook (halo_rx_tune_variant); 0 = automatic
+
+uint32_t grid_for(uint64_t n, uint32_t frames_per_wave) {
+    const uint64_t waves = (n + frames_per_wave - 1) / frames_per_wave;
     uint64_t blocks = (waves + 3) / 4;
     const uint64_t kMaxBlocks = 256ull * 8 * 8;  // 256 CUs x 8 resident blocks x 8 rounds
-    if (blocks > kMaxBlocks) blocks = kMaxBlocks;
-    const dim3 grid((uint32_t)blocks), block(256);
-    switch (layout) {
-        case 0: hipLaunchKernelGGL((rx_parse_kernel<G, 0>), grid, block, 0, s, p); break;
-        case 1: hipLaunchKernelGGL((rx_parse_kernel<G, 1>), grid, block, 0, s, p); break;
-        default: hipLaunchKernelGGL((rx_parse_kernel<G, 2>), grid, block, 0, s, p); break;
+    return (uint32_t)(blocks > kMaxBlocks ? kMaxBlocks : blocks);
+}
+
+template <int LAYOUT>
+hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
+    const dim3 block(256);
+    switch (variant) {
+        case 1: hipLaunchKernelGGL((rx_group_kernel<1, LAYOUT>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
+        case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
+        case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
+        case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
+        default: hipLaunchKernelGGL((rx_tile_kernel<LAYOUT>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
     }
     return hipGetLastError();
 }
 
-std::atomic<int> g_force_group{0};  // tuning hook (halo_rx_tune_group); 0 = automatic
-
-// lanes per frame from the longest frame (DESIGN.md "Choosing G")
-int pick_group(uint32_t max_len) {
-    const int forced = g_force_group.load(std::memory_order_relaxed);
+// Kernel variant (DESIGN.md "Choosing the variant", from the G sweep in profiles/):
+// a known uniform length picks the best lanes-per-frame; otherwise frames of at most 64 B
+// go lane-per-frame and anything longer or mixed goes to the tile kernel.
+int pick_variant(uint32_t max_len, bool uniform) {
+    const int forced = g_force_variant.load(std::memory_order_relaxed);
     if (forced) return forced;
-    if (max_len == 0) return 16;
-    if (max_len <= 128) return 1;
-    if (max_len <= 256) return 16;
-    if (max_len <= 512) return 32;
-    return 64;
+    if (max_len != 0 && max_len <= 64) return 1;
+    if (!uniform) return kVariantTile;
+    if (max_len <= 640) return 4;
+    if (max_len <= 2048) return 8;
+    return 16;
 }
 
-int launch_parse(const RxParams& p, int layout, uint32_t max_len, hipStream_t s) {
+int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, hipStream_t s) {
+    const int v = pick_variant(max_len, uniform);
     hipError_t e;
-    switch (pick_group(max_len)) {
-        case 1: e = launch_g<1>(p, layout, s); break;
-        case 4: e = launch_g<4>(p, layout, s); break;
-        case 8: e = launch_g<8>(p, layout, s); break;
-        case 16: e = launch_g<16>(p, layout, s); break;
-        case 32: e = launch_g<32>(p, layout, s); break;
-        default: e = launch_g<64>(p, layout, s); break;
+    switch (layout) {
+        case 0: e = launch_variant<0>(p, v, s); break;
+        case 1: e = launch_variant<1>(p, v, s); break;
+        default: e = launch_variant<2>(p, v, s); break;
     }
     return e == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
@@ -422,7 +475,7 @@ extern "C" HALO_API int halo_rx_parse_batch_device(const uint8_t* d_bytes, const
     p.bytes = d_bytes;
     p.offsets_dw = d_offsets_dw;
     p.lens = d_lens;
-    return halo::launch_parse(p, 0, max_len_hint, static_cast<hipStream_t>(stream));
+    return halo::launch_parse(p, 0, max_len_hint, false, static_cast<hipStream_t>(stream));
 }
 
 extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uint64_t stride,
@@ -441,15 +494,14 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
     p.lens = d_lens;
     p.stride = stride;
     p.len = len;
-    // the longest frame bounds the group width: uniform length is known, lens[] is not
+    // with per-frame lengths only the stride bounds them (mixed sizes possible)
     const uint32_t max_len = d_lens ? (uint32_t)(stride < 65535 ? stride : 65535) : len;
-    return halo::launch_parse(p, d_lens ? 1 : 2, max_len, static_cast<hipStream_t>(stream));
+    return halo::launch_parse(p, d_lens ? 1 : 2, max_len, d_lens == nullptr, static_cast<hipStream_t>(stream));
 }
 
-extern "C" HALO_API int halo_rx_tune_group(int lanes_per_frame) {
-    if (lanes_per_frame != 0 && lanes_per_frame != 1 && lanes_per_frame != 4 && lanes_per_frame != 8 &&
-        lanes_per_frame != 16 && lanes_per_frame != 32 && lanes_per_frame != 64)
+extern "C" HALO_API int halo_rx_tune_variant(int variant) {
+    if (variant != 0 && variant != 1 && variant != 4 && variant != 8 && variant != 16 && variant != -1)
         return HALO_E_INVAL;
-    halo::g_force_group.store(lanes_per_frame, std::memory_order_relaxed);
+    halo::g_force_variant.store(variant, std::memory_order_relaxed);
     return HALO_OK;
 }

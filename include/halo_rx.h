@@ -161,9 +161,11 @@ HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uint64_t strid
                                           halo_rx_result_t* d_out, uint32_t* d_status_hist,
                                           halo_stream_t stream);
 
-/* Tuning hook: force the lanes-per-frame variant (1, 4, 8, 16, 32 or 64; 0 = choose from
- * max_len_hint). Process-wide; results are identical for every value, only speed changes. */
-HALO_API int halo_rx_tune_group(int lanes_per_frame);
+/* Tuning hook: force the kernel variant process-wide. 1, 4, 8, 16 = that many lanes per frame
+ * for every frame; -1 = tile kernel (lane-per-frame for frames <= 64 B, compacted 8-lane
+ * groups for longer ones); 0 = automatic (from max_len_hint / the uniform length).
+ * Results are identical for every value; only speed changes. */
+HALO_API int halo_rx_tune_variant(int variant);
 
 /* ---- host-memory batch parse -----------------------------------
  * Frames in HOST memory (any alignment, ragged byte offsets). Stages them into pinned

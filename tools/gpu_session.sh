@@ -28,6 +28,11 @@ for s in "$@"; do
     pmcf)  step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
     pmcw)  step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 ;;
     tune)  step tune 900 python tools/tune.py ;;
+    list)  step counters 300 rocprofv3 -L ;;
+    kt)    step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 tools/prof_kernels.py ;;
+    kfetch) step kfetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/kfetch" -o run -- python3 tools/prof_kernels.py ;;
+    kwrite) step kwrite 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/kwrite" -o run -- python3 tools/prof_kernels.py ;;
+    ksq)   step ksq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ksq" -o run -- python3 tools/prof_kernels.py ;;
     tuneq) step tuneq 600 python tools/tune.py --quick ;;
     *) echo "unknown step $s" ;;
   esac

@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_session.sh profiling session (kt, kfetch, kwrite, ksq steps) into
+per-workload numbers and write profiles/pmc_summary.json (read by bench.py for `traffic`).
+
+    python tools/pmc_summary.py gpurun_out/<tag> [--out profiles/pmc_summary.json]
+
+rx_* dispatches are attributed to tools/prof_kernels.py's WORKLOADS in launch order.
+HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from separate
+--pmc passes; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced streaming read,
+so read bytes = 2 x FETCH_SIZE x 1024 (the calibration column checks that against the bytes
+each launch must read: frames + metadata).
+"""
+from __future__ import annotations
+
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _rows(path):
+    if not os.path.exists(path):
+        return []
+    with open(path) as fh:
+        return list(csv.DictReader(fh))
+
+
+def alg_bytes():
+    """(read bytes, written bytes) per launch for each profiled workload."""
+    from halo_amd import synth
+    from tools.prof_kernels import WORKLOADS
+
+    out = {}
+    for name, kw, n, _rot, _launches, slen, _flags, _hint in WORKLOADS:
+        kw = dict(kw)
+        kw.pop("strided", None)
+        lay = synth.layout(n, **kw, ragged=not slen)
+        frames = int(lay["lens"].astype("int64").sum())
+        meta = 0 if slen else 6 * n
+        out[name] = (frames + meta, 32 * n)
+    return out
+
+
+def main():
+    sess = sys.argv[1]
+    out_path = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else os.path.join(
+        ROOT, "profiles", "pmc_summary.json")
+    from tools.prof_kernels import WORKLOADS
+
+    order = []
+    for name, _kw, _n, _rot, launches, *_ in WORKLOADS:
+        order += [name] * launches
+
+    def attribute(rows, key="Dispatch_Id"):
+        disp = sorted({int(r[key]) for r in rows if "rx_" in r["Kernel_Name"]})
+        return {d: order[k] for k, d in enumerate(disp) if k < len(order)}
+
+    res = defaultdict(lambda: defaultdict(list))
+    kt = _rows(os.path.join(sess, "kt", "run_kernel_trace.csv"))
+    amap = attribute(kt)
+    for r in kt:
+        d = int(r["Dispatch_Id"])
+        if d in amap:
+            w = amap[d]
+            res[w]["duration_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            res[w]["kernel"] = [r["Kernel_Name"]]
+            res[w]["vgpr"] = [int(r["VGPR_Count"])]
+            res[w]["sgpr"] = [int(r["SGPR_Count"])]
+    for step in ("kfetch", "kwrite", "ksq"):
+        rows = _rows(os.path.join(sess, step, "run_counter_collection.csv"))
+        amap = attribute(rows)
+        per = defaultdict(dict)
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            if d in amap:
+                per[d][r["Counter_Name"]] = per[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        for d, cs in per.items():
+            for c, v in cs.items():
+                res[amap[d]][c].append(v)
+    algs = alg_bytes()
+    summary = {}
+    for w, m in res.items():
+        avg = {k: (sum(v) / len(v) if v and not isinstance(v[0], str) else v[0]) for k, v in m.items()}
+        rd_alg, wr_alg = algs[w]
+        s = {"kernel": avg.get("kernel"), "vgpr": avg.get("vgpr"), "sgpr": avg.get("sgpr"),
+             "launches": len(m.get("duration_ns", [])),
+             "avg_duration_us": round(avg["duration_ns"] / 1e3, 3) if "duration_ns" in avg else None,
+             "alg_read_bytes": rd_alg, "alg_write_bytes": wr_alg}
+        if "duration_ns" in avg:
+            s["alg_GBps"] = round((rd_alg + wr_alg) / avg["duration_ns"], 1)
+        if "FETCH_SIZE" in avg:
+            raw = avg["FETCH_SIZE"] * 1024
+            s["fetch_bytes_raw"] = int(raw)
+            s["fetch_bytes_corrected_x2"] = int(2 * raw)
+            s["fetch_over_alg_read_raw"] = round(raw / rd_alg, 3)
+        if "WRITE_SIZE" in avg:
+            s["write_bytes"] = int(avg["WRITE_SIZE"] * 1024)
+            s["write_over_alg"] = round(avg["WRITE_SIZE"] * 1024 / wr_alg, 3)
+        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+            s["hbm_bytes_per_launch"] = int(2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024)
+        for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS",
+                  "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT"):
+            if c in avg:
+                s[c] = avg[c]
+        if "SQ_WAVES" in avg and avg["SQ_WAVES"]:
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS"):
+                if c in avg:
+                    s[c + "_per_wave"] = round(avg[c] / avg["SQ_WAVES"], 1)
+        if "SQ_WAIT_ANY" in avg and avg.get("SQ_WAVE_CYCLES"):
+            s["wait_frac"] = round(avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"], 3)
+        if "GRBM_GUI_ACTIVE" in avg and "duration_ns" in avg:
+            s["eff_clock_GHz"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / avg["duration_ns"], 3)
+        summary[w] = s
+    os.makedirs(os.path.dirname(out_path), exist_ok=True)
+    with open(out_path, "w") as fh:
+        json.dump({"session": os.path.basename(sess.rstrip("/")), **summary}, fh, indent=1)
+    for w, s in summary.items():
+        print(w, json.dumps(s))
+
+
+if __name__ == "__main__":
+    main()

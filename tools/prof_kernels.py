@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Launch each hot-path workload a fixed number of times for rocprofv3 (kernel trace / PMC).
+
+    rocprofv3 --kernel-trace --stats -d OUT -o run -- python3 tools/prof_kernels.py
+    rocprofv3 --pmc FETCH_SIZE -d OUT -o run -- python3 tools/prof_kernels.py
+
+Workloads run in a fixed order, each with its own kernel variant, so per-dispatch rows can be
+attributed by order (see tools/pmc_summary.py).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# name, synth kwargs, frames, rotating batches, launches, strided length (0 = ragged), flags, hint
+WORKLOADS = [
+    ("config2", dict(length=64), 1 << 20, 8, 20, 0, 1, 64),
+    ("1500B_udp_1M", dict(length=1500), 1 << 20, 2, 10, 0, 1, 1500),
+    ("config3_imix_16M", dict(size_mode=1, proto_mode=3), 16 << 20, 1, 5, 0, 1, 1500),
+    ("config5_jumbo_9000B_tcp_4M_ext", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, 3, 9000, 3, 0),
+]
+
+
+def main():
+    import torch
+
+    import bench
+    from halo_amd import _lib
+    from halo_amd._lib import NetIf
+
+    only = sys.argv[1:]
+    _lib.check("init", _lib.lib.halo_rx_init(0))
+    dev = torch.device("cuda:0")
+    netif = NetIf.make()
+    for name, kw, n, rot, launches, slen, flags, hint in WORKLOADS:
+        if only and name not in only:
+            continue
+        bs = bench.make_batches(dev, netif, n=n, rotate=rot, rank=0, **kw)
+        out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        launch = (bench.strided_launcher(bs, out, netif, slen, flags) if slen
+                  else bench.ragged_launcher(bs, out, netif, hint, flags))
+        for i in range(launches):
+            launch(i)
+        torch.cuda.synchronize()
+        print(f"{name}: {launches} launches of {n} frames", flush=True)
+        del bs, out
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

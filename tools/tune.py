@@ -27,12 +27,12 @@ def main():
     netif = NetIf.make()
     d = bench.Dist()
     workloads = [
-        ("64B", dict(length=64), 1 << 20, 8, [1, 4, 8, 16]),
-        ("128B", dict(length=128), 1 << 20, 8, [1, 4, 8, 16]),
-        ("570B", dict(length=570), 1 << 20, 2, [1, 8, 16, 32, 64]),
-        ("1500B", dict(length=1500), 1 << 20, 2, [4, 8, 16, 32, 64]),
-        ("imix", dict(size_mode=1, proto_mode=3), 16 << 20, 1, [1, 4, 8, 16, 32, 64]),
-        ("jumbo9000", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, [16, 32, 64]),
+        ("64B", dict(length=64), 1 << 20, 8, [1, 4, -1]),
+        ("128B", dict(length=128), 1 << 20, 8, [1, 4, 8, -1]),
+        ("570B", dict(length=570), 1 << 20, 2, [4, 8, 16, -1]),
+        ("1500B", dict(length=1500), 1 << 20, 2, [4, 8, 16, -1]),
+        ("imix", dict(size_mode=1, proto_mode=3), 16 << 20, 1, [1, 4, 8, -1]),
+        ("jumbo9000", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, [8, 16, -1]),
     ]
     if quick:
         workloads = workloads[:2] + workloads[3:5]
@@ -48,7 +48,7 @@ def main():
         ref = None
         res[name] = {}
         for g in gs:
-            _lib.check("tune", _lib.lib.halo_rx_tune_group(g))
+            _lib.check("tune", _lib.lib.halo_rx_tune_variant(g))
             launch = (bench.strided_launcher(bs, out, netif, kw["length"], flags) if strided
                       else bench.ragged_launcher(bs, out, netif, 0, flags))
             wall, kms, kmed = bench.time_kernel(launch, 20, 3, d)
@@ -60,9 +60,9 @@ def main():
             ok = h == ref
             res[name][g] = {"kernel_ms": round(kms, 4), "median_ms": round(kmed, 4),
                             "GBps": round(alg / kms / 1e6, 1), "Mpps": round(n / kms / 1e3, 1), "same": ok}
-            print(f"{name:10s} G={g:2d} {kms*1e3:9.1f} us  {alg / kms / 1e6:8.1f} GB/s  "
+            print(f"{name:10s} V={g:2d} {kms*1e3:9.1f} us  {alg / kms / 1e6:8.1f} GB/s  "
                   f"{n / kms / 1e3:9.1f} Mpps  {'ok' if ok else 'MISMATCH'}", flush=True)
-        _lib.lib.halo_rx_tune_group(0)
+        _lib.lib.halo_rx_tune_variant(0)
         del bs, out
         torch.cuda.empty_cache()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
