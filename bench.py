@@ -40,8 +40,8 @@ def log(*a):
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per batch per GPU")
     p.add_argument("--rotate", type=int, default=8, help="distinct batches cycled through")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -105,57 +105,59 @@ def frame_bytes(fr) -> int:
     return int(fr["layout"]["lens"].astype("int64").sum())
 
 
-def time_kernel(launch, steps, warmup, d: Dist):
-    """Wall time of `steps` launches (barrier + sync both sides) and per-launch HIP-event
-    kernel time on the launch stream (torch's current stream, which the C ABI is given)."""
+_BENCH_LIB = None
+
+
+def bench_lib():
+    """tools/libhalo_bench.so: the native step loop (built on demand if missing)."""
+    global _BENCH_LIB
+    if _BENCH_LIB is None:
+        import ctypes
+        import importlib.util
+
+        spec = importlib.util.spec_from_file_location("halo_build", os.path.join(ROOT, "halo_amd", "build.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        if not os.path.exists(mod.BENCH_OUT):
+            mod.build_bench()
+        L = ctypes.CDLL(mod.BENCH_OUT)
+        vp = ctypes.c_void_p
+        L.halo_bench_steps.restype = ctypes.c_int
+        L.halo_bench_steps.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                       ctypes.c_uint32, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp,
+                                       ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
+        _BENCH_LIB = L
+    return _BENCH_LIB
+
+
+def time_steps(batches, out, netif, *, flags, hint, steps, warmup, d: Dist, strided_len: int = 0):
+    """`steps` hot-path launches, one per batch (cycling), issued back to back by the native loop
+    on torch's current stream. Barrier + device sync on both sides. One HIP event pair on that
+    stream brackets the timed region. Returns (max-over-ranks wall seconds, average launch
+    duration in ms = event elapsed / steps)."""
+    import ctypes
+
     import torch
 
-    for i in range(warmup):
-        launch(i)
+    from halo_amd import _lib
+
+    nb = len(batches)
+    arr = lambda xs: (ctypes.c_void_p * nb)(*xs)  # noqa: E731
+    b_bytes = arr([b["bytes"].data_ptr() for b in batches])
+    b_offs = None if strided_len else arr([b["offsets_dw"].data_ptr() for b in batches])
+    b_lens = None if strided_len else arr([b["lens"].data_ptr() for b in batches])
+    region = ctypes.c_float()
+    wall = ctypes.c_double()
     torch.cuda.synchronize()
     d.barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    t0 = time.perf_counter()
-    for i in range(steps):
-        ev[i][0].record()
-        launch(i)
-        ev[i][1].record()
+    rc = bench_lib().halo_bench_steps(nb, b_bytes, b_offs, b_lens, batches[0]["layout"]["n"], strided_len,
+                                      strided_len, flags, ctypes.addressof(netif), hint, out.data_ptr(), warmup,
+                                      steps, torch.cuda.current_stream().cuda_stream, ctypes.byref(region),
+                                      ctypes.byref(wall))
+    _lib.check("halo_bench_steps", rc)
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
     d.barrier()
-    kern = sorted(a.elapsed_time(b) for a, b in ev)
-    return d.max(wall), sum(kern) / len(kern), kern[len(kern) // 2]
-
-
-def ragged_launcher(batches, out, netif, hint, flags=1):
-    from halo_amd import _lib
-    import torch
-
-    L = _lib.lib
-
-    def launch(i):
-        fr = batches[i % len(batches)]
-        rc = L.halo_rx_parse_batch_device(fr["bytes"].data_ptr(), fr["offsets_dw"].data_ptr(),
-                                          fr["lens"].data_ptr(), fr["layout"]["n"], flags, netif, hint,
-                                          out.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
-        if rc:
-            raise _lib.HaloError("halo_rx_parse_batch_device", rc)
-    return launch
-
-
-def strided_launcher(batches, out, netif, length, flags):
-    from halo_amd import _lib
-    import torch
-
-    L = _lib.lib
-
-    def launch(i):
-        fr = batches[i % len(batches)]
-        rc = L.halo_rx_parse_strided_device(fr["bytes"].data_ptr(), length, None, length, fr["layout"]["n"], flags,
-                                            netif, out.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
-        if rc:
-            raise _lib.HaloError("halo_rx_parse_strided_device", rc)
-    return launch
+    return d.max(wall.value), region.value / steps
 
 
 def roofline(alg_bytes_per_launch, kernel_ms, traffic=None):
@@ -231,7 +233,7 @@ def main():
     batches = make_batches(dev, netif, n=n, rotate=args.rotate, rank=d.rank)
     out = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    wall, kern_ms, kern_med = time_kernel(ragged_launcher(batches, out, netif, 64), args.steps, args.warmup, d)
+    wall, kern_ms = time_steps(batches, out, netif, flags=1, hint=64, steps=args.steps, warmup=args.warmup, d=d)
     frames_total = n * args.steps * d.world
     mpps = frames_total / wall / 1e6
     fbytes = frame_bytes(batches[0])
@@ -246,21 +248,31 @@ def main():
                    "frames_per_gpu_per_step": n, "frame_bytes": 64, "rotating_batches": args.rotate,
                    "parallelism": f"index-sharded x{d.world}, no collective"},
         "gbit_s": round(gbit, 2),
-        "kernel_ms": round(kern_ms, 5), "kernel_ms_median": round(kern_med, 5),
-        "kernel": "rx_parse_kernel<G=4,ragged>",
+        "kernel_ms": round(kern_ms, 5),
+        "kernel": "rx_group_kernel<1,0> (lane per frame, ragged)",
         "roofline": roofline(alg, kern_ms, load_traffic("config2")),
         "alg_bytes_per_launch": alg,
         "cpu_baseline": None,
     }
-    line["roofline"]["note"] = ("achieved = (frame bytes + 6 B metadata + 32 B record) per launch / HIP-event "
-                                "kernel time; peak = HBM3E spec")
+    line["roofline"]["note"] = ("achieved = (frame bytes + 6 B metadata + 32 B record) per launch / average "
+                                "launch duration (one HIP event pair over the timed region / steps); "
+                                "peak = HBM3E spec; traffic = 2 x FETCH_SIZE + WRITE_SIZE per launch from "
+                                "profiles/pmc_summary.json")
 
     if d.world == 1 and not args.no_secondary:
         sec = {}
         # cache-resident variant of the headline (one batch, 102 MB < 256 MB Infinity Cache)
-        w1, k1, _ = time_kernel(ragged_launcher(batches[:1], out, netif, 64), args.steps, args.warmup, d)
+        w1, k1 = time_steps(batches[:1], out, netif, flags=1, hint=64, steps=args.steps, warmup=args.warmup, d=d)
         sec["config2_mall_resident"] = {"mpps": round(n * args.steps / w1 / 1e6, 1), "kernel_ms": round(k1, 5),
                                         "roofline": roofline(alg, k1)}
+        # the same headline workload writing the compact 16 B record (verdict + 5-tuple only)
+        from halo_amd._lib import HALO_RX_RECORD_COMPACT
+
+        wc, kc = time_steps(batches, out, netif, flags=1 | HALO_RX_RECORD_COMPACT, hint=64, steps=args.steps,
+                            warmup=args.warmup, d=d)
+        algc = fbytes + n * (4 + 2 + 16)
+        sec["config2_compact_record16"] = {"mpps": round(n * args.steps / wc / 1e6, 1), "kernel_ms": round(kc, 5),
+                                           "roofline": roofline(algc, kc)}
         del batches
         torch.cuda.empty_cache()
         for name, kw, hint, strided_len, flags in [
@@ -275,9 +287,8 @@ def main():
             o2 = torch.empty((nn, RESULT_BYTES), dtype=torch.uint8, device=dev)
             torch.cuda.synchronize()
             steps = max(5, args.steps // 5)
-            launch = (strided_launcher(bs, o2, netif, strided_len, flags) if strided_len
-                      else ragged_launcher(bs, o2, netif, hint, flags))
-            w2, k2, _ = time_kernel(launch, steps, 2, d)
+            w2, k2 = time_steps(bs, o2, netif, flags=flags, hint=hint, steps=steps, warmup=2, d=d,
+                                strided_len=strided_len)
             fb = frame_bytes(bs[0])
             meta = 0 if strided_len else 6
             a2 = fb + nn * (meta + RESULT_BYTES)

@@ -25,6 +25,7 @@ HALO_E_RANGE = -6
 
 HALO_RX_CSUM_ENABLE = 0x1
 HALO_RX_JUMBO_EXT = 0x2
+HALO_RX_RECORD_COMPACT = 0x4
 
 STATUS_NAMES = (
     "OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_PROTO", "IP_HDR_CKSUM",
@@ -55,6 +56,25 @@ RESULT_DTYPE = np.dtype([
 ])
 assert RESULT_DTYPE.itemsize == 32
 
+# halo_rx_record16_t (16 bytes): flags bits 4-5 hold the EtherType class
+RECORD16_DTYPE = np.dtype([
+    ("status", "u1"), ("flags", "u1"), ("ip_proto", "u1"), ("l4_aux", "u1"),
+    ("src_ip", "<u4"), ("dst_ip", "<u4"), ("sport", "<u2"), ("dport", "<u2"),
+])
+assert RECORD16_DTYPE.itemsize == 16
+ET_CLASS = {0x0800: 0x00, 0x0806: 0x10, 0x86DD: 0x20, 0x05DC: 0x30}
+
+
+def compact_of(full: np.ndarray) -> np.ndarray:
+    """The halo_rx_record16_t a full record maps to (host-side reference of the packing)."""
+    out = np.zeros(full.shape[0], dtype=RECORD16_DTYPE)
+    for f in ("status", "ip_proto", "l4_aux", "src_ip", "dst_ip", "sport", "dport"):
+        out[f] = full[f]
+    cls = np.zeros(full.shape[0], dtype=np.uint8)
+    for et, c in ET_CLASS.items():
+        cls[full["ethertype"] == et] = c
+    out["flags"] = full["flags"] | cls
+    return out
 
 class NetIf(ctypes.Structure):
     """halo_rx_netif_t — engine.NetIfConfig's MacAddr / IpAddr / NatEnable."""
@@ -98,6 +118,7 @@ _PROTOS = {
         ctypes.c_void_p, _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf),
         _u8p, _u8p]),
     "halo_rx_dispatch": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
+    "halo_rx_dispatch_compact": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_synth_layout": (ctypes.c_int, [
         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint64)]),

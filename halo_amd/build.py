@@ -12,6 +12,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "halo_amd", "csrc")
 OUT = os.path.join(ROOT, "halo_amd", "lib", "libhalo_rx.so")
 SOURCES = ["rx_parse.hip", "synth.hip", "host_path.hip"]
+# measurement tooling (bench.py's native step loop), linked against the product library
+BENCH_SRC = os.path.join(ROOT, "tools", "bench_loop.hip")
+BENCH_OUT = os.path.join(ROOT, "tools", "libhalo_bench.so")
 HEADERS = ["halo_common.h", os.path.join("..", "..", "include", "halo_rx.h")]
 
 
@@ -38,5 +41,22 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return OUT
 
 
+def build_bench(force: bool = False, verbose: bool = False) -> str:
+    """tools/libhalo_bench.so: the native timed step loop used by bench.py."""
+    lib = build(force=False, verbose=verbose)
+    if not force and os.path.exists(BENCH_OUT) and os.path.getmtime(BENCH_OUT) >= max(
+            os.path.getmtime(BENCH_SRC), os.path.getmtime(lib)):
+        return BENCH_OUT
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+           "-I" + os.path.join(ROOT, "include"), BENCH_SRC, "-L" + os.path.dirname(OUT), "-lhalo_rx",
+           "-Wl,-rpath,$ORIGIN/../halo_amd/lib", "-o", BENCH_OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(BENCH_OUT + ".tmp", BENCH_OUT)
+    return BENCH_OUT
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_bench(force="--force" in sys.argv, verbose=True))

@@ -60,19 +60,32 @@ extern "C" HALO_API const char* halo_rx_status_name(int status) {
 }
 
 // ---- engine decision (engine/ethernet_engine.go:13-31, engine/ipv4_engine.go:18-47) -----
-extern "C" HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32_t n, const halo_rx_netif_t* netif,
-                                         uint8_t* actions, uint32_t* action_hist) {
+namespace {
+uint16_t ethertype_of(const halo_rx_result_t& r) { return r.ethertype; }
+uint16_t ethertype_of(const halo_rx_record16_t& r) {
+    if (r.status == HALO_RX_ETH_LEN || r.status == HALO_RX_ETH_TYPE) return halo::kEthUnknown;
+    switch (r.flags & 0x30u) {
+        case HALO_RX_F_ET_ARP: return halo::kEthArp;
+        case HALO_RX_F_ET_IPV6: return halo::kEthIpv6;
+        case HALO_RX_F_ET_8023: return halo::kEthIeee8023;
+        default: return halo::kEthIpv4;
+    }
+}
+
+template <typename Rec>
+int dispatch(const Rec* results, uint32_t n, const halo_rx_netif_t* netif, uint8_t* actions, uint32_t* action_hist) {
     if (n && (!results || !netif || !actions)) return HALO_E_INVAL;
     for (uint32_t i = 0; i < n; ++i) {
-        const halo_rx_result_t& r = results[i];
+        const Rec& r = results[i];
+        const uint16_t ethertype = ethertype_of(r);
         uint8_t a;
         if (r.status == HALO_RX_ETH_LEN || r.status == HALO_RX_ETH_TYPE) {
             a = HALO_RX_ACT_DROP_ETH;                        // ethernet_engine.go:18-21
         } else if (!(r.flags & HALO_RX_F_MAC_MATCH)) {
             a = HALO_RX_ACT_IGNORE_MAC;                      // ethernet_engine.go:22
-        } else if (r.ethertype == halo::kEthArp) {
+        } else if (ethertype == halo::kEthArp) {
             a = HALO_RX_ACT_ARP;                             // ethernet_engine.go:24-25
-        } else if (r.ethertype != halo::kEthIpv4) {
+        } else if (ethertype != halo::kEthIpv4) {
             a = HALO_RX_ACT_IGNORE_TYPE;                     // ethernet_engine.go:28
         } else if (r.status >= HALO_RX_IP_LEN && r.status <= HALO_RX_IP_TOTLEN_OVERRUN) {
             a = HALO_RX_ACT_DROP_IP;                         // ipv4_engine.go:19-23
@@ -94,6 +107,18 @@ extern "C" HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32
         if (action_hist) ++action_hist[a];
     }
     return HALO_OK;
+}
+}  // namespace
+
+extern "C" HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32_t n, const halo_rx_netif_t* netif,
+                                         uint8_t* actions, uint32_t* action_hist) {
+    return dispatch(results, n, netif, actions, action_hist);
+}
+
+extern "C" HALO_API int halo_rx_dispatch_compact(const halo_rx_record16_t* records, uint32_t n,
+                                                 const halo_rx_netif_t* netif, uint8_t* actions,
+                                                 uint32_t* action_hist) {
+    return dispatch(records, n, netif, actions, action_hist);
 }
 
 // ---- host-memory batch path ---------------------------------------------------------------
@@ -190,6 +215,7 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
     if (!ctx || !netif) return HALO_E_INVAL;
     if (n == 0) return HALO_OK;
     if (!bytes || !offsets || !lens || !out) return HALO_E_INVAL;
+    if (flags & HALO_RX_RECORD_COMPACT) return HALO_E_INVAL;  // host path returns full records
     if (hipSetDevice(ctx->device) != hipSuccess) return HALO_E_NODEV;
     const uint32_t cap = (flags & HALO_RX_JUMBO_EXT) ? halo::kEthMaxJumbo : halo::kEthMax;
     int rc = HALO_OK;

@@ -246,52 +246,65 @@ struct Hist {
     }
 };
 
-// The whole chain for frame i on a group of G lanes (G = 1: one lane, no cross-lane traffic).
-// Every lane of the group must call it with the same i / present (lanes of other groups may
-// be doing the same for other frames); `present` false means "no frame": nothing is read or
-// written, but the group still executes the collective steps.
-template <int G, int LAYOUT>
-__device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, bool present, uint32_t gl,
-                                              uint32_t grp_base, Hist& hist) {
+// One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
+struct FrameState {
+    const uint8_t* frame;
+    uint32_t L, ndw;
+    uint32_t buf[4][4];  // round 0: chunks (u*G + gl), u = 0..3, of 16 bytes
+};
+
+template <int LAYOUT>
+__device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool present, FrameState& st) {
+    st.frame = p.bytes;
+    st.L = 0;
+    if (present) frame_at<LAYOUT>(p, i, st.frame, st.L);
+    const uint32_t eth_max = (p.flags & HALO_RX_JUMBO_EXT) ? kEthMaxJumbo : kEthMax;
+    // frames failing the length check are never read (ParseEthFrm looks at no byte)
+    st.ndw = (present && st.L >= kEthMin && st.L <= eth_max) ? (st.L + 3) >> 2 : 0;
+}
+
+// Round 0: four 16-byte chunks per lane issued back to back, bounded by the frame length (the
+// L4 end is not known before the header is parsed, and never exceeds the frame length).
+template <int G>
+__device__ __forceinline__ void frame_loads(uint32_t gl, FrameState& st) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
+}
+
+// Everything after round 0 for frame i on a group of G lanes (G = 1: one lane, no cross-lane
+// traffic). Every lane of a group calls it with the same i / present (other groups may be doing
+// the same for other frames); `present` false means "no frame": nothing is read or written,
+// but the group still executes the collective steps.
+template <int G>
+__device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool present, uint32_t gl,
+                                             uint32_t grp_base, FrameState& st, Hist& hist) {
     constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
     constexpr int U = 4;              // 16-byte chunks in flight per lane per round
-    const uint32_t eth_max = (p.flags & HALO_RX_JUMBO_EXT) ? kEthMaxJumbo : kEthMax;
-    const uint8_t* frame = p.bytes;
-    uint32_t L = 0;
-    if (present) frame_at<LAYOUT>(p, i, frame, L);
-    // frames failing the length check are never read (ParseEthFrm looks at no byte)
-    const uint32_t ndw = (present && L >= kEthMin && L <= eth_max) ? (L + 3) >> 2 : 0;
-
-    // Round 0: U 16-byte chunks per lane issued back to back, bounded by the frame length (the
-    // L4 end is not known before the header is parsed, and never exceeds the frame length).
-    uint32_t buf[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) load4(frame, (u * G + gl) * 4, ndw, buf[u]);
     uint32_t h[12];
     if constexpr (G == 1) {
 #pragma unroll
-        for (int j = 0; j < 12; ++j) h[j] = buf[j >> 2][j & 3];  // the lane's own frame
+        for (int j = 0; j < 12; ++j) h[j] = st.buf[j >> 2][j & 3];  // the lane's own frame
     } else {
         // header dwords 0..11 sit in chunk 0 of group lanes 0..2
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            h[j] = group_bcast<G, 0>(buf[0][j], grp_base);
-            h[4 + j] = group_bcast<G, 1>(buf[0][j], grp_base);
-            h[8 + j] = group_bcast<G, 2>(buf[0][j], grp_base);
+            h[j] = group_bcast<G, 0>(st.buf[0][j], grp_base);
+            h[4 + j] = group_bcast<G, 1>(st.buf[0][j], grp_base);
+            h[8 + j] = group_bcast<G, 2>(st.buf[0][j], grp_base);
         }
     }
-    Verdict v = parse_header(h, L, present, p);
+    Verdict v = parse_header(h, st.L, present, p);
 
     // L4 segment sum over [34, seg_end): round 0 from registers, then U chunks per round
     uint64_t c = 0;
     if (v.seg_end) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc_segment(buf[u], (u * G + gl) * 4, v.seg_end, c);
+        for (int u = 0; u < U; ++u) acc_segment(st.buf[u], (u * G + gl) * 4, v.seg_end, c);
         const uint32_t seg_dw = (v.seg_end + 3) >> 2;
         for (uint32_t r0 = U * STEP; r0 < seg_dw; r0 += U * STEP) {
             uint32_t x[U][4];
 #pragma unroll
-            for (int u = 0; u < U; ++u) load4(frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
+            for (int u = 0; u < U; ++u) load4(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
 #pragma unroll
             for (int u = 0; u < U; ++u) acc_segment(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
         }
@@ -310,16 +323,37 @@ __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, boo
         hi.y = v.pay_off | (v.pay_len << 16);
         hi.z = v.l4_seq;
         hi.w = v.l4_ack;
-        uint4* rec = reinterpret_cast<uint4*>(p.out + i);
-        if constexpr (G == 1) {
-            rec[0] = lo;
-            rec[1] = hi;
-        } else {  // lane 0 writes bytes 0..15, lane 1 bytes 16..31 (per-component select: no scratch)
-            const bool h1 = gl != 0;
-            rec[gl] = make_uint4(h1 ? hi.x : lo.x, h1 ? hi.y : lo.y, h1 ? hi.z : lo.z, h1 ? hi.w : lo.w);
+        if (p.flags & HALO_RX_RECORD_COMPACT) {  // halo_rx_record16_t
+            if (gl == 0) {
+                const uint32_t et_class = v.ethertype == kEthArp ? HALO_RX_F_ET_ARP
+                                        : v.ethertype == kEthIpv6 ? HALO_RX_F_ET_IPV6
+                                        : v.ethertype == kEthIeee8023 ? HALO_RX_F_ET_8023 : 0u;
+                reinterpret_cast<uint4*>(p.out)[i] =
+                    make_uint4(v.status | ((v.flags | et_class) << 8) | (v.ip_proto << 16) | (v.l4_aux << 24),
+                               v.src_ip, v.dst_ip, hi.x);
+            }
+        } else {
+            uint4* rec = reinterpret_cast<uint4*>(p.out + i);
+            if constexpr (G == 1) {
+                rec[0] = lo;
+                rec[1] = hi;
+            } else {  // lane 0 writes bytes 0..15, lane 1 bytes 16..31 (per-component select: no scratch)
+                const bool h1 = gl != 0;
+                rec[gl] = make_uint4(h1 ? hi.x : lo.x, h1 ? hi.y : lo.y, h1 ? hi.z : lo.z, h1 ? hi.w : lo.w);
+            }
         }
         if (gl == 0 && p.hist) hist.add(v.status);
     }
+}
+
+// The whole chain for frame i on a group of G lanes.
+template <int G, int LAYOUT>
+__device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, bool present, uint32_t gl,
+                                              uint32_t grp_base, Hist& hist) {
+    FrameState st;
+    frame_meta<LAYOUT>(p, i, present, st);
+    frame_loads<G>(gl, st);
+    frame_finish<G>(p, i, present, gl, grp_base, st, hist);
 }
 
 __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
@@ -333,8 +367,9 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
 }
 
 // Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
+// SGPRs <= 80 lets 8 blocks of 256 threads share a CU (MI355X_MICROARCH.md "Residency").
 template <int G, int LAYOUT>
-__global__ void __launch_bounds__(256) rx_group_kernel(const RxParams p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) rx_group_kernel(const RxParams p) {
     static_assert(G == 1 || G == 4 || G == 8 || G == 16, "G must be 1, 4, 8 or 16");
     constexpr uint32_t FPW = 64 / G;  // frames per wave
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
@@ -344,11 +379,46 @@ __global__ void __launch_bounds__(256) rx_group_kernel(const RxParams p) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp_base = lane & ~(uint32_t)(G - 1);
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t base = wave * FPW; base < p.n; base += nwaves * FPW) {
-        const uint64_t i = base + lane / G;
+    // frame indices fit in 32 bits (n is a u32): 32-bit loop state keeps the SGPR budget low
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t base = wave * FPW; base < p.n; base += nwaves * FPW) {
+        const uint32_t i = base + lane / G;
         process_frame<G, LAYOUT>(p, i, i < p.n, gl, grp_base, hist);
+    }
+    flush_hist(p, hist);
+}
+
+// Small frames, lane per frame, software-pipelined across tiles: while tile k is parsed, the
+// frame bytes of tile k+1 are already in flight (and the metadata of tile k+1 was requested
+// before that), so a wave keeps two tiles' loads outstanding instead of one.
+template <int LAYOUT>
+__global__ void __launch_bounds__(256) rx_lane_pipe_kernel(const RxParams p) {
+    __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
+    if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    Hist hist{s_hist, 0};
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t step = ((uint64_t)gridDim.x * blockDim.x) & ~63ull;  // frames per grid sweep
+    uint64_t ia = wave * 64 + lane;
+    if (wave * 64 < p.n) {
+        FrameState a, b;
+        frame_meta<LAYOUT>(p, ia, ia < p.n, a);
+        frame_loads<1>(0, a);
+        uint64_t ib = ia + step;
+        bool more = ib - lane < p.n;  // wave-uniform: next tile exists
+        if (more) frame_meta<LAYOUT>(p, ib, ib < p.n, b);
+        for (;;) {
+            if (more) frame_loads<1>(0, b);
+            frame_finish<1>(p, ia, ia < p.n, 0, lane, a, hist);
+            if (!more) break;
+            a = b;
+            ia = ib;
+            ib += step;
+            more = ib - lane < p.n;
+            if (more) frame_meta<LAYOUT>(p, ib, ib < p.n, b);
+        }
     }
     flush_hist(p, hist);
 }
@@ -405,11 +475,20 @@ uint32_t grid_for(uint64_t n, uint32_t frames_per_wave) {
     return (uint32_t)(blocks > kMaxBlocks ? kMaxBlocks : blocks);
 }
 
+// pipelined kernel: about two tiles per wave, at most ~resident capacity (256 CUs x 6 blocks)
+uint32_t grid_pipe(uint64_t n) {
+    const uint64_t tiles = (n + 63) / 64;
+    uint64_t blocks = (tiles + 7) / 8;  // 4 waves per block, 2 tiles per wave
+    if (blocks > 256ull * 6) blocks = 256ull * 6;
+    return (uint32_t)(blocks ? blocks : 1);
+}
+
 template <int LAYOUT>
 hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     const dim3 block(256);
     switch (variant) {
         case 1: hipLaunchKernelGGL((rx_group_kernel<1, LAYOUT>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
+        case 2: hipLaunchKernelGGL((rx_lane_pipe_kernel<LAYOUT>), dim3(grid_pipe(p.n)), block, 0, s, p); break;
         case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
         case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
         case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
@@ -445,7 +524,7 @@ int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, 
 int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
                 halo_rx_result_t* d_out, uint32_t* d_hist) {
     if (!netif || !d_out) return HALO_E_INVAL;
-    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT)) return HALO_E_INVAL;
+    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_RECORD_COMPACT)) return HALO_E_INVAL;
     if (reinterpret_cast<uintptr_t>(d_out) & 15u) return HALO_E_INVAL;
     p.n = n;
     p.flags = flags;
@@ -500,7 +579,8 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
 }
 
 extern "C" HALO_API int halo_rx_tune_variant(int variant) {
-    if (variant != 0 && variant != 1 && variant != 4 && variant != 8 && variant != 16 && variant != -1)
+    if (variant != 0 && variant != 1 && variant != 2 && variant != 4 && variant != 8 && variant != 16 &&
+        variant != -1)
         return HALO_E_INVAL;
     halo::g_force_variant.store(variant, std::memory_order_relaxed);
     return HALO_OK;

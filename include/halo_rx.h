@@ -67,6 +67,8 @@ extern "C" {
 #define HALO_RX_CSUM_ENABLE 0x1u /* verify IPv4 header + UDP/TCP checksums (ICMP: always)  */
 #define HALO_RX_JUMBO_EXT 0x2u   /* build-defined extension: lift the 1514/1500/1480 caps   */
                                  /* to 9014/9000/8980 (MTU 9000); arithmetic unchanged      */
+#define HALO_RX_RECORD_COMPACT 0x4u /* write halo_rx_record16_t (16 B) instead of            */
+                                    /* halo_rx_result_t (32 B); device entry points only     */
 
 /* ---- per-frame status: the FIRST failing check in reference order, 0 = OK ---------- */
 typedef enum halo_rx_status {
@@ -127,6 +129,26 @@ typedef struct halo_rx_result {
     uint32_t l4_ack;
 } halo_rx_result_t;
 
+/* ---- compact per-frame record (16 B; flags |= HALO_RX_RECORD_COMPACT) ------------------
+ * The verdict and the extracted 5-tuple only: the fields of halo_rx_result_t named the same,
+ * with the EtherType folded into flags bits 4-5 (HALO_RX_F_ET_*; the EtherType is 0xFFFF when
+ * status is HALO_RX_ETH_LEN or HALO_RX_ETH_TYPE, whatever those bits hold).                */
+#define HALO_RX_F_ET_SHIFT 4
+#define HALO_RX_F_ET_IPV4 0x00u    /* 0x0800 */
+#define HALO_RX_F_ET_ARP 0x10u     /* 0x0806 */
+#define HALO_RX_F_ET_IPV6 0x20u    /* 0x86DD */
+#define HALO_RX_F_ET_8023 0x30u    /* 0x05DC */
+typedef struct halo_rx_record16 {
+    uint8_t status;
+    uint8_t flags;     /* HALO_RX_F_* | HALO_RX_F_ET_* */
+    uint8_t ip_proto;
+    uint8_t l4_aux;
+    uint32_t src_ip;
+    uint32_t dst_ip;
+    uint16_t sport;
+    uint16_t dport;
+} halo_rx_record16_t;
+
 /* ---- the interface a frame is received on (engine.NetIfConfig, engine/engine.go:65-81) - */
 typedef struct halo_rx_netif {
     uint8_t mac[6];  /* NetIf.MacAddr                              */
@@ -145,7 +167,8 @@ HALO_API const char* halo_rx_strerror(int code);
 HALO_API const char* halo_rx_status_name(int status);
 
 /* ---- device-resident batch parse (the hot path) --------------------------------------
- * All pointers are device pointers. `d_out` receives n records. `d_status_hist`, if not
+ * All pointers are device pointers. `d_out` receives n records (halo_rx_result_t, or
+ * halo_rx_record16_t with HALO_RX_RECORD_COMPACT; 16-byte aligned). `d_status_hist`, if not
  * NULL, receives HALO_RX_STATUS_COUNT u32 counters that are INCREMENTED (the caller
  * zeroes them). `max_len_hint` (0 = unknown) selects the lanes-per-frame variant.
  * Asynchronous on `stream`.                                                              */
@@ -205,6 +228,10 @@ typedef enum halo_rx_action {
 HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32_t n,
                               const halo_rx_netif_t* netif, uint8_t* actions,
                               uint32_t* action_hist);
+/* The same over compact records. */
+HALO_API int halo_rx_dispatch_compact(const halo_rx_record16_t* records, uint32_t n,
+                                      const halo_rx_netif_t* netif, uint8_t* actions,
+                                      uint32_t* action_hist);
 
 /* ---- synthetic traffic (bench + tests; SURVEY.md §8d generator) ----------------------
  * Every field of frame i is a pure function of (seed, i), so any shard of the global

@@ -152,3 +152,23 @@ def test_synth_twin_frames_verify(oracle_lib):
     assert mutated.sum() > 50
     assert np.all(recs["status"][~mutated] == 0)
     assert np.all(recs["status"][mutated] != 0)
+
+
+def test_dispatch_compact_matches_full(golden, oracle_lib):
+    """halo_rx_dispatch_compact on the compact form of each record == halo_rx_dispatch."""
+    from halo_amd import _lib
+    from halo_amd._lib import NetIf, compact_of
+    from tests.helpers import golden_arrays
+
+    meta, blob = golden
+    data, offs, lens, _ = golden_arrays(meta, blob)
+    for nat in (False, True):
+        hn = NetIf.make(nat_enable=nat)
+        for fl in (0, 1, 2, 3):
+            recs, _ = oracle_lib.rx_batch(data, lens, oracle_lib.NetIf.make(nat_enable=nat), fl, offsets_dw=offs)
+            full = np.empty(len(recs), np.uint8)
+            comp = np.empty(len(recs), np.uint8)
+            c16 = compact_of(recs)
+            assert _lib.lib.halo_rx_dispatch(recs.ctypes.data, len(recs), hn, full.ctypes.data, None) == 0
+            assert _lib.lib.halo_rx_dispatch_compact(c16.ctypes.data, len(recs), hn, comp.ctypes.data, None) == 0
+            assert np.array_equal(full, comp)

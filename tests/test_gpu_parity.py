@@ -64,7 +64,7 @@ def lanes_per_frame(request):
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2, 3])
-@pytest.mark.parametrize("lanes_per_frame", [1, 4, 8, 16, -1], indirect=True)
+@pytest.mark.parametrize("lanes_per_frame", [1, 2, 4, 8, 16, -1], indirect=True)
 def test_golden_ragged_all_group_widths(dev, golden, flags, lanes_per_frame):
     from halo_amd._lib import RESULT_DTYPE
 
@@ -86,7 +86,7 @@ def test_golden_ragged_auto_variant(dev, golden, hint):
     assert_records_equal(got, expected_records(meta, 3, RESULT_DTYPE), names, f"GPU ragged hint={hint}")
 
 
-@pytest.mark.parametrize("lanes_per_frame", [1, 4, 8, 16, -1], indirect=True)
+@pytest.mark.parametrize("lanes_per_frame", [1, 2, 4, 8, 16, -1], indirect=True)
 def test_random_imix_every_group_width(dev, oracle_lib, lanes_per_frame):
     """30k IMIX frames, mixed protocols, 1/4 mutated: each kernel variant vs the oracle."""
     import torch
@@ -102,6 +102,32 @@ def test_random_imix_every_group_width(dev, oracle_lib, lanes_per_frame):
     want, _ = oracle_lib.rx_batch(fr["bytes"].cpu().numpy(), lay["lens"], oracle_lib.NetIf.make(), 1,
                                   offsets_dw=lay["offsets_dw"], threads=8)
     assert_records_equal(protocol.records(out), want, None, f"IMIX G={lanes_per_frame}")
+
+
+@pytest.mark.parametrize("lanes_per_frame", [0, 1, 4, 8, 16, -1], indirect=True)
+def test_golden_compact_records(dev, golden, lanes_per_frame):
+    """HALO_RX_RECORD_COMPACT: 16-byte records == the compact form of the expected records."""
+    import torch
+
+    from halo_amd import _lib
+    from halo_amd._lib import RECORD16_DTYPE, RESULT_DTYPE, NetIf, compact_of
+
+    meta, blob = golden
+    data, offs, lens, names = golden_arrays(meta, blob)
+    d = _to_dev(data, dev)
+    o = _to_dev(offs.astype(np.uint32), dev, np.int32)
+    ln = _to_dev(lens.astype(np.uint16), dev, np.int16)
+    for flags in (1, 3):
+        out = torch.full((len(lens), 16), 0xEE, dtype=torch.uint8, device=dev)
+        rc = _lib.lib.halo_rx_parse_batch_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens),
+                                                 flags | _lib.HALO_RX_RECORD_COMPACT, NetIf.make(), 0,
+                                                 out.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().reshape(-1).view(RECORD16_DTYPE)
+        want = compact_of(expected_records(meta, flags, RESULT_DTYPE))
+        bad = np.nonzero(got.view(np.uint8).reshape(-1, 16) != want.view(np.uint8).reshape(-1, 16))[0]
+        assert bad.size == 0, [names[i] for i in np.unique(bad)[:5]]
 
 
 def test_golden_gap_bytes_are_ignored(dev, golden):

@@ -1,0 +1,47 @@
+// bench_loop.hip — native timed step loop for bench.py (measurement tooling, not the product).
+//
+// bench.py's Python loop cost several microseconds of host time per launch, comparable to a
+// 25 us kernel. This loop issues the same C-ABI calls a compiled host (the Go reference's
+// PacketHandle replacement) would: one halo_rx_parse_*_device call per step, back to back on
+// one stream. One HIP event pair brackets the whole timed region on that stream: the average
+// launch duration is its elapsed time / steps. (An event pair around every launch would add
+// about 2.5 us to each launch on the GPU timeline: measured in tools/gap_probe.py.)
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+
+#include "halo_rx.h"
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_steps(
+    int nbatch, const uint8_t* const* bytes, const uint32_t* const* offsets_dw, const uint16_t* const* lens,
+    uint32_t n, uint64_t stride, uint32_t len, uint32_t flags, const halo_rx_netif_t* netif, uint32_t hint,
+    halo_rx_result_t* out, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0 || steps <= 0 || !region_ms || !wall_s) return HALO_E_INVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto launch = [&](int k) -> int {
+        const int b = k % nbatch;
+        if (offsets_dw)
+            return halo_rx_parse_batch_device(bytes[b], offsets_dw[b], lens[b], n, flags, netif, hint, out, nullptr,
+                                              stream);
+        return halo_rx_parse_strided_device(bytes[b], stride, lens ? lens[b] : nullptr, len, n, flags, netif, out,
+                                            nullptr, stream);
+    };
+    int rc = HALO_OK;
+    for (int k = 0; k < warmup && rc == HALO_OK; ++k) rc = launch(k);
+    if (rc) return rc;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return HALO_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return HALO_E_HIP;
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)hipEventRecord(e0, s);
+    for (int k = 0; k < steps && rc == HALO_OK; ++k) rc = launch(k);
+    (void)hipEventRecord(e1, s);
+    if (hipStreamSynchronize(s) != hipSuccess && rc == HALO_OK) rc = HALO_E_HIP;
+    const auto t1 = std::chrono::steady_clock::now();
+    *wall_s = std::chrono::duration<double>(t1 - t0).count();
+    *region_ms = -1.0f;
+    (void)hipEventElapsedTime(region_ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}

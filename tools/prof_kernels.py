@@ -41,10 +41,17 @@ def main():
         bs = bench.make_batches(dev, netif, n=n, rotate=rot, rank=0, **kw)
         out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
         torch.cuda.synchronize()
-        launch = (bench.strided_launcher(bs, out, netif, slen, flags) if slen
-                  else bench.ragged_launcher(bs, out, netif, hint, flags))
+        stream = torch.cuda.current_stream().cuda_stream
         for i in range(launches):
-            launch(i)
+            fr = bs[i % len(bs)]
+            if slen:
+                rc = _lib.lib.halo_rx_parse_strided_device(fr["bytes"].data_ptr(), slen, None, slen, n, flags, netif,
+                                                           out.data_ptr(), None, stream)
+            else:
+                rc = _lib.lib.halo_rx_parse_batch_device(fr["bytes"].data_ptr(), fr["offsets_dw"].data_ptr(),
+                                                         fr["lens"].data_ptr(), n, flags, netif, hint,
+                                                         out.data_ptr(), None, stream)
+            _lib.check("parse", rc)
         torch.cuda.synchronize()
         print(f"{name}: {launches} launches of {n} frames", flush=True)
         del bs, out
