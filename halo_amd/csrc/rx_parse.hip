@@ -83,11 +83,16 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
 
 // Load dwords [d0, d0+4) of a frame that has ndw readable dwords; zero beyond. Never touches a
 // dword past the one holding the frame's last byte (halo_rx.h layout contract).
+// Frame bytes are always in global memory: say so, so that a pointer that came through LDS or a
+// register still compiles to global_load (a flat_load would also count against lgkmcnt and make
+// every later LDS access wait for it).
+typedef const __attribute__((address_space(1))) uint32_t gu32;
+
 __device__ __forceinline__ void load4(const uint8_t* frame, uint32_t d0, uint32_t ndw, uint32_t (&w)[4]) {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(frame) + d0;
+    gu32* p = (gu32*)(reinterpret_cast<const uint32_t*>(frame) + d0);
     if (d0 + 4 <= ndw) {
-        uint4 v;
-        __builtin_memcpy(&v, p, 16);  // 4-byte aligned 16-byte load: global_load_dwordx4
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));  // 4-byte aligned 16 B
+        const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;
         w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
     } else {
 #pragma unroll
@@ -246,15 +251,22 @@ struct Hist {
     }
 };
 
+// 16-byte chunks per lane issued before the header is parsed (a lane-per-frame lane needs its
+// first 64 bytes). Eight for groups would let a 570 B frame finish in one round trip, but costs
+// ~55 VGPRs (occupancy 5 -> 3) and lost more than it gained; kept as a knob.
+template <int G>
+constexpr int kRound0 = 4;
+
 // One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
+template <int G>
 struct FrameState {
     const uint8_t* frame;
     uint32_t L, ndw;
-    uint32_t buf[4][4];  // round 0: chunks (u*G + gl), u = 0..3, of 16 bytes
+    uint32_t buf[kRound0<G>][4];  // round 0: chunks (u*G + gl) of 16 bytes
 };
 
-template <int LAYOUT>
-__device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool present, FrameState& st) {
+template <int LAYOUT, typename FS>
+__device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool present, FS& st) {
     st.frame = p.bytes;
     st.L = 0;
     if (present) frame_at<LAYOUT>(p, i, st.frame, st.L);
@@ -266,26 +278,18 @@ __device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool p
 // Round 0: four 16-byte chunks per lane issued back to back, bounded by the frame length (the
 // L4 end is not known before the header is parsed, and never exceeds the frame length).
 template <int G>
-__device__ __forceinline__ void frame_loads(uint32_t gl, FrameState& st) {
+__device__ __forceinline__ void frame_loads(uint32_t gl, FrameState<G>& st) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
+    for (int u = 0; u < kRound0<G>; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
 }
 
-// Everything after round 0 for frame i on a group of G lanes (G = 1: one lane, no cross-lane
-// traffic). Every lane of a group calls it with the same i / present (other groups may be doing
-// the same for other frames); `present` false means "no frame": nothing is read or written,
-// but the group still executes the collective steps.
+// Header dwords 0..11 of the frame: the lane's own chunks (G = 1) or chunk 0 of group lanes 0..2.
 template <int G>
-__device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool present, uint32_t gl,
-                                             uint32_t grp_base, FrameState& st, Hist& hist) {
-    constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
-    constexpr int U = 4;              // 16-byte chunks in flight per lane per round
-    uint32_t h[12];
+__device__ __forceinline__ void frame_header(const FrameState<G>& st, uint32_t grp_base, uint32_t (&h)[12]) {
     if constexpr (G == 1) {
 #pragma unroll
-        for (int j = 0; j < 12; ++j) h[j] = st.buf[j >> 2][j & 3];  // the lane's own frame
+        for (int j = 0; j < 12; ++j) h[j] = st.buf[j >> 2][j & 3];
     } else {
-        // header dwords 0..11 sit in chunk 0 of group lanes 0..2
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             h[j] = group_bcast<G, 0>(st.buf[0][j], grp_base);
@@ -293,22 +297,12 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
             h[8 + j] = group_bcast<G, 2>(st.buf[0][j], grp_base);
         }
     }
-    Verdict v = parse_header(h, st.L, present, p);
+}
 
-    // L4 segment sum over [34, seg_end): round 0 from registers, then U chunks per round
-    uint64_t c = 0;
-    if (v.seg_end) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc_segment(st.buf[u], (u * G + gl) * 4, v.seg_end, c);
-        const uint32_t seg_dw = (v.seg_end + 3) >> 2;
-        for (uint32_t r0 = U * STEP; r0 < seg_dw; r0 += U * STEP) {
-            uint32_t x[U][4];
-#pragma unroll
-            for (int u = 0; u < U; ++u) load4(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
-#pragma unroll
-            for (int u = 0; u < U; ++u) acc_segment(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
-        }
-    }
+// Verdict after the L4 segment sum (this lane's or group's partial `c`), record store and count.
+template <int G>
+__device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool present, uint32_t gl,
+                                            const uint32_t (&h)[12], Verdict& v, uint64_t c, Hist& hist) {
     const uint32_t c32 = group_sum<G>(fold64(c));
     if (v.status == HALO_RX_OK && v.check_l4 && fold16(c32 + v.l4_extra) != 0xFFFFu) v.status = HALO_RX_L4_CKSUM;
     if (v.status == HALO_RX_OK && v.ip_proto != kIpUnknown) finish_l4(h, v);
@@ -346,11 +340,42 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
     }
 }
 
+// Everything after round 0 for frame i on a group of G lanes (G = 1: one lane, no cross-lane
+// traffic). Every lane of a group calls it with the same i / present (other groups may be doing
+// the same for other frames); `present` false means "no frame": nothing is read or written,
+// but the group still executes the collective steps.
+template <int G>
+__device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool present, uint32_t gl,
+                                             uint32_t grp_base, FrameState<G>& st, Hist& hist) {
+    constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
+    constexpr int U0 = kRound0<G>;    // chunks already loaded
+    constexpr int U = 4;              // 16-byte chunks in flight per lane per later round
+    uint32_t h[12];
+    frame_header<G>(st, grp_base, h);
+    Verdict v = parse_header(h, st.L, present, p);
+
+    // L4 segment sum over [34, seg_end): round 0 from registers, then U chunks per round
+    uint64_t c = 0;
+    if (v.seg_end) {
+#pragma unroll
+        for (int u = 0; u < U0; ++u) acc_segment(st.buf[u], (u * G + gl) * 4, v.seg_end, c);
+        const uint32_t seg_dw = (v.seg_end + 3) >> 2;
+        for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
+            uint32_t x[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load4(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc_segment(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
+        }
+    }
+    frame_store<G>(p, i, present, gl, h, v, c, hist);
+}
+
 // The whole chain for frame i on a group of G lanes.
 template <int G, int LAYOUT>
 __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, bool present, uint32_t gl,
                                               uint32_t grp_base, Hist& hist) {
-    FrameState st;
+    FrameState<G> st;
     frame_meta<LAYOUT>(p, i, present, st);
     frame_loads<G>(gl, st);
     frame_finish<G>(p, i, present, gl, grp_base, st, hist);
@@ -367,10 +392,8 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
 }
 
 // Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
-// SGPRs <= 80 lets 8 blocks of 256 threads share a CU (MI355X_MICROARCH.md "Residency").
 template <int G, int LAYOUT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) rx_group_kernel(const RxParams p) {
-    static_assert(G == 1 || G == 4 || G == 8 || G == 16, "G must be 1, 4, 8 or 16");
+__device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     constexpr uint32_t FPW = 64 / G;  // frames per wave
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
@@ -389,83 +412,112 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) rx_g
     flush_hist(p, hist);
 }
 
-// Small frames, lane per frame, software-pipelined across tiles: while tile k is parsed, the
-// frame bytes of tile k+1 are already in flight (and the metadata of tile k+1 was requested
-// before that), so a wave keeps two tiles' loads outstanding instead of one.
+// Lane per frame. SGPRs <= 80 lets 8 blocks of 256 threads share a CU (MI355X_MICROARCH.md
+// "Residency"); at 55 VGPRs that is the full 8 waves per SIMD.
 template <int LAYOUT>
-__global__ void __launch_bounds__(256) rx_lane_pipe_kernel(const RxParams p) {
-    __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
-    if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
-    __syncthreads();
-    Hist hist{s_hist, 0};
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t step = ((uint64_t)gridDim.x * blockDim.x) & ~63ull;  // frames per grid sweep
-    uint64_t ia = wave * 64 + lane;
-    if (wave * 64 < p.n) {
-        FrameState a, b;
-        frame_meta<LAYOUT>(p, ia, ia < p.n, a);
-        frame_loads<1>(0, a);
-        uint64_t ib = ia + step;
-        bool more = ib - lane < p.n;  // wave-uniform: next tile exists
-        if (more) frame_meta<LAYOUT>(p, ib, ib < p.n, b);
-        for (;;) {
-            if (more) frame_loads<1>(0, b);
-            frame_finish<1>(p, ia, ia < p.n, 0, lane, a, hist);
-            if (!more) break;
-            a = b;
-            ia = ib;
-            ib += step;
-            more = ib - lane < p.n;
-            if (more) frame_meta<LAYOUT>(p, ib, ib < p.n, b);
-        }
-    }
-    flush_hist(p, hist);
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) rx_lane_kernel(const RxParams p) {
+    group_kernel_body<1, LAYOUT>(p);
 }
 
-// Mixed-size batches (IMIX): each wave takes a tile of 64 consecutive frames. Frames of at most
-// 64 bytes (or failing the length check) are done lane-per-frame in place; the tile's longer
-// frames are then compacted (ballot rank -> LDS) and done 8 at a time by 8-lane groups, so no
-// lane idles behind a 1500-byte neighbour and no global workspace is needed.
+// G lanes per frame (G in {4, 8, 16}); VGPR-limited occupancy, so no SGPR cap.
+template <int G, int LAYOUT>
+__global__ void __launch_bounds__(256) rx_group_kernel(const RxParams p) {
+    static_assert(G == 4 || G == 8 || G == 16, "G must be 4, 8 or 16");
+    group_kernel_body<G, LAYOUT>(p);
+}
+
+// Mixed sizes (IMIX): each wave takes a window of 256 consecutive frames (four per lane), sorts
+// them by size class into LDS (ballot ranks; the frame address and length travel with the
+// entry, so nothing is re-loaded), then runs one pass per class with the lanes-per-frame that
+// the uniform sweep found best for that size: <= 128 B (and frames failing the length check)
+// lane per frame, <= 1024 B 4 lanes, <= 4096 B 8 lanes, longer 16 lanes. Every pass keeps all
+// groups busy with frames of one class, so no lane waits behind a longer neighbour.
+constexpr uint32_t kMixWindow = 256;
+
+template <int G>
+__device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, uint32_t e_end, uint32_t lane,
+                                         const uint64_t* s_ptr, const uint32_t* s_idx, const uint16_t* s_len,
+                                         uint32_t eth_max, Hist& hist) {
+    constexpr uint32_t FPW = 64 / G;
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp_base = lane & ~(uint32_t)(G - 1);
+    for (uint32_t e0 = e_begin; e0 < e_end; e0 += FPW) {
+        const uint32_t e = e0 + lane / G;
+        const bool has = e < e_end;
+        FrameState<G> st;
+        st.frame = has ? reinterpret_cast<const uint8_t*>(s_ptr[e]) : p.bytes;
+        st.L = has ? s_len[e] : 0u;
+        st.ndw = (has && st.L >= kEthMin && st.L <= eth_max) ? (st.L + 3) >> 2 : 0;
+        frame_loads<G>(gl, st);
+        frame_finish<G>(p, has ? s_idx[e] : 0u, has, gl, grp_base, st, hist);
+    }
+}
+
 template <int LAYOUT>
-__global__ void __launch_bounds__(256) rx_tile_kernel(const RxParams p) {
-    constexpr int GL = 8;  // lanes per long frame
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) rx_mix_kernel(const RxParams p) {
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
-    __shared__ uint8_t s_slot[4][64];  // per wave: tile-local index of the k-th long frame
+    __shared__ uint64_t s_ptr[4][kMixWindow];
+    __shared__ uint32_t s_idx[4][kMixWindow];
+    __shared__ uint16_t s_len[4][kMixWindow];
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
     Hist hist{s_hist, 0};
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wib = threadIdx.x >> 6;  // wave in block
+    const uint32_t w = threadIdx.x >> 6;
     const uint32_t eth_max = (p.flags & HALO_RX_JUMBO_EXT) ? kEthMaxJumbo : kEthMax;
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t base = wave * 64; base < p.n; base += nwaves * 64) {
-        const uint64_t i = base + lane;
-        const bool present = i < p.n;
-        uint32_t L = 0;
-        if (present) L = LAYOUT == 2 ? p.len : p.lens[i];
-        const bool is_long = present && L > 64 && L <= eth_max;
-        if (!is_long) process_frame<1, LAYOUT>(p, i, present, 0, lane, hist);
-        const uint64_t long_mask = __ballot(is_long);
-        if (long_mask == 0) continue;
-        const uint32_t nlong = (uint32_t)__popcll(long_mask);
-        if (is_long) s_slot[wib][__builtin_amdgcn_mbcnt_hi((uint32_t)(long_mask >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)long_mask, 0u))] = (uint8_t)lane;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        for (uint32_t k0 = 0; k0 < nlong; k0 += 64 / GL) {
-            const uint32_t k = k0 + lane / GL;
-            const bool has = k < nlong;
-            const uint32_t t = has ? s_slot[wib][k] : 0u;
-            process_frame<GL, LAYOUT>(p, base + t, has, lane & (GL - 1), lane & ~(uint32_t)(GL - 1), hist);
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t base = wave * kMixWindow; base < p.n; base += nwaves * kMixWindow) {
+        // classify: frame base + 64k + lane, k = 0..3
+        const uint8_t* fp[4];
+        uint32_t fl[4], cls[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = base + 64 * k + lane;
+            fp[k] = p.bytes;
+            fl[k] = 0;
+            if (i < p.n) frame_at<LAYOUT>(p, i, fp[k], fl[k]);
+            cls[k] = i >= p.n ? 4u
+                   : (fl[k] <= 128 || fl[k] > eth_max) ? 0u
+                   : fl[k] <= 1024 ? 1u : fl[k] <= 4096 ? 2u : 3u;
         }
+        // counting sort by class: one ballot live at a time
+        uint32_t pos[4] = {0, 0, 0, 0};
+        uint32_t start[5];
+        uint32_t run = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            start[c] = run;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t b = __ballot(cls[k] == (uint32_t)c);
+                if (cls[k] == (uint32_t)c)
+                    pos[k] = run + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+                run += (uint32_t)__popcll(b);
+            }
+        }
+        start[4] = run;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (cls[k] < 4u) {
+                s_ptr[w][pos[k]] = reinterpret_cast<uint64_t>(fp[k]);
+                s_idx[w][pos[k]] = base + 64 * k + lane;
+                s_len[w][pos[k]] = (uint16_t)fl[k];
+            }
+        }
+        const uint32_t st0 = start[0], st1 = start[1], st2 = start[2], st3 = start[3], nall = start[4];
+        __builtin_amdgcn_wave_barrier();
+        mix_pass<1>(p, st0, st1, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        mix_pass<4>(p, st1, st2, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        mix_pass<8>(p, st2, st3, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        mix_pass<16>(p, st3, nall, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
         __builtin_amdgcn_wave_barrier();
     }
     flush_hist(p, hist);
 }
 
-constexpr int kVariantTile = -1;
+constexpr int kVariantMix = -1;
 std::atomic<int> g_force_variant{0};  // tuning hook (halo_rx_tune_variant); 0 = automatic
 
 uint32_t grid_for(uint64_t n, uint32_t frames_per_wave) {
@@ -475,38 +527,30 @@ uint32_t grid_for(uint64_t n, uint32_t frames_per_wave) {
     return (uint32_t)(blocks > kMaxBlocks ? kMaxBlocks : blocks);
 }
 
-// pipelined kernel: about two tiles per wave, at most ~resident capacity (256 CUs x 6 blocks)
-uint32_t grid_pipe(uint64_t n) {
-    const uint64_t tiles = (n + 63) / 64;
-    uint64_t blocks = (tiles + 7) / 8;  // 4 waves per block, 2 tiles per wave
-    if (blocks > 256ull * 6) blocks = 256ull * 6;
-    return (uint32_t)(blocks ? blocks : 1);
-}
-
 template <int LAYOUT>
 hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     const dim3 block(256);
     switch (variant) {
-        case 1: hipLaunchKernelGGL((rx_group_kernel<1, LAYOUT>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
-        case 2: hipLaunchKernelGGL((rx_lane_pipe_kernel<LAYOUT>), dim3(grid_pipe(p.n)), block, 0, s, p); break;
+        case 1: hipLaunchKernelGGL((rx_lane_kernel<LAYOUT>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
         case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
         case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
         case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
-        default: hipLaunchKernelGGL((rx_tile_kernel<LAYOUT>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
+        default: hipLaunchKernelGGL((rx_mix_kernel<LAYOUT>), dim3(grid_for(p.n, kMixWindow)), block, 0, s, p); break;
     }
     return hipGetLastError();
 }
 
-// Kernel variant (DESIGN.md "Choosing the variant", from the G sweep in profiles/):
-// a known uniform length picks the best lanes-per-frame; otherwise frames of at most 64 B
-// go lane-per-frame and anything longer or mixed goes to the tile kernel.
+// Kernel variant (from the sweeps in profiles/r01/tune_*.log): a known uniform
+// length picks the best lanes-per-frame; a ragged batch whose frames are all <= 64 B goes lane
+// per frame, and any other ragged batch goes to the size-class mix kernel.
 int pick_variant(uint32_t max_len, bool uniform) {
     const int forced = g_force_variant.load(std::memory_order_relaxed);
     if (forced) return forced;
     if (max_len != 0 && max_len <= 64) return 1;
-    if (!uniform) return kVariantTile;
-    if (max_len <= 640) return 4;
-    if (max_len <= 2048) return 8;
+    if (!uniform) return kVariantMix;
+    if (max_len <= 128) return 1;
+    if (max_len <= 1024) return 4;
+    if (max_len <= 4096) return 8;
     return 16;
 }
 
@@ -579,8 +623,7 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
 }
 
 extern "C" HALO_API int halo_rx_tune_variant(int variant) {
-    if (variant != 0 && variant != 1 && variant != 2 && variant != 4 && variant != 8 && variant != 16 &&
-        variant != -1)
+    if (variant != 0 && variant != 1 && variant != 4 && variant != 8 && variant != 16 && variant != -1)
         return HALO_E_INVAL;
     halo::g_force_variant.store(variant, std::memory_order_relaxed);
     return HALO_OK;

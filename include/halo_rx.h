@@ -185,9 +185,9 @@ HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uint64_t strid
                                           halo_stream_t stream);
 
 /* Tuning hook: force the kernel variant process-wide. 1, 4, 8, 16 = that many lanes per frame
- * for every frame; -1 = tile kernel (lane-per-frame for frames <= 64 B, compacted 8-lane
- * groups for longer ones); 0 = automatic (from max_len_hint / the uniform length).
- * Results are identical for every value; only speed changes. */
+ * for every frame; -1 = size-class mix kernel (each wave sorts 256 frames by size and runs
+ * lane-per-frame, 4-, 8- and 16-lane passes); 0 = automatic (from max_len_hint / the uniform
+ * length). Results are identical for every value; only speed changes. */
 HALO_API int halo_rx_tune_variant(int variant);
 
 /* ---- host-memory batch parse -----------------------------------

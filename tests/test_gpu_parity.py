@@ -64,7 +64,7 @@ def lanes_per_frame(request):
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2, 3])
-@pytest.mark.parametrize("lanes_per_frame", [1, 2, 4, 8, 16, -1], indirect=True)
+@pytest.mark.parametrize("lanes_per_frame", [1, 4, 8, 16, -1], indirect=True)
 def test_golden_ragged_all_group_widths(dev, golden, flags, lanes_per_frame):
     from halo_amd._lib import RESULT_DTYPE
 
@@ -86,7 +86,7 @@ def test_golden_ragged_auto_variant(dev, golden, hint):
     assert_records_equal(got, expected_records(meta, 3, RESULT_DTYPE), names, f"GPU ragged hint={hint}")
 
 
-@pytest.mark.parametrize("lanes_per_frame", [1, 2, 4, 8, 16, -1], indirect=True)
+@pytest.mark.parametrize("lanes_per_frame", [1, 4, 8, 16, -1], indirect=True)
 def test_random_imix_every_group_width(dev, oracle_lib, lanes_per_frame):
     """30k IMIX frames, mixed protocols, 1/4 mutated: each kernel variant vs the oracle."""
     import torch
