@@ -177,6 +177,46 @@ def load_traffic(workload: str):
         return None
 
 
+def e2e_host(dev, netif, steps: int):
+    """PCIe-inclusive rate of halo_rx_parse_batch_host on packed host batches."""
+    import numpy as np
+    import torch
+
+    from halo_amd import _lib
+    from halo_amd.engine import HostBatcher
+
+    res = {}
+    for name, kw, n in [("e2e_host_config2_64B_1M", dict(length=64), 1 << 20),
+                        ("e2e_host_imix_4M", dict(size_mode=1, proto_mode=3), 4 << 20)]:
+        fr = make_batches(dev, netif, n=n, rotate=1, rank=0, **kw)[0]
+        lay = fr["layout"]
+        host = fr["bytes"].cpu().numpy()
+        offs = lay["offsets_dw"].astype(np.uint64) * 4
+        hb = HostBatcher(dev.index or 0)
+        out = np.zeros(n, dtype=_lib.RESULT_DTYPE)  # touched once: no page faults in the timed loop
+        for registered in (True, False):
+            if registered:
+                _lib.check("register", _lib.lib.halo_rx_host_register(host.ctypes.data, host.nbytes))
+                _lib.check("register", _lib.lib.halo_rx_host_register(out.ctypes.data, out.nbytes))
+            hb.parse(host, offs, lay["lens"], netif, 1, out=out)  # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                hb.parse(host, offs, lay["lens"], netif, 1, out=out)
+            el = (time.perf_counter() - t0) / steps
+            if registered:
+                _lib.lib.halo_rx_host_unregister(host.ctypes.data)
+                _lib.lib.halo_rx_host_unregister(out.ctypes.data)
+            fb = int(lay["lens"].astype(np.int64).sum())
+            res[name + ("_registered" if registered else "_pageable")] = {
+                "frames": n, "mpps": round(n / el / 1e6, 1), "gbit_s": round(fb * 8 / el / 1e9, 1),
+                "ms_per_batch": round(el * 1e3, 3), "ok": int((out["status"] == 0).sum()) == n}
+        hb.close()
+        del fr
+        torch.cuda.empty_cache()
+    return res
+
+
 def cpu_baseline(fr, seconds: float):
     """The C oracle (scalar restatement of the Go path) on the host, 1 thread, then all cores."""
     import numpy as np
@@ -297,6 +337,10 @@ def main():
                          "roofline": roofline(a2, k2, load_traffic(name))}
             del bs, o2
             torch.cuda.empty_cache()
+        # end to end from host memory: pinned H2D -> kernel -> D2H, double
+        # buffered in 64 MB chunks by halo_rx_parse_batch_host; the frame buffer is registered
+        # (pinned in place) so each chunk is one DMA straight from it
+        sec.update(e2e_host(dev, netif, steps=max(3, args.steps // 40)))
         line["secondary"] = sec
     if d.world == 1 and not args.no_cpu:  # rank 0 at N=1 only
         bs = make_batches(dev, netif, n=n, rotate=1, rank=0)

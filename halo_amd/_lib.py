@@ -117,6 +117,8 @@ _PROTOS = {
     "halo_rx_parse_batch_host": (ctypes.c_int, [
         ctypes.c_void_p, _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf),
         _u8p, _u8p]),
+    "halo_rx_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "halo_rx_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
     "halo_rx_dispatch": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_rx_dispatch_compact": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_synth_layout": (ctypes.c_int, [

@@ -131,7 +131,6 @@ struct halo_rx_host_ctx {
         uint8_t* h_bytes = nullptr;   // pinned staging
         uint32_t* h_off = nullptr;
         uint16_t* h_len = nullptr;
-        halo_rx_result_t* h_res = nullptr;
         uint8_t* d_bytes = nullptr;
         uint32_t* d_off = nullptr;
         uint16_t* d_len = nullptr;
@@ -151,7 +150,6 @@ void free_ctx(halo_rx_host_ctx* c) {
         if (s.h_bytes) (void)hipHostFree(s.h_bytes);
         if (s.h_off) (void)hipHostFree(s.h_off);
         if (s.h_len) (void)hipHostFree(s.h_len);
-        if (s.h_res) (void)hipHostFree(s.h_res);
         if (s.d_bytes) (void)hipFree(s.d_bytes);
         if (s.d_off) (void)hipFree(s.d_off);
         if (s.d_len) (void)hipFree(s.d_len);
@@ -182,8 +180,6 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
         ok = ok && hipHostMalloc((void**)&s.h_bytes, chunk_bytes, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipHostMalloc((void**)&s.h_off, 4ull * chunk_frames, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipHostMalloc((void**)&s.h_len, 2ull * chunk_frames, hipHostMallocDefault) == hipSuccess;
-        ok = ok && hipHostMalloc((void**)&s.h_res, sizeof(halo_rx_result_t) * chunk_frames,
-                                 hipHostMallocDefault) == hipSuccess;
         ok = ok && hipMalloc((void**)&s.d_bytes, chunk_bytes) == hipSuccess;
         ok = ok && hipMalloc((void**)&s.d_off, 4ull * chunk_frames) == hipSuccess;
         ok = ok && hipMalloc((void**)&s.d_len, 2ull * chunk_frames) == hipSuccess;
@@ -222,37 +218,62 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
     auto drain = [&](halo_rx_host_ctx::Slot& s) -> int {
         if (!s.busy) return HALO_OK;
         s.busy = false;
-        if (hipStreamSynchronize(s.stream) != hipSuccess) return HALO_E_HIP;
-        memcpy(out + s.first, s.h_res, sizeof(halo_rx_result_t) * s.count);
-        return HALO_OK;
+        return hipStreamSynchronize(s.stream) == hipSuccess ? HALO_OK : HALO_E_HIP;
     };
     uint64_t next = 0;
     uint32_t k = 0;
     while (next < n && rc == HALO_OK) {
         auto& s = ctx->slot[k & 1];
         if ((rc = drain(s))) break;
-        // pack frames [next, ...) into the pinned slot, 4-byte aligned (ring-record style)
+        // Direct mode: frames in order, 4-byte aligned relative to the first, spanning at most
+        // chunk_bytes (a drained ring segment, or a packed batch): one DMA of the caller's span
+        // (pinned if registered with halo_rx_host_register), no CPU copy of frame bytes.
         uint64_t used = 0;
         uint32_t cnt = 0;
-        while (next + cnt < n && cnt < ctx->chunk_frames) {
-            const uint32_t L = lens[next + cnt];
-            const uint64_t need = L <= cap ? ((L + 3u) & ~3u) : 0;  // over-long frames are never read
-            if (used + need > ctx->chunk_bytes) break;
-            if (need) memcpy(s.h_bytes + used, bytes + offsets[next + cnt], L);
-            s.h_off[cnt] = (uint32_t)(used >> 2);
-            s.h_len[cnt] = (uint16_t)L;
-            used += need;
-            ++cnt;
+        const uint8_t* src = s.h_bytes;
+        {
+            const uint64_t lo = offsets[next];
+            uint64_t hi = lo;
+            while (next + cnt < n && cnt < ctx->chunk_frames) {
+                const uint64_t o = offsets[next + cnt];
+                const uint64_t e = o + lens[next + cnt];
+                if (o < lo || ((o - lo) & 3u) || (e > hi ? e : hi) - lo > ctx->chunk_bytes) break;
+                s.h_off[cnt] = (uint32_t)((o - lo) >> 2);
+                s.h_len[cnt] = lens[next + cnt];
+                if (e > hi) hi = e;
+                ++cnt;
+            }
+            // take the direct path only when it covers the whole chunk's worth of frames
+            if (cnt > 0 && (next + cnt == n || cnt == ctx->chunk_frames || hi - lo > ctx->chunk_bytes / 2)) {
+                used = hi - lo;
+                src = bytes + lo;
+            } else {
+                cnt = 0;
+            }
+        }
+        // Pack mode: copy frames [next, ...) into the pinned slot, 4-byte aligned (ring-record style)
+        if (cnt == 0) {
+            while (next + cnt < n && cnt < ctx->chunk_frames) {
+                const uint32_t L = lens[next + cnt];
+                const uint64_t need = L <= cap ? ((L + 3u) & ~3u) : 0;  // over-long frames are never read
+                if (used + need > ctx->chunk_bytes) break;
+                if (need) memcpy(s.h_bytes + used, bytes + offsets[next + cnt], L);
+                s.h_off[cnt] = (uint32_t)(used >> 2);
+                s.h_len[cnt] = (uint16_t)L;
+                used += need;
+                ++cnt;
+            }
         }
         hipError_t e = hipSuccess;
-        if (used) e = hipMemcpyAsync(s.d_bytes, s.h_bytes, used, hipMemcpyHostToDevice, s.stream);
+        if (used) e = hipMemcpyAsync(s.d_bytes, src, used, hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, 4ull * cnt, hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess) e = hipMemcpyAsync(s.d_len, s.h_len, 2ull * cnt, hipMemcpyHostToDevice, s.stream);
         if (e != hipSuccess) { rc = HALO_E_HIP; break; }
         rc = halo_rx_parse_batch_device(s.d_bytes, s.d_off, s.d_len, cnt, flags, netif, 0, s.d_res,
                                         status_hist ? s.d_hist : nullptr, s.stream);
         if (rc) break;
-        if (hipMemcpyAsync(s.h_res, s.d_res, sizeof(halo_rx_result_t) * cnt, hipMemcpyDeviceToHost, s.stream) !=
+        // records go straight to the caller's array (full rate when it is pinned/registered)
+        if (hipMemcpyAsync(out + next, s.d_res, sizeof(halo_rx_result_t) * cnt, hipMemcpyDeviceToHost, s.stream) !=
             hipSuccess) { rc = HALO_E_HIP; break; }
         s.busy = true;
         s.first = next;
@@ -274,4 +295,15 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
         }
     }
     return rc;
+}
+
+extern "C" HALO_API int halo_rx_host_register(const void* ptr, uint64_t bytes) {
+    if (!ptr || !bytes) return HALO_E_INVAL;
+    return hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) == hipSuccess ? HALO_OK
+                                                                                                : HALO_E_HIP;
+}
+
+extern "C" HALO_API int halo_rx_host_unregister(const void* ptr) {
+    if (!ptr) return HALO_E_INVAL;
+    return hipHostUnregister(const_cast<void*>(ptr)) == hipSuccess ? HALO_OK : HALO_E_HIP;
 }

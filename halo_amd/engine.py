@@ -62,12 +62,14 @@ class HostBatcher:
         self.close()
 
     def parse(self, data: np.ndarray, offsets: np.ndarray, lens: np.ndarray, netif: NetIfAbi, flags: int,
-              hist: Optional[np.ndarray] = None) -> np.ndarray:
+              hist: Optional[np.ndarray] = None, out: Optional[np.ndarray] = None) -> np.ndarray:
         data = np.ascontiguousarray(data, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint16)
         n = lens.shape[0]
-        out = np.empty(n, dtype=RESULT_DTYPE)
+        if out is None:
+            out = np.empty(n, dtype=RESULT_DTYPE)
+        assert out.dtype == RESULT_DTYPE and out.shape[0] >= n and out.flags.c_contiguous
         if hist is not None:
             assert hist.dtype == np.uint32 and hist.flags.c_contiguous
         rc = _lib.lib.halo_rx_parse_batch_host(self._ctx, _lib.ptr(data), _lib.ptr(offsets), _lib.ptr(lens), n,

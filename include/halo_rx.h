@@ -202,6 +202,12 @@ HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* by
                                       const uint64_t* offsets, const uint16_t* lens, uint32_t n,
                                       uint32_t flags, const halo_rx_netif_t* netif,
                                       halo_rx_result_t* out, uint32_t* status_hist);
+/* Frames whose offsets are ascending and 4-byte aligned relative to each other (a drained ring
+ * segment, a packed batch) are sent with one DMA per chunk straight from `bytes`; registering
+ * that memory (e.g. the ring's hugepages) makes the DMA run at full PCIe rate. Other batches
+ * are repacked into pinned staging by the CPU.                                            */
+HALO_API int halo_rx_host_register(const void* ptr, uint64_t bytes);
+HALO_API int halo_rx_host_unregister(const void* ptr);
 
 /* ---- the reference engine's per-frame decision (engine/ethernet_engine.go:13-31,
  *      engine/ipv4_engine.go:18-47, engine/{udp,tcp,icmp}_engine.go) ------------------ */

@@ -374,6 +374,31 @@ def test_host_path_double_buffered(dev, golden, oracle_lib):
         hb.close()
 
 
+def test_host_path_direct_dma_registered(dev, oracle_lib):
+    """Packed host batch (ascending 4-byte-aligned offsets): the direct-DMA mode, with the
+    buffer registered and not, in chunks much smaller than the batch."""
+    from halo_amd import _lib, synth
+    from halo_amd._lib import NetIf
+    from halo_amd.engine import HostBatcher
+
+    lay = synth.layout(40_000, size_mode=1, proto_mode=3, mutate_shift=3, first_index=9_000_000)
+    data = oracle_lib.synth_batch(synth.SEED, 9_000_000, lay["lens"], lay["kinds"], oracle_lib.NetIf.make(),
+                                  offsets_dw=lay["offsets_dw"], fill=0x77)
+    offs = lay["offsets_dw"].astype(np.uint64) * 4
+    want, whist = oracle_lib.rx_batch(data, lay["lens"], oracle_lib.NetIf.make(), 1, offsets_dw=lay["offsets_dw"])
+    hb = HostBatcher(0, chunk_frames=3000, chunk_bytes=1 << 20)
+    for registered in (False, True):
+        if registered:
+            _lib.check("register", _lib.lib.halo_rx_host_register(data.ctypes.data, data.nbytes))
+        hist = np.zeros(14, np.uint32)
+        got = hb.parse(data, offs, lay["lens"], NetIf.make(), 1, hist)
+        if registered:
+            _lib.check("unregister", _lib.lib.halo_rx_host_unregister(data.ctypes.data))
+        assert_records_equal(got, want, None, f"host direct registered={registered}")
+        assert np.array_equal(hist, whist)
+    hb.close()
+
+
 def test_netif_packet_handle_batch(dev, golden, oracle_lib):
     """Batched PacketHandle: same actions as the reference engine, handlers get payloads."""
     from halo_amd import ACTION_NAMES
