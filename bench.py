@@ -260,12 +260,14 @@ def main():
     import torch
 
     d = Dist()
-    torch.cuda.set_device(d.local)
-    dev = torch.device("cuda", d.local)
+    # one process per GPU; ranks beyond the visible devices share them (rehearsals on fewer GPUs)
+    gpu = d.local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     from halo_amd import _lib
     from halo_amd._lib import NetIf
 
-    _lib.check("halo_rx_init", _lib.lib.halo_rx_init(d.local))
+    _lib.check("halo_rx_init", _lib.lib.halo_rx_init(gpu))
     netif = NetIf.make()  # eth0 of example.UsePcapDev (example/example.go:768-773)
     n = args.frames
 
