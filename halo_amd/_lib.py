@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libhalo_rx.so")
+# HALO_RX_LIB overrides the library path (A/B experiments with alternative builds only)
+LIB_PATH = os.environ.get("HALO_RX_LIB") or os.path.join(LIB_DIR, "libhalo_rx.so")
 
 # ---- constants mirrored from include/halo_rx.h ---------------------------------------
 HALO_OK = 0

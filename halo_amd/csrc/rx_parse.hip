@@ -92,12 +92,25 @@ __device__ __forceinline__ void load4(const uint8_t* frame, uint32_t d0, uint32_
     gu32* p = (gu32*)(reinterpret_cast<const uint32_t*>(frame) + d0);
     if (d0 + 4 <= ndw) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));  // 4-byte aligned 16 B
+#if HALO_RX_NT_LOADS
+        const u32x4 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)p);
+#else
         const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;
+#endif
         w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) w[j] = (d0 + j < ndw) ? p[j] : 0u;
     }
+}
+
+__device__ __forceinline__ void store16(uint4* dst, uint4 v) {
+#if HALO_RX_NT_STORES
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst));
+#else
+    *dst = v;
+#endif
 }
 
 // Accumulate the L4-segment bytes [34, seg_end) held in dwords [d0, d0+4).
@@ -300,9 +313,12 @@ __device__ __forceinline__ void frame_header(const FrameState<G>& st, uint32_t g
 }
 
 // Verdict after the L4 segment sum (this lane's or group's partial `c`), record store and count.
+// `stage` (lane-per-frame only): write the record to this wave's LDS staging slot instead of
+// global memory; the wave then stores its 64 consecutive records fully coalesced.
 template <int G>
 __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool present, uint32_t gl,
-                                            const uint32_t (&h)[12], Verdict& v, uint64_t c, Hist& hist) {
+                                            const uint32_t (&h)[12], Verdict& v, uint64_t c, Hist& hist,
+                                            uint4* stage = nullptr) {
     const uint32_t c32 = group_sum<G>(fold64(c));
     if (v.status == HALO_RX_OK && v.check_l4 && fold16(c32 + v.l4_extra) != 0xFFFFu) v.status = HALO_RX_L4_CKSUM;
     if (v.status == HALO_RX_OK && v.ip_proto != kIpUnknown) finish_l4(h, v);
@@ -322,10 +338,19 @@ __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool 
                 const uint32_t et_class = v.ethertype == kEthArp ? HALO_RX_F_ET_ARP
                                         : v.ethertype == kEthIpv6 ? HALO_RX_F_ET_IPV6
                                         : v.ethertype == kEthIeee8023 ? HALO_RX_F_ET_8023 : 0u;
-                reinterpret_cast<uint4*>(p.out)[i] =
+                const uint4 r16 =
                     make_uint4(v.status | ((v.flags | et_class) << 8) | (v.ip_proto << 16) | (v.l4_aux << 24),
                                v.src_ip, v.dst_ip, hi.x);
+                if constexpr (G == 1) {
+                    if (stage) stage[0] = r16;
+                    else reinterpret_cast<uint4*>(p.out)[i] = r16;
+                } else {
+                    reinterpret_cast<uint4*>(p.out)[i] = r16;
+                }
             }
+        } else if (G == 1 && stage) {
+            stage[0] = lo;
+            stage[1] = hi;
         } else {
             uint4* rec = reinterpret_cast<uint4*>(p.out + i);
             if constexpr (G == 1) {
@@ -346,7 +371,8 @@ __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool 
 // but the group still executes the collective steps.
 template <int G>
 __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool present, uint32_t gl,
-                                             uint32_t grp_base, FrameState<G>& st, Hist& hist) {
+                                             uint32_t grp_base, FrameState<G>& st, Hist& hist,
+                                             uint4* stage = nullptr) {
     constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
     constexpr int U0 = kRound0<G>;    // chunks already loaded
     constexpr int U = 4;              // 16-byte chunks in flight per lane per later round
@@ -368,7 +394,7 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
             for (int u = 0; u < U; ++u) acc_segment(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
         }
     }
-    frame_store<G>(p, i, present, gl, h, v, c, hist);
+    frame_store<G>(p, i, present, gl, h, v, c, hist, stage);
 }
 
 // The whole chain for frame i on a group of G lanes.
@@ -413,10 +439,40 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
 }
 
 // Lane per frame. SGPRs <= 80 lets 8 blocks of 256 threads share a CU (MI355X_MICROARCH.md
-// "Residency"); at 55 VGPRs that is the full 8 waves per SIMD.
+// "Residency"); at ~56 VGPRs that is the full 8 waves per SIMD. A wave's 64 records are
+// consecutive: they are staged in LDS and written with fully coalesced 16-byte stores (a lane
+// writing its own 32 B record at a 32 B stride stored the same bytes 25 % slower:
+// profiles/r01/probe_store_patterns.log).
 template <int LAYOUT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) rx_lane_kernel(const RxParams p) {
-    group_kernel_body<1, LAYOUT>(p);
+    __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
+    __shared__ uint4 s_rec[4][128];  // per wave: 64 records of 32 B
+    if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    Hist hist{s_hist, 0};
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = threadIdx.x >> 6;
+    const bool compact = (p.flags & HALO_RX_RECORD_COMPACT) != 0;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t base = wave * 64; base < p.n; base += nwaves * 64) {
+        const uint32_t i = base + lane;
+        FrameState<1> st;
+        frame_meta<LAYOUT>(p, i, i < p.n, st);
+        frame_loads<1>(0, st);
+        frame_finish<1>(p, i, i < p.n, 0, lane, st, hist, &s_rec[w][compact ? lane : 2 * lane]);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t nrec = p.n - base < 64 ? p.n - base : 64;  // records of this wave
+        if (compact) {
+            if (lane < nrec) store16(reinterpret_cast<uint4*>(p.out) + base + lane, s_rec[w][lane]);
+        } else {
+            uint4* out4 = reinterpret_cast<uint4*>(p.out) + 2ull * base;
+            if (lane < 2 * nrec) store16(out4 + lane, s_rec[w][lane]);
+            if (64 + lane < 2 * nrec) store16(out4 + 64 + lane, s_rec[w][64 + lane]);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    flush_hist(p, hist);
 }
 
 // G lanes per frame (G in {4, 8, 16}); VGPR-limited occupancy, so no SGPR cap.

@@ -96,6 +96,32 @@ __global__ void __launch_bounds__(256) p_lds(const uint8_t* __restrict__ bytes, 
     rec[2 * i + 1] = make_uint4(d.w, s ^ 1, s ^ 2, s ^ 3);
 }
 
+// record-store shapes (no reads): lane-strided 2 x 16 B (the kernel's), LDS-transposed fully
+// coalesced 16 B per lane, and non-temporal lane-strided
+template <int MODE>
+__global__ void __launch_bounds__(256) p_store(uint4* __restrict__ rec, uint32_t n) {
+    __shared__ uint4 lds[4][128];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 lo = make_uint4(i, i ^ 1, i ^ 2, i ^ 3), hi = make_uint4(i ^ 4, i ^ 5, i ^ 6, i ^ 7);
+    if (MODE == 0) {
+        rec[2 * i] = lo;
+        rec[2 * i + 1] = hi;
+    } else if (MODE == 1) {
+        const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, base = i - lane;
+        lds[w][2 * lane] = lo;
+        lds[w][2 * lane + 1] = hi;
+        __builtin_amdgcn_wave_barrier();
+        rec[2 * base + lane] = lds[w][lane];
+        rec[2 * base + 64 + lane] = lds[w][64 + lane];
+    } else {
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        v4* r = reinterpret_cast<v4*>(rec);
+        __builtin_nontemporal_store((v4){lo.x, lo.y, lo.z, lo.w}, &r[2 * i]);
+        __builtin_nontemporal_store((v4){hi.x, hi.y, hi.z, hi.w}, &r[2 * i + 1]);
+    }
+}
+
 int main() {
     const int R = 8, K = 40;
     std::vector<uint8_t*> bytes(R);
@@ -137,6 +163,18 @@ int main() {
     };
     const double fr_mb = N * (double)FB / 1e6, rec_mb = N * 32.0 / 1e6, meta_mb = N * 6.0 / 1e6;
     for (int rep = 0; rep < 2; ++rep) {
+        run("store 32 MB records, lane-strided 2x16B", rec_mb, [&](int r) {
+            (void)r;
+            hipLaunchKernelGGL((p_store<0>), dim3(N / 256), dim3(256), 0, 0, rec, N);
+        });
+        run("store 32 MB records, LDS-transposed", rec_mb, [&](int r) {
+            (void)r;
+            hipLaunchKernelGGL((p_store<1>), dim3(N / 256), dim3(256), 0, 0, rec, N);
+        });
+        run("store 32 MB records, nontemporal", rec_mb, [&](int r) {
+            (void)r;
+            hipLaunchKernelGGL((p_store<2>), dim3(N / 256), dim3(256), 0, 0, rec, N);
+        });
         run("coalesced read 64 MB", fr_mb, [&](int r) {
             hipLaunchKernelGGL(p_coalesced, dim3(N * FB / 16 / 256), dim3(256), 0, 0, (const uint4*)bytes[r], sink,
                                N * FB / 16);
