@@ -126,6 +126,10 @@ def bench_lib():
         L.halo_bench_steps.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                        ctypes.c_uint32, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp,
                                        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
+        L.halo_bench_tx_steps.restype = ctypes.c_int
+        L.halo_bench_tx_steps.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_uint32,
+                                          ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp,
+                                          ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
         _BENCH_LIB = L
     return _BENCH_LIB
 
@@ -155,6 +159,52 @@ def time_steps(batches, out, netif, *, flags, hint, steps, warmup, d: Dist, stri
                                       steps, torch.cuda.current_stream().cuda_stream, ctypes.byref(region),
                                       ctypes.byref(wall))
     _lib.check("halo_bench_steps", rc)
+    torch.cuda.synchronize()
+    d.barrier()
+    return d.max(wall.value), region.value / steps
+
+
+TX_BENCH_STEPS = 0x01 | 0x04 | 0x10  # NatChangeDst + NatChangeSrc + eth_tx DPDK fill
+TX_WRITE_BYTES = 20  # header dwords 6..10 rewritten per UDP frame (addresses, ports, both checksums)
+
+
+def tx_ops_for(n: int):
+    """Per-frame halo_tx_op_t records for the transmit bench: seeded addresses and ports per frame.
+    No TTL step: repeated passes over the same batches must do identical work (a TTL step would
+    move frames to the TTL-exceeded branch after <= 255 passes)."""
+    import numpy as np
+
+    from halo_amd import protocol
+
+    rng = np.random.default_rng(0x5458)
+    ops = protocol.tx_ops(n, TX_BENCH_STEPS)
+    ops["dst_ip"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    ops["src_ip"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    ops["dst_port"] = rng.integers(1, 1 << 16, n, dtype=np.uint32).astype(np.uint16)
+    ops["src_port"] = rng.integers(1, 1 << 16, n, dtype=np.uint32).astype(np.uint16)
+    return ops
+
+
+def time_tx_steps(batches, ops_dev, res_dev, *, flags, hint, steps, warmup, d: Dist):
+    """time_steps for halo_tx_fixup_batch_device (frames rewritten in place each launch)."""
+    import ctypes
+
+    import torch
+
+    from halo_amd import _lib
+
+    nb = len(batches)
+    arr = lambda xs: (ctypes.c_void_p * nb)(*xs)  # noqa: E731
+    region, wall = ctypes.c_float(), ctypes.c_double()
+    torch.cuda.synchronize()
+    d.barrier()
+    rc = bench_lib().halo_bench_tx_steps(nb, arr([b["bytes"].data_ptr() for b in batches]),
+                                         arr([b["offsets_dw"].data_ptr() for b in batches]),
+                                         arr([b["lens"].data_ptr() for b in batches]), batches[0]["layout"]["n"],
+                                         ops_dev.data_ptr(), flags, hint, res_dev.data_ptr(), warmup, steps,
+                                         torch.cuda.current_stream().cuda_stream, ctypes.byref(region),
+                                         ctypes.byref(wall))
+    _lib.check("halo_bench_tx_steps", rc)
     torch.cuda.synchronize()
     d.barrier()
     return d.max(wall.value), region.value / steps
@@ -315,7 +365,19 @@ def main():
         algc = fbytes + n * (4 + 2 + 16)
         sec["config2_compact_record16"] = {"mpps": round(n * args.steps / wc / 1e6, 1), "kernel_ms": round(kc, 5),
                                            "roofline": roofline(algc, kc)}
-        del batches
+        # forward / transmit rewrite (§8f row f2) on the headline frames: DNAT + SNAT + DPDK fill
+        import numpy as np
+
+        ops_h = tx_ops_for(n)
+        ops_d = torch.from_numpy(ops_h.view(np.uint8)).to(dev)
+        res_d = torch.empty(n, dtype=torch.uint8, device=dev)
+        wt, kt = time_tx_steps(batches, ops_d, res_d, flags=1, hint=64, steps=args.steps, warmup=args.warmup, d=d)
+        algt = fbytes + n * (4 + 2 + 16 + 1 + TX_WRITE_BYTES)
+        sec["tx_fixup_config2_nat_dpdk"] = {
+            "mpps": round(n * args.steps / wt / 1e6, 1), "kernel_ms": round(kt, 5),
+            "roofline": roofline(algt, kt, load_traffic("tx_config2")), "alg_bytes_per_launch": algt,
+            "steps": "NatChangeDst + NatChangeSrc + eth_tx DPDK fill, per-frame addresses/ports"}
+        del batches, ops_d, res_d
         torch.cuda.empty_cache()
         for name, kw, hint, strided_len, flags in [
             ("1500B_udp_1M", dict(length=1500), 1500, 0, 1),

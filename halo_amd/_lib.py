@@ -77,6 +77,14 @@ def compact_of(full: np.ndarray) -> np.ndarray:
     out["flags"] = full["flags"] | cls
     return out
 
+# halo_tx_op_t (16 bytes): per-frame steps of halo_tx_fixup_batch_device
+TX_OP_DTYPE = np.dtype([("steps", "u1"), ("pad", "u1"), ("dst_port", "<u2"), ("dst_ip", "<u4"),
+                        ("src_port", "<u2"), ("pad2", "<u2"), ("src_ip", "<u4")])
+assert TX_OP_DTYPE.itemsize == 16
+TX_NAT_DST, TX_TTL, TX_NAT_SRC, TX_RECALC, TX_DPDK_FILL = 0x01, 0x02, 0x04, 0x08, 0x10
+TX_R_TTL_ALIVE, TX_R_SKIPPED, TX_R_OVERRUN = 0x01, 0x02, 0x04
+
+
 class NetIf(ctypes.Structure):
     """halo_rx_netif_t — engine.NetIfConfig's MacAddr / IpAddr / NatEnable."""
 
@@ -122,6 +130,8 @@ _PROTOS = {
     "halo_rx_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
     "halo_rx_dispatch": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_rx_dispatch_compact": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
+    "halo_tx_fixup_batch_device": (ctypes.c_int, [
+        _u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_synth_layout": (ctypes.c_int, [
         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint64)]),

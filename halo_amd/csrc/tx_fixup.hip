@@ -1,0 +1,364 @@
+// tx_fixup.hip — SURVEY.md §8f row f2 on gfx950: the forward / transmit direction of halo's
+// packet path, rewritten in place over a batch of frames resident in HBM.
+//
+// Restates bit-exactly, per frame (pkt = frame[14:len], engine/ipv4_engine.go:31-37):
+//   NatChangeDst / NatChangeSrc   protocol/ipv4.go:277-302, :249-275
+//   HandleIpv4PktTtl              protocol/ipv4.go:134-145
+//   ReCalcIpv4 / Icmp / Tcp / UdpCheckSum   protocol/ipv4.go:148-226
+//   eth_tx software checksum fill cgo/dpdk.c:333-365 (DPDK 20.11 rte_ipv4_cksum /
+//                                  rte_ipv4_udptcp_cksum, restated in oracle/halo_tx_oracle.c)
+// in the order Ipv4RouteForward applies them (engine/ipv4_engine.go:108-269).
+//
+// Shape: the rx kernel's (rx_parse.hip) — G lanes of a wave per frame, 16-byte loads, header
+// dwords 0..12 broadcast to the group. Every step only rewrites header bytes (< 52), and every
+// checksum the steps ask for is a function of the FINAL packet bytes (no checksum field lies in
+// another checksum's range), so the steps are first applied to a register copy of the header,
+// then each needed checksum is summed once over the final bytes: header dwords from the copy,
+// the rest of the frame from the loads. Sums are taken in the little-endian dword domain (see
+// rx_parse.hip): the stored field, read as a little-endian half-word, is ~fold(sum) — for the
+// Go functions (big-endian store of ^fold(BE sum)) and for DPDK (host-order store of
+// ~rte_raw_cksum) alike. One lane per frame then writes the dirty header dwords back.
+#include <hip/hip_runtime.h>
+
+#include "device_util.h"
+#include "halo_common.h"
+
+namespace halo {
+namespace {
+
+struct TxParams {
+    uint8_t* bytes;
+    const uint32_t* offsets_dw;
+    const uint16_t* lens;
+    const halo_tx_op_t* ops;
+    uint32_t n;
+    uint32_t flags;
+    uint8_t* result;
+};
+
+constexpr uint32_t kGoSteps = HALO_TX_NAT_DST | HALO_TX_TTL | HALO_TX_NAT_SRC | HALO_TX_RECALC;
+constexpr uint32_t kHdrDw = 13;  // header dwords 0..12 (frame bytes 0..51: up to the TCP checksum)
+
+// byte b of the header copy / a big-endian 16-bit field at even frame offset b
+#define MB(b) ((m[(b) >> 2] >> (((b)&3) * 8)) & 0xFFu)
+#define SET_BE16(b, v)                                                                              \
+    do {                                                                                            \
+        constexpr uint32_t sh_ = ((b)&2) * 8;                                                       \
+        m[(b) >> 2] = (m[(b) >> 2] & ~(0xFFFFu << sh_)) | (bswap16((uint32_t)(v)&0xFFFFu) << sh_); \
+        dirty |= 1u << ((b) >> 2);                                                                  \
+    } while (0)
+#define SET_LE16(b, v)                                                                              \
+    do {                                                                                            \
+        constexpr uint32_t sh_ = ((b)&2) * 8;                                                       \
+        m[(b) >> 2] = (m[(b) >> 2] & ~(0xFFFFu << sh_)) | (((uint32_t)(v)&0xFFFFu) << sh_);         \
+        dirty |= 1u << ((b) >> 2);                                                                  \
+    } while (0)
+
+// bytes of dword d inside [lo, hi)
+__device__ __forceinline__ uint32_t range_keep(uint32_t d, uint32_t lo, uint32_t hi) {
+    const int32_t s = (int32_t)lo - (int32_t)(4u * d);
+    const int32_t e = (int32_t)hi - (int32_t)(4u * d);
+    const uint32_t k_hi = e >= 4 ? 0xFFFFFFFFu : (e <= 0 ? 0u : ((1u << (e * 8)) - 1u));
+    const uint32_t k_lo = s <= 0 ? 0xFFFFFFFFu : (s >= 4 ? 0u : ~((1u << (s * 8)) - 1u));
+    return k_hi & k_lo;
+}
+
+// [lo, hi) restricted to the header copy (dwords 3..12); sum of half-words, < 2^21
+__device__ __forceinline__ uint32_t header_sum(const uint32_t (&m)[kHdrDw], uint32_t lo, uint32_t hi) {
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t d = 3; d < kHdrDw; ++d) s += hsum(m[d] & range_keep(d, lo, hi));
+    return s;
+}
+
+// bytes [4*kHdrDw, hi) of the loaded dwords [d0, d0+4); the header part comes from the copy
+__device__ __forceinline__ void acc_tail(const uint32_t (&w)[4], uint32_t d0, uint32_t hi, uint64_t& c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t d = d0 + j;
+        const int32_t rel = (int32_t)hi - (int32_t)(4u * d);
+        uint32_t keep = rel >= 4 ? 0xFFFFFFFFu : (rel <= 0 ? 0u : ((1u << (rel * 8)) - 1u));
+        keep = d >= kHdrDw ? keep : 0u;
+        c += (uint64_t)(w[j] & keep);
+    }
+}
+
+struct TxPlan {
+    uint32_t ip_hi;      // IPv4 header checksum over [14, ip_hi); 0: no sum
+    uint32_t l4_hi;      // L4 checksum over [34, l4_hi) + l4_extra; 0: no sum
+    uint32_t l4_extra;   // pseudo header, LE domain
+    uint32_t l4_field;   // frame offset of the L4 checksum field being summed (0: none)
+    bool udp_zero_ffff;  // DPDK: a zero UDP checksum is sent as 0xFFFF
+};
+
+// Apply the steps to the header copy; returns the checksum plan. All lanes of a group run this
+// on identical inputs. `skip`/`alive`/`overrun` feed the result byte.
+__device__ __forceinline__ TxPlan apply_steps(uint32_t (&m)[kHdrDw], uint32_t& dirty, uint32_t L, uint32_t steps,
+                                              uint32_t dst_ip, uint32_t dst_port, uint32_t src_ip,
+                                              uint32_t src_port, bool en, uint32_t& res) {
+    TxPlan pl{0, 0, 0, 0, false};
+    bool skip = false;
+    if (L < 14) {  // no IPv4 packet: every Go step returns on its length guard
+        res = (steps & kGoSteps) ? HALO_TX_R_SKIPPED : 0u;
+        return pl;
+    }
+    const uint32_t len = L - 14;
+    const uint32_t proto = MB(23);
+    bool ip_go = false;   // a Go ReCalcIpv4CheckSum ran
+    uint32_t l4_go = 0;   // the Go L4 recalc that ran: 1 ICMP, 6 TCP, 17 UDP
+
+    // Go ReCalc* on the current packet (their guards; the field is (re)computed at the end)
+    auto recalc_ip = [&]() { if (len < 20) skip = true; else ip_go = true; };
+    auto recalc_l4 = [&]() {
+        if (proto == kIpIcmp) { if (len < 24) skip = true; else l4_go = kIpIcmp; }
+        else if (proto == kIpTcp) { if (len < 38) skip = true; else l4_go = kIpTcp; }
+        else if (proto == kIpUdp) { if (len < 28) skip = true; else l4_go = kIpUdp; }
+    };
+    bool alive = true;
+    if (steps & HALO_TX_NAT_DST) {  // protocol/ipv4.go:277-302
+        if (len < 26) {
+            skip = true;
+        } else {
+            SET_BE16(30, dst_ip >> 16);
+            SET_BE16(32, dst_ip);
+            recalc_ip();
+            // ICMP: echo identifier (frame 38..39), TCP/UDP: destination port (36..37); both in
+            // dword 9 (selects, not branches: branches let the compiler index m dynamically)
+            const uint32_t pw = bswap16(dst_port & 0xFFFFu);
+            const bool icmp = proto == kIpIcmp, tu = proto == kIpTcp || proto == kIpUdp;
+            m[9] = icmp ? (m[9] & 0xFFFFu) | (pw << 16) : tu ? (m[9] & 0xFFFF0000u) | pw : m[9];
+            dirty |= (icmp || tu) ? 1u << 9 : 0u;
+            recalc_l4();
+        }
+    }
+    if (steps & HALO_TX_TTL) {  // protocol/ipv4.go:134-145
+        if (len < 9) {
+            skip = true;
+            alive = false;
+        } else if (MB(22) <= 1u) {
+            alive = false;
+        } else {
+            m[5] -= 1u << 16;  // pkt[8]-- (frame byte 22, > 1 so no borrow)
+            dirty |= 1u << 5;
+            recalc_ip();
+        }
+    }
+    if (alive) {
+        if (steps & HALO_TX_NAT_SRC) {  // protocol/ipv4.go:249-275
+            if (len < 26) {
+                skip = true;
+            } else {
+                SET_BE16(26, src_ip >> 16);
+                SET_BE16(28, src_ip);
+                recalc_ip();
+                // ICMP: echo identifier (frame 38..39, dword 9), TCP/UDP: source port (34..35, dword 8)
+                const uint32_t pw = bswap16(src_port & 0xFFFFu);
+                const bool icmp = proto == kIpIcmp, tu = proto == kIpTcp || proto == kIpUdp;
+                m[9] = icmp ? (m[9] & 0xFFFFu) | (pw << 16) : m[9];
+                m[8] = tu ? (m[8] & 0xFFFFu) | (pw << 16) : m[8];
+                dirty |= (icmp ? 1u << 9 : 0u) | (tu ? 1u << 8 : 0u);
+                recalc_l4();
+            }
+        }
+        if (steps & HALO_TX_RECALC) {
+            recalc_ip();
+            if (len >= 10) recalc_l4();
+        }
+    }
+    res = (alive && (steps & HALO_TX_TTL) ? HALO_TX_R_TTL_ALIVE : 0u) | (skip ? HALO_TX_R_SKIPPED : 0u);
+
+    // Go checksums: field zeroed; summed when CheckSumEnable (ICMP: always)
+    if (ip_go) {
+        SET_LE16(24, 0);
+        if (en) pl.ip_hi = 34;
+    }
+    const uint32_t sum_addrs = (m[6] >> 16) + hsum(m[7]) + (m[8] & 0xFFFFu);  // pseudo src+dst
+    if (l4_go == kIpIcmp) {
+        SET_LE16(36, 0);
+        pl.l4_hi = L;
+        pl.l4_field = 36;
+    } else if (l4_go) {
+        const uint32_t f = l4_go == kIpTcp ? 50u : 40u;
+        if (f == 50u) SET_LE16(50, 0);
+        else SET_LE16(40, 0);
+        if (en) {
+            const uint32_t total_len = bswap16(m[4] & 0xFFFFu);  // frame bytes 16..17
+            pl.l4_hi = L;
+            pl.l4_field = f;
+            pl.l4_extra = sum_addrs + (l4_go << 8) + bswap16((total_len - 20u) & 0xFFFFu);  // Go int, 2 bytes
+        }
+    }
+
+    // eth_tx software fill (cgo/dpdk.c:333-365), after everything else
+    if (alive && (steps & HALO_TX_DPDK_FILL) && (m[3] & 0xFFFFu) == 0x0008u) {
+        if (L < 34) {
+            res |= HALO_TX_R_OVERRUN;
+        } else {
+            SET_LE16(24, 0);
+            const uint32_t ihl4 = (MB(14) & 0xFu) * 4u;
+            if (14u + ihl4 <= L) pl.ip_hi = 14u + ihl4;
+            else { pl.ip_hi = 0; res |= HALO_TX_R_OVERRUN; }
+            if (proto == kIpUdp || proto == kIpTcp) {
+                const uint32_t f = proto == kIpUdp ? 40u : 50u;
+                if (f + 2u > L) {
+                    res |= HALO_TX_R_OVERRUN;  // (a Go L4 recalc cannot have run: its guard is stricter)
+                } else {
+                    if (f == 50u) SET_LE16(50, 0);
+                    else SET_LE16(40, 0);
+                    pl.l4_hi = 0; pl.l4_field = 0; pl.l4_extra = 0;  // DPDK's value replaces Go's
+                    const uint32_t l3 = bswap16(m[4] & 0xFFFFu);
+                    if (l3 >= ihl4) {
+                        const uint32_t l4_len = l3 - ihl4;
+                        if (34u + l4_len > L) {
+                            res |= HALO_TX_R_OVERRUN;
+                        } else {
+                            pl.l4_hi = 34u + l4_len;
+                            pl.l4_field = f;
+                            pl.l4_extra = sum_addrs + (proto << 8) + bswap16(l4_len);
+                            pl.udp_zero_ffff = proto == kIpUdp;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    return pl;
+}
+
+template <int G>
+__device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool present, uint32_t gl, uint32_t grp_base) {
+    constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
+    constexpr int U0 = 4;             // 16-byte chunks per lane in round 0 (>= the 52-byte header)
+    constexpr int U = 4;
+    uint8_t* frame = p.bytes;
+    uint32_t L = 0;
+    uint4 op = make_uint4(0, 0, 0, 0);
+    if (present) {
+        frame = p.bytes + ((uint64_t)p.offsets_dw[i] << 2);
+        L = p.lens[i];
+        op = reinterpret_cast<const uint4*>(p.ops)[i];
+    }
+    const uint32_t steps = op.x & 0xFFu;
+    const uint32_t ndw = (present && L >= 14 && steps) ? (L + 3) >> 2 : 0;  // nothing is read for no work
+    uint32_t buf[U0][4];
+#pragma unroll
+    for (int u = 0; u < U0; ++u) load4(frame, (u * G + gl) * 4, ndw, buf[u]);
+    uint32_t m[kHdrDw];
+    if constexpr (G == 1) {
+#pragma unroll
+        for (uint32_t j = 0; j < kHdrDw; ++j) m[j] = buf[j >> 2][j & 3];
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            m[j] = group_bcast<G, 0>(buf[0][j], grp_base);
+            m[4 + j] = group_bcast<G, 1>(buf[0][j], grp_base);
+            m[8 + j] = group_bcast<G, 2>(buf[0][j], grp_base);
+        }
+        m[12] = group_bcast<G, 3>(buf[0][0], grp_base);
+    }
+    uint32_t dirty = 0, res = 0;
+    const TxPlan pl = apply_steps(m, dirty, L, steps, op.y,
+                                  op.x >> 16, op.w, op.z & 0xFFFFu, (p.flags & HALO_RX_CSUM_ENABLE) != 0, res);
+
+    // sums over the final bytes: the header copy + this lane's loaded dwords past it
+    uint64_t c_ip = 0, c_l4 = 0;
+    const uint32_t hi = pl.ip_hi > pl.l4_hi ? pl.ip_hi : pl.l4_hi;
+    if (hi > 4 * kHdrDw) {
+#pragma unroll
+        for (int u = 0; u < U0; ++u) {
+            acc_tail(buf[u], (u * G + gl) * 4, pl.ip_hi, c_ip);
+            acc_tail(buf[u], (u * G + gl) * 4, pl.l4_hi, c_l4);
+        }
+        const uint32_t seg_dw = (hi + 3) >> 2;
+        for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
+            uint32_t x[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load4(frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc_tail(x[u], r0 + (u * G + gl) * 4, pl.ip_hi, c_ip);
+                acc_tail(x[u], r0 + (u * G + gl) * 4, pl.l4_hi, c_l4);
+            }
+        }
+    }
+    const uint32_t g_ip = group_sum<G>(fold64(c_ip));
+    const uint32_t g_l4 = group_sum<G>(fold64(c_l4));
+    if (pl.ip_hi) {
+        const uint32_t s = fold16(fold64((uint64_t)g_ip + header_sum(m, 14, pl.ip_hi)));
+        SET_LE16(24, ~s);
+    }
+    if (pl.l4_hi) {
+        const uint32_t s = fold16(fold64((uint64_t)g_l4 + header_sum(m, 34, pl.l4_hi) + pl.l4_extra));
+        uint32_t f = (~s) & 0xFFFFu;
+        if (pl.udp_zero_ffff && f == 0) f = 0xFFFFu;
+        if (pl.l4_field == 36u) SET_LE16(36, f);
+        else if (pl.l4_field == 40u) SET_LE16(40, f);
+        else SET_LE16(50, f);
+    }
+
+    if (present && gl == 0) {
+        __attribute__((address_space(1))) uint32_t* fw =
+            (__attribute__((address_space(1))) uint32_t*)reinterpret_cast<uint32_t*>(frame);
+#pragma unroll
+        for (uint32_t d = 3; d < kHdrDw; ++d) {
+            if (dirty & (1u << d)) {
+                if (4 * d + 4 <= L) {
+                    fw[d] = m[d];
+                } else {
+                    for (uint32_t b = 4 * d; b < L; ++b) frame[b] = (uint8_t)(m[d] >> ((b & 3) * 8));
+                }
+            }
+        }
+        if (p.result) p.result[i] = (uint8_t)res;
+    }
+}
+#undef MB
+#undef SET_BE16
+#undef SET_LE16
+
+template <int G>
+__global__ void __launch_bounds__(256) tx_fixup_kernel(const TxParams p) {
+    constexpr uint32_t FPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp_base = lane & ~(uint32_t)(G - 1);
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t base = wave * FPW; base < p.n; base += nwaves * FPW) {
+        const uint32_t i = base + lane / G;
+        tx_frame<G>(p, i, i < p.n, gl, grp_base);
+    }
+}
+
+uint32_t tx_grid(uint64_t n, uint32_t frames_per_wave) {
+    const uint64_t waves = (n + frames_per_wave - 1) / frames_per_wave;
+    const uint64_t blocks = (waves + 3) / 4;
+    const uint64_t kMaxBlocks = 256ull * 8 * 8;
+    return (uint32_t)(blocks > kMaxBlocks ? kMaxBlocks : blocks);
+}
+
+}  // namespace
+}  // namespace halo
+
+extern "C" HALO_API int halo_tx_fixup_batch_device(uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                                   const uint16_t* d_lens, uint32_t n,
+                                                   const halo_tx_op_t* d_ops, uint32_t flags,
+                                                   uint32_t max_len_hint, uint8_t* d_result,
+                                                   halo_stream_t stream) {
+    if (flags & ~(uint32_t)HALO_RX_CSUM_ENABLE) return HALO_E_INVAL;
+    if (n == 0) return HALO_OK;
+    if (!d_bytes || !d_offsets_dw || !d_lens || !d_ops) return HALO_E_INVAL;
+    if (reinterpret_cast<uintptr_t>(d_bytes) & 3u || reinterpret_cast<uintptr_t>(d_ops) & 15u) return HALO_E_INVAL;
+    int rc = halo::check_device();
+    if (rc) return rc;
+    halo::TxParams p{d_bytes, d_offsets_dw, d_lens, d_ops, n, flags, d_result};
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 block(256);
+    // lanes per frame from the longest frame (0: unknown -> widest); any G handles any length
+    const uint32_t h = max_len_hint ? max_len_hint : 65535u;
+    if (h <= 128) hipLaunchKernelGGL(halo::tx_fixup_kernel<1>, dim3(halo::tx_grid(n, 64)), block, 0, s, p);
+    else if (h <= 1024) hipLaunchKernelGGL(halo::tx_fixup_kernel<4>, dim3(halo::tx_grid(n, 16)), block, 0, s, p);
+    else if (h <= 4096) hipLaunchKernelGGL(halo::tx_fixup_kernel<8>, dim3(halo::tx_grid(n, 8)), block, 0, s, p);
+    else hipLaunchKernelGGL(halo::tx_fixup_kernel<16>, dim3(halo::tx_grid(n, 4)), block, 0, s, p);
+    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}

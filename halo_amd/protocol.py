@@ -130,3 +130,41 @@ def status_name(code: int) -> str:
 
 
 __all__ = [name for name in dir() if not name.startswith("_")] + ["STATUS"]
+
+
+# ---- forward / transmit direction -------------------------------------
+# Step bits of halo_tx_op_t.steps: NatChangeDst, HandleIpv4PktTtl, NatChangeSrc, the ReCalc*
+# pair for the packet's protocol, and eth_tx's DPDK software checksum fill, applied in the order
+# Ipv4RouteForward applies them (engine/ipv4_engine.go:108-269).
+from ._lib import (TX_DPDK_FILL, TX_NAT_DST, TX_NAT_SRC, TX_OP_DTYPE, TX_R_OVERRUN,  # noqa: E402
+                   TX_R_SKIPPED, TX_R_TTL_ALIVE, TX_RECALC, TX_TTL)
+
+
+
+
+def tx_ops(n: int, steps: int = 0, dst_ip: int = 0, dst_port: int = 0, src_ip: int = 0, src_port: int = 0):
+    """A host halo_tx_op_t array (numpy) with every field broadcast; edit per frame as needed."""
+    ops = np.zeros(n, dtype=TX_OP_DTYPE)
+    ops["steps"], ops["dst_ip"], ops["dst_port"], ops["src_ip"], ops["src_port"] = (
+        steps, dst_ip, dst_port, src_ip, src_port)
+    return ops
+
+
+def tx_fixup_batch(frames, offsets_dw, lens, ops, *, check_sum_enable: bool = True, max_len_hint: int = 0,
+                   result=None, stream=None):
+    """Rewrite a device-resident ragged batch in place (halo_tx_fixup_batch_device).
+
+    frames: cuda uint8 tensor (modified); offsets_dw / lens as parse_frames_batch; ops: cuda
+    uint8 tensor of n*16 bytes holding halo_tx_op_t records (``torch.from_numpy(tx_ops(...)
+    .view(np.uint8)).cuda()``). ``result`` (cuda uint8[n], optional) receives HALO_TX_R_* per
+    frame. Asynchronous on ``stream``; returns ``result``.
+    """
+    n = int(lens.numel())
+    assert ops.is_cuda and ops.numel() >= 16 * n, "ops: cuda uint8[n*16]"
+    if result is not None:
+        assert result.is_cuda and result.numel() >= n
+    rc = _lib.lib.halo_tx_fixup_batch_device(
+        _lib.ptr(frames), _lib.ptr(offsets_dw), _lib.ptr(lens), n, _lib.ptr(ops),
+        HALO_RX_CSUM_ENABLE if check_sum_enable else 0, max_len_hint, _lib.ptr(result), _stream_handle(stream))
+    _lib.check("halo_tx_fixup_batch_device", rc)
+    return result

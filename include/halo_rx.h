@@ -209,6 +209,48 @@ HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* by
 HALO_API int halo_rx_host_register(const void* ptr, uint64_t bytes);
 HALO_API int halo_rx_host_unregister(const void* ptr);
 
+/* ---- forward / transmit direction: in-place header rewrite + checksum fill --------------
+ * (SURVEY.md §8f row f2). Frame i's IPv4 packet is pkt = frame[14 : len] — exactly the slice
+ * engine.RxIpv4 hands to Ipv4RouteForward (engine/ipv4_engine.go:31-37) — and each frame gets
+ * the steps set in ops[i].steps, applied in this order (the order Ipv4RouteForward applies
+ * them, engine/ipv4_engine.go:108-269):
+ *   HALO_TX_NAT_DST   NatChangeDst(pkt, dst_ip, dst_port)      protocol/ipv4.go:277-302
+ *   HALO_TX_TTL       HandleIpv4PktTtl(pkt)                    protocol/ipv4.go:134-145
+ *   HALO_TX_NAT_SRC   NatChangeSrc(pkt, src_ip, src_port)      protocol/ipv4.go:249-275
+ *   HALO_TX_RECALC    ReCalcIpv4CheckSum + the L4 ReCalc* picked by pkt[9]
+ *                                                               protocol/ipv4.go:148-226
+ *   HALO_TX_DPDK_FILL eth_tx's software checksum fill (cgo/dpdk.c:333-365: rte_ipv4_cksum and
+ *                     rte_ipv4_udptcp_cksum of DPDK 20.11, the reference's pinned DPDK)
+ * `flags & HALO_RX_CSUM_ENABLE` is protocol.CheckSumEnable for the Go steps (ReCalcIcmp and
+ * DPDK_FILL ignore it, as the reference does). Every length guard of the Go functions is kept:
+ * a step whose guard fails leaves the packet as Go would. Result byte per frame: HALO_TX_R_*. */
+#define HALO_TX_NAT_DST 0x01u
+#define HALO_TX_TTL 0x02u
+#define HALO_TX_NAT_SRC 0x04u
+#define HALO_TX_RECALC 0x08u
+#define HALO_TX_DPDK_FILL 0x10u
+#define HALO_TX_R_TTL_ALIVE 0x01u /* HandleIpv4PktTtl returned true                        */
+#define HALO_TX_R_SKIPPED 0x02u   /* a step's length guard left the packet (partly) as is   */
+#define HALO_TX_R_OVERRUN 0x04u   /* DPDK_FILL: IPv4 totalLen runs past the frame (DPDK would
+                                     read stale mbuf bytes); L4 checksum left zero          */
+typedef struct halo_tx_op {
+    uint8_t steps;     /* HALO_TX_* */
+    uint8_t pad;
+    uint16_t dst_port; /* NatChangeDst port */
+    uint32_t dst_ip;   /* NatChangeDst address, IpAddrToU form */
+    uint16_t src_port; /* NatChangeSrc port */
+    uint16_t pad2;
+    uint32_t src_ip;   /* NatChangeSrc address, IpAddrToU form */
+} halo_tx_op_t;       /* 16 B */
+
+/* Device pointers; frames rewritten in place; `d_result` (optional) gets one byte per frame.
+ * Ragged layout as halo_rx_parse_batch_device. Asynchronous on `stream`.                */
+HALO_API int halo_tx_fixup_batch_device(uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                        const uint16_t* d_lens, uint32_t n,
+                                        const halo_tx_op_t* d_ops, uint32_t flags,
+                                        uint32_t max_len_hint, uint8_t* d_result,
+                                        halo_stream_t stream);
+
 /* ---- the reference engine's per-frame decision (engine/ethernet_engine.go:13-31,
  *      engine/ipv4_engine.go:18-47, engine/{udp,tcp,icmp}_engine.go) ------------------ */
 typedef enum halo_rx_action {

@@ -1,0 +1,263 @@
+/*
+ * halo_tx_oracle.c — TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline for SURVEY.md §8f
+ * row f2, the forward/transmit rewrite). Linked into oracle/liboracle.so next to the rx
+ * restatement; the product library never links or calls it.
+ *
+ * Followed reference lines (paths under /root/reference), restated one Go function at a time
+ * on (pointer, length) slices; `append` into `sumData` becomes a copy into a heap buffer:
+ *   HandleIpv4PktTtl     protocol/ipv4.go:134-145
+ *   ReCalcIpv4CheckSum   protocol/ipv4.go:148-161
+ *   ReCalcIcmpCheckSum   protocol/ipv4.go:164-174
+ *   ReCalcTcpCheckSum    protocol/ipv4.go:177-200
+ *   ReCalcUdpCheckSum    protocol/ipv4.go:203-226
+ *   NatChangeSrc / Dst   protocol/ipv4.go:249-275, :277-302
+ *   step order           engine/ipv4_engine.go:108-269 (Ipv4RouteForward: DNAT, TTL, SNAT)
+ *   eth_tx SW checksum   cgo/dpdk.c:333-365 with offloads off, calling DPDK 20.11.10 LTS
+ *                        (README.md:103, not vendored, not in this image) rte_ipv4_cksum and
+ *                        rte_ipv4_udptcp_cksum from lib/librte_net/rte_ip.h, restated from the
+ *                        published header: header length from IHL (rte_ipv4_hdr_len), IPv4
+ *                        checksum = ~raw_sum, L4 length = total_length - IHL*4 (0 when
+ *                        total_length < IHL*4), pseudo header {src, dst, 0, proto, l4_len},
+ *                        result 0 -> 0xFFFF for UDP only (RFC 768).
+ *
+ * Pinning: the Go functions cannot run here (no Go toolchain); GetCheckSum is pinned by the
+ * RFC 1071 known answer, the rewrite semantics by this restatement and the independent Python
+ * one in oracle/ref_py.py agreeing on tests/golden/tx_*.  DPDK is absent, so the DPDK fill is
+ * pinned only by RFC 768/1071 arithmetic and by agreeing with ReCalc* on well-formed packets
+ * (tests/test_oracle.py); DESIGN.md §5 says "parity unpinned by reference execution".
+ *
+ * Build-defined behaviour where the reference has none (documented in include/halo_rx.h):
+ *   - DPDK writes/reads past send_len into the mbuf when total_length or IHL point beyond the
+ *     frame; here the affected checksum is left zero and HALO_TX_R_OVERRUN is reported.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/halo_rx.h"
+
+#define ORA_API __attribute__((visibility("default")))
+
+uint16_t ora_get_checksum(const uint8_t* data, size_t len); /* halo_rx_oracle.c (utils.go:11-31) */
+
+static uint16_t be16(const uint8_t* p) { return (uint16_t)(((uint16_t)p[0] << 8) | p[1]); }
+
+/* protocol/ipv4.go:148-161 */
+/* Each helper returns 1 when its length guard returned early (HALO_TX_R_SKIPPED), else 0. */
+static int recalc_ipv4(uint8_t* pkt, size_t len, int csum_enable) {
+    if (len < 20) return 1;
+    pkt[10] = 0x00;
+    pkt[11] = 0x00;
+    if (!csum_enable) return 0;
+    uint16_t sum = ora_get_checksum(pkt, 20);
+    pkt[10] = (uint8_t)(sum >> 8);
+    pkt[11] = (uint8_t)sum;
+    return 0;
+}
+
+/* protocol/ipv4.go:164-174 (CheckSumEnable is not consulted) */
+static int recalc_icmp(uint8_t* pkt, size_t len) {
+    if (len < 24) return 1;
+    pkt[22] = 0x00;
+    pkt[23] = 0x00;
+    uint16_t sum = ora_get_checksum(pkt + 20, len - 20);
+    pkt[22] = (uint8_t)(sum >> 8);
+    pkt[23] = (uint8_t)sum;
+    return 0;
+}
+
+/* protocol/ipv4.go:177-200 (TCP: guard 38, field 36, proto 6) and :203-226 (UDP: guard 28,
+ * field 26, proto 17). totalLen-20 is Go int arithmetic truncated to two bytes. */
+static int recalc_l4(uint8_t* pkt, size_t len, int csum_enable, size_t guard, size_t field, uint8_t proto) {
+    if (len < guard) return 1;
+    pkt[field] = 0x00;
+    pkt[field + 1] = 0x00;
+    if (!csum_enable) return 0;
+    uint8_t* sum_data = (uint8_t*)malloc(12 + len - 20);
+    if (!sum_data) abort();
+    memcpy(sum_data, pkt + 12, 4);
+    memcpy(sum_data + 4, pkt + 16, 4);
+    sum_data[8] = 0x00;
+    sum_data[9] = proto;
+    int total_len = (int)be16(pkt + 2);
+    sum_data[10] = (uint8_t)((total_len - 20) >> 8);
+    sum_data[11] = (uint8_t)(total_len - 20);
+    memcpy(sum_data + 12, pkt + 20, len - 20);
+    uint16_t sum = ora_get_checksum(sum_data, 12 + len - 20);
+    free(sum_data);
+    pkt[field] = (uint8_t)(sum >> 8);
+    pkt[field + 1] = (uint8_t)sum;
+    return 0;
+}
+
+/* protocol/ipv4.go:134-145. Returns the bool result; *skip as the helpers above. */
+static int handle_ipv4_pkt_ttl(uint8_t* pkt, size_t len, int csum_enable, int* skip) {
+    if (len < 9) { *skip |= 1; return 0; }
+    if (pkt[8] <= 1) return 0;
+    pkt[8] -= 0x01;
+    *skip |= recalc_ipv4(pkt, len, csum_enable);
+    return 1;
+}
+
+/* protocol/ipv4.go:249-275 (src) and :277-302 (dst). */
+static int nat_change(uint8_t* pkt, size_t len, uint32_t ip, uint16_t port, int dst, int csum_enable) {
+    if (len < 26) return 1;
+    uint8_t* a = pkt + (dst ? 16 : 12);
+    a[0] = (uint8_t)(ip >> 24);
+    a[1] = (uint8_t)(ip >> 16);
+    a[2] = (uint8_t)(ip >> 8);
+    a[3] = (uint8_t)ip;
+    int skip = recalc_ipv4(pkt, len, csum_enable);
+    switch (pkt[9]) {
+    case 1: /* IPH_PROTO_ICMP: the echo identifier is both NAT keys */
+        pkt[24] = (uint8_t)(port >> 8);
+        pkt[25] = (uint8_t)port;
+        skip |= recalc_icmp(pkt, len);
+        break;
+    case 6:
+        pkt[dst ? 22 : 20] = (uint8_t)(port >> 8);
+        pkt[dst ? 23 : 21] = (uint8_t)port;
+        skip |= recalc_l4(pkt, len, csum_enable, 38, 36, 6);
+        break;
+    case 17:
+        pkt[dst ? 22 : 20] = (uint8_t)(port >> 8);
+        pkt[dst ? 23 : 21] = (uint8_t)port;
+        skip |= recalc_l4(pkt, len, csum_enable, 28, 26, 17);
+        break;
+    }
+    return skip;
+}
+
+/* DPDK 20.11 rte_raw_cksum: 16-bit words in host (little-endian) order, a trailing byte as
+ * the low byte of a word, folded to 16 bits; returned in host order of the LE words. */
+static uint16_t rte_raw_cksum_le(const uint8_t* p, size_t len) {
+    uint32_t sum = 0;
+    size_t i = 0;
+    for (; i + 1 < len; i += 2) sum += (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8);
+    if (len & 1) sum += p[i];
+    while (sum >> 16) sum = (sum & 0xffff) + (sum >> 16);
+    return (uint16_t)sum;
+}
+
+/* cgo/dpdk.c:333-365 with port_conf.txmode.offloads == 0. Returns HALO_TX_R_OVERRUN or 0. */
+static uint8_t dpdk_tx_fill(uint8_t* frame, size_t L) {
+    if (L < 14 || be16(frame + 12) != 0x0800) return 0;  /* ether_type != IPv4: untouched */
+    if (L < 34) return HALO_TX_R_OVERRUN;                 /* the IPv4 header itself is cut */
+    uint8_t* ip = frame + 14;
+    uint8_t rc = 0;
+    ip[10] = ip[11] = 0;                                   /* hdr_checksum = 0 */
+    const size_t ihl4 = (size_t)(ip[0] & 0x0f) * 4;      /* rte_ipv4_hdr_len */
+    if (14 + ihl4 <= L) {
+        uint16_t c = (uint16_t)~rte_raw_cksum_le(ip, ihl4);  /* rte_ipv4_cksum */
+        ip[10] = (uint8_t)c;                                 /* stored as a host-order u16 */
+        ip[11] = (uint8_t)(c >> 8);
+    } else {
+        rc |= HALO_TX_R_OVERRUN;
+    }
+    const uint8_t proto = ip[9];
+    size_t field;
+    if (proto == 17) field = 20 + 6;       /* rte_udp_hdr.dgram_cksum at ipv4_hdr + 20 */
+    else if (proto == 6) field = 20 + 16;  /* rte_tcp_hdr.cksum */
+    else return rc;
+    if (14 + field + 2 > L) return rc | HALO_TX_R_OVERRUN;
+    ip[field] = ip[field + 1] = 0;
+    const uint32_t l3_len = be16(ip + 2);
+    if (l3_len < ihl4) return rc;          /* rte_ipv4_udptcp_cksum returns 0 */
+    const uint32_t l4_len = l3_len - (uint32_t)ihl4;
+    if (34 + (size_t)l4_len > L) return rc | HALO_TX_R_OVERRUN;
+    uint32_t cksum = rte_raw_cksum_le(ip + 20, l4_len);
+    uint8_t psd[12];                       /* rte_ipv4_phdr_cksum(ipv4_hdr, 0) */
+    memcpy(psd, ip + 12, 8);
+    psd[8] = 0;
+    psd[9] = proto;
+    psd[10] = (uint8_t)(l4_len >> 8);
+    psd[11] = (uint8_t)l4_len;
+    cksum += rte_raw_cksum_le(psd, 12);
+    cksum = ((cksum & 0xffff0000u) >> 16) + (cksum & 0xffffu);
+    cksum = (~cksum) & 0xffffu;
+    if (cksum == 0 && proto == 17) cksum = 0xffff;
+    ip[field] = (uint8_t)cksum;
+    ip[field + 1] = (uint8_t)(cksum >> 8);
+    return rc;
+}
+
+/* One frame, the steps of op->steps in the Ipv4RouteForward order. Returns HALO_TX_R_*. */
+ORA_API uint8_t ora_tx_frame(uint8_t* frame, uint32_t L, const halo_tx_op_t* op, uint32_t flags) {
+    const int en = (flags & HALO_RX_CSUM_ENABLE) != 0;
+    const unsigned st = op->steps;
+    uint8_t* pkt = frame + 14;
+    const size_t len = L >= 14 ? L - 14 : 0;  /* pkt = frame[14:], engine/ipv4_engine.go:31-37 */
+    int skip = 0;
+    uint8_t r = 0;
+    if (L < 14) {  /* no IPv4 packet at all: every Go step returns on its guard */
+        if (st & (HALO_TX_NAT_DST | HALO_TX_TTL | HALO_TX_NAT_SRC | HALO_TX_RECALC)) r |= HALO_TX_R_SKIPPED;
+        return r;  /* (and the TTL step, if set, ends the chain) */
+    }
+    if (st & HALO_TX_NAT_DST) skip |= nat_change(pkt, len, op->dst_ip, op->dst_port, 1, en);
+    if (st & HALO_TX_TTL) {
+        int alive = handle_ipv4_pkt_ttl(pkt, len, en, &skip);
+        if (!alive) return skip ? HALO_TX_R_SKIPPED : 0;  /* TTL-exceeded branch, ipv4_engine.go:132-142 */
+        r |= HALO_TX_R_TTL_ALIVE;
+    }
+    if (st & HALO_TX_NAT_SRC) skip |= nat_change(pkt, len, op->src_ip, op->src_port, 0, en);
+    if (st & HALO_TX_RECALC) {
+        skip |= recalc_ipv4(pkt, len, en);
+        if (len >= 10) {
+            switch (pkt[9]) {
+            case 1: skip |= recalc_icmp(pkt, len); break;
+            case 6: skip |= recalc_l4(pkt, len, en, 38, 36, 6); break;
+            case 17: skip |= recalc_l4(pkt, len, en, 28, 26, 17); break;
+            }
+        }
+    }
+    if (skip) r |= HALO_TX_R_SKIPPED;
+    if (st & HALO_TX_DPDK_FILL) r |= dpdk_tx_fill(frame, L);
+    return r;
+}
+
+typedef struct {
+    uint8_t* bytes;
+    const uint32_t* offsets_dw;
+    const uint16_t* lens;
+    const halo_tx_op_t* ops;
+    uint32_t flags;
+    uint8_t* result;
+    uint64_t first, last;
+} tx_job_t;
+
+static void* tx_job(void* arg) {
+    tx_job_t* j = (tx_job_t*)arg;
+    for (uint64_t i = j->first; i < j->last; ++i) {
+        uint8_t r = ora_tx_frame(j->bytes + ((uint64_t)j->offsets_dw[i] << 2), j->lens[i], &j->ops[i], j->flags);
+        if (j->result) j->result[i] = r;
+    }
+    return NULL;
+}
+
+/* In place, ragged dword offsets; threads <= 1 runs on the calling thread. */
+ORA_API int ora_tx_batch(uint8_t* bytes, const uint32_t* offsets_dw, const uint16_t* lens, uint32_t n,
+                         const halo_tx_op_t* ops, uint32_t flags, uint8_t* result, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    tx_job_t* jobs = (tx_job_t*)calloc((size_t)threads, sizeof(tx_job_t));
+    pthread_t* tid = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    if (!jobs || !tid) { free(jobs); free(tid); return -1; }
+    for (int t = 0; t < threads; ++t) {
+        tx_job_t* j = &jobs[t];
+        j->bytes = bytes; j->offsets_dw = offsets_dw; j->lens = lens; j->ops = ops; j->flags = flags;
+        j->result = result;
+        j->first = (uint64_t)n * t / threads;
+        j->last = (uint64_t)n * (t + 1) / threads;
+    }
+    int rc = 0, started = 0;
+    for (int t = 1; t < threads; ++t) {
+        if (pthread_create(&tid[t], NULL, tx_job, &jobs[t]) != 0) { rc = -1; break; }
+        started = t;
+    }
+    if (rc == 0) tx_job(&jobs[0]);
+    for (int t = 1; t <= started; ++t) pthread_join(tid[t], NULL);
+    free(jobs);
+    free(tid);
+    return rc;
+}

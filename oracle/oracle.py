@@ -24,6 +24,8 @@ RESULT_DTYPE = np.dtype([
     ("l4_seq", "<u4"), ("l4_ack", "<u4"),
 ])
 STATUS_COUNT = 14
+TX_OP_DTYPE = np.dtype([("steps", "u1"), ("pad", "u1"), ("dst_port", "<u2"), ("dst_ip", "<u4"),
+                        ("src_port", "<u2"), ("pad2", "<u2"), ("src_ip", "<u4")])
 
 
 class NetIf(ctypes.Structure):
@@ -42,8 +44,8 @@ class NetIf(ctypes.Structure):
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "halo_rx_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("halo_rx_oracle.c", "halo_tx_oracle.c")]
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, srcs)):
         subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
     return LIB_PATH
 
@@ -72,6 +74,10 @@ def lib() -> ctypes.CDLL:
         L.ora_synth_kind.argtypes = [u64, u64, u32, u32, u32, u32, vp, vp]
         L.ora_synth_frame.restype = None
         L.ora_synth_frame.argtypes = [u64, u64, u32, ctypes.c_uint8, ctypes.POINTER(NetIf), vp]
+        L.ora_tx_frame.restype = ctypes.c_uint8
+        L.ora_tx_frame.argtypes = [vp, u32, vp, u32]
+        L.ora_tx_batch.restype = ctypes.c_int
+        L.ora_tx_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -148,3 +154,24 @@ def synth_batch(seed, first_index, lens, kinds, netif, offsets_dw=None, stride=0
         L = int(lens[k])
         buf[start:start + L] = np.frombuffer(synth_frame(seed, first_index + k, L, int(kinds[k]), netif), np.uint8)
     return buf
+
+
+def tx_frame(frame: bytes, op: np.void, flags: int = 1):
+    """Returns (rewritten frame bytes, HALO_TX_R_* byte)."""
+    b = np.frombuffer(bytes(frame) + b"\0", dtype=np.uint8).copy()
+    o = np.array([op], dtype=TX_OP_DTYPE)
+    r = lib().ora_tx_frame(_p(b), len(frame), _p(o), flags)
+    return b[:len(frame)].tobytes(), int(r)
+
+
+def tx_batch(data: np.ndarray, offsets_dw: np.ndarray, lens: np.ndarray, ops: np.ndarray, flags: int = 1,
+             threads: int = 1):
+    """Rewrites a COPY of `data`; returns (new data, result bytes)."""
+    out = np.array(data, dtype=np.uint8, copy=True)
+    n = int(lens.shape[0])
+    res = np.zeros(n, dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets_dw, dtype=np.uint32)
+    lens_c = np.ascontiguousarray(lens, dtype=np.uint16)
+    ops_c = np.ascontiguousarray(ops, dtype=TX_OP_DTYPE)
+    assert lib().ora_tx_batch(_p(out), _p(offs), _p(lens_c), n, _p(ops_c), flags, _p(res), threads) == 0
+    return out, res

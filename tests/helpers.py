@@ -41,3 +41,56 @@ def assert_records_equal(got: np.ndarray, want: np.ndarray, names=None, what="")
             diffs = [f"{f}: got {got[i][f]} want {want[i][f]}" for f in FIELDS if got[i][f] != want[i][f]]
             lines.append(f"  [{i}] {nm}: " + "; ".join(diffs))
         raise AssertionError("\n".join(lines))
+
+
+def tx_golden(root):
+    """The §8f f2 fixtures: (meta, frames blob, expected header bytes [entries, 2, 52])."""
+    import json
+    import os
+
+    g = os.path.join(root, "tests", "golden")
+    with open(os.path.join(g, "tx.json")) as fh:
+        meta = json.load(fh)
+    blob = np.fromfile(os.path.join(g, "tx_frames.bin"), dtype=np.uint8)
+    exp = np.fromfile(os.path.join(g, "tx_expect.bin"), dtype=np.uint8).reshape(len(meta["entries"]), 2,
+                                                                                 meta["hdr_bytes"])
+    return meta, blob, exp
+
+
+def tx_batch_arrays(meta, blob, op_dtype, entries=None):
+    """Lay the fixture entries out as one ragged batch: (data, offsets_dw, lens, ops, originals)."""
+    ents = meta["entries"] if entries is None else [meta["entries"][k] for k in entries]
+    frs = meta["frames"]
+    lens = np.array([frs[e["frame"]]["len"] for e in ents], dtype=np.uint16)
+    sizes = (lens.astype(np.int64) + 3) & ~3
+    offs = np.zeros(len(ents), dtype=np.int64)
+    if len(ents):
+        offs[1:] = np.cumsum(sizes)[:-1]
+    data = np.zeros(max(16, int(sizes.sum()) + 16), dtype=np.uint8)
+    originals = []
+    for k, e in enumerate(ents):
+        f = frs[e["frame"]]
+        src = blob[f["offset"]:f["offset"] + f["len"]]
+        data[offs[k]:offs[k] + f["len"]] = src
+        originals.append(src)
+    ops = np.zeros(len(ents), dtype=op_dtype)
+    for k, e in enumerate(ents):
+        ops[k]["steps"], ops[k]["dst_ip"], ops[k]["dst_port"], ops[k]["src_ip"], ops[k]["src_port"] = e["op"]
+    return data, (offs // 4).astype(np.uint32), lens, ops, originals
+
+
+def assert_tx_equal(data, offsets_dw, lens, results, meta, exp, flag, entries=None, what=""):
+    """Rewritten frames == fixture (header bytes) and untouched past byte 51; result bytes equal."""
+    ents = meta["entries"] if entries is None else [meta["entries"][k] for k in entries]
+    idx = range(len(meta["entries"])) if entries is None else entries
+    hb = meta["hdr_bytes"]
+    bad = []
+    for k, (ek, e) in enumerate(zip(idx, ents)):
+        L = int(lens[k])
+        o = int(offsets_dw[k]) * 4
+        got = data[o:o + min(L, hb)]
+        want = exp[ek, flag, :min(L, hb)]
+        if not np.array_equal(got, want) or int(results[k]) != e["result"][str(flag)]:
+            bad.append((k, meta["frames"][e["frame"]]["name"], e["op"][0], got.tobytes().hex(),
+                        want.tobytes().hex(), int(results[k]), e["result"][str(flag)]))
+    assert not bad, f"{what}: {len(bad)} of {len(ents)} entries differ; first: {bad[:3]}"

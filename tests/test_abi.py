@@ -172,3 +172,35 @@ def test_dispatch_compact_matches_full(golden, oracle_lib):
             assert _lib.lib.halo_rx_dispatch(recs.ctypes.data, len(recs), hn, full.ctypes.data, None) == 0
             assert _lib.lib.halo_rx_dispatch_compact(c16.ctypes.data, len(recs), hn, comp.ctypes.data, None) == 0
             assert np.array_equal(full, comp)
+
+
+def test_tx_op_struct_layout_and_validation(tmp_path):
+    """halo_tx_op_t matches TX_OP_DTYPE; halo_tx_fixup_batch_device validates before touching
+    a device and has no CPU fallback."""
+    import torch
+
+    from halo_amd import _lib
+    from halo_amd._lib import TX_OP_DTYPE
+
+    src = tmp_path / "txl.c"
+    fields = [f for f in TX_OP_DTYPE.names]
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "halo_rx.h"\nint main(void){\n'
+                   + "".join(f'printf("%zu\\n", offsetof(halo_tx_op_t, {f}));\n' for f in fields)
+                   + 'printf("%zu\\n", sizeof(halo_tx_op_t));\nreturn 0;}\n')
+    exe = tmp_path / "txl"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals == [TX_OP_DTYPE.fields[f][1] for f in fields] + [16]
+    L = _lib.lib
+    buf = np.zeros(128, np.uint8)
+    ops = np.zeros(1, TX_OP_DTYPE)
+    offs = np.zeros(1, np.uint32)
+    lens = np.full(1, 64, np.uint16)
+    assert L.halo_tx_fixup_batch_device(None, None, None, 0, None, 1, 0, None, None) == 0
+    assert L.halo_tx_fixup_batch_device(buf.ctypes.data, None, None, 1, ops.ctypes.data, 1, 0, None, None) == -1
+    assert L.halo_tx_fixup_batch_device(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, 1, ops.ctypes.data,
+                                        0x4, 0, None, None) == -1  # only CSUM_ENABLE is defined here
+    if not torch.cuda.is_available():
+        rc = L.halo_tx_fixup_batch_device(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, 1,
+                                          ops.ctypes.data, 1, 0, None, None)
+        assert rc == _lib.HALO_E_NODEV

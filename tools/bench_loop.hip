@@ -45,3 +45,34 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_steps(
     (void)hipEventDestroy(e1);
     return rc;
 }
+
+// The same loop for the forward / transmit rewrite (halo_tx_fixup_batch_device, §8f row f2).
+extern "C" __attribute__((visibility("default"))) int halo_bench_tx_steps(
+    int nbatch, uint8_t* const* bytes, const uint32_t* const* offsets_dw, const uint16_t* const* lens, uint32_t n,
+    const halo_tx_op_t* ops, uint32_t flags, uint32_t hint, uint8_t* result, int warmup, int steps, void* stream,
+    float* region_ms, double* wall_s) {
+    if (nbatch <= 0 || steps <= 0 || !region_ms || !wall_s) return HALO_E_INVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto launch = [&](int k) -> int {
+        const int b = k % nbatch;
+        return halo_tx_fixup_batch_device(bytes[b], offsets_dw[b], lens[b], n, ops, flags, hint, result, stream);
+    };
+    int rc = HALO_OK;
+    for (int k = 0; k < warmup && rc == HALO_OK; ++k) rc = launch(k);
+    if (rc) return rc;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return HALO_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return HALO_E_HIP;
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)hipEventRecord(e0, s);
+    for (int k = 0; k < steps && rc == HALO_OK; ++k) rc = launch(k);
+    (void)hipEventRecord(e1, s);
+    if (hipStreamSynchronize(s) != hipSuccess && rc == HALO_OK) rc = HALO_E_HIP;
+    const auto t1 = std::chrono::steady_clock::now();
+    *wall_s = std::chrono::duration<double>(t1 - t0).count();
+    *region_ms = -1.0f;
+    (void)hipEventElapsedTime(region_ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}

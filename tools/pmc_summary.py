@@ -4,7 +4,7 @@ per-workload numbers and write profiles/pmc_summary.json (read by bench.py for `
 
     python tools/pmc_summary.py gpurun_out/<tag> [--out profiles/pmc_summary.json]
 
-rx_* dispatches are attributed to tools/prof_kernels.py's WORKLOADS in launch order.
+rx_* / tx_fixup_* dispatches are attributed to tools/prof_kernels.py's WORKLOADS in launch order.
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from separate
 --pmc passes; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced streaming read,
 so read bytes = 2 x FETCH_SIZE x 1024 (the calibration column checks that against the bytes
@@ -41,7 +41,12 @@ def alg_bytes():
         lay = synth.layout(n, **kw, ragged=not slen)
         frames = int(lay["lens"].astype("int64").sum())
         meta = 0 if slen else 6 * n
-        out[name] = (frames + meta, 32 * n)
+        if name.startswith("tx_"):  # + 16 B op in; 1 B result + 20 B of rewritten header out
+            import bench
+
+            out[name] = (frames + meta + 16 * n, (1 + bench.TX_WRITE_BYTES) * n)
+        else:
+            out[name] = (frames + meta, 32 * n)
     return out
 
 
@@ -56,7 +61,7 @@ def main():
         order += [name] * launches
 
     def attribute(rows, key="Dispatch_Id"):
-        disp = sorted({int(r[key]) for r in rows if "rx_" in r["Kernel_Name"]})
+        disp = sorted({int(r[key]) for r in rows if "rx_" in r["Kernel_Name"] or "tx_fixup" in r["Kernel_Name"]})
         return {d: order[k] for k, d in enumerate(disp) if k < len(order)}
 
     res = defaultdict(lambda: defaultdict(list))

@@ -21,6 +21,8 @@ WORKLOADS = [
     ("1500B_udp_1M", dict(length=1500), 1 << 20, 2, 10, 0, 1, 1500),
     ("config3_imix_16M", dict(size_mode=1, proto_mode=3), 16 << 20, 1, 5, 0, 1, 1500),
     ("config5_jumbo_9000B_tcp_4M_ext", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, 3, 9000, 3, 0),
+    # forward / transmit rewrite (§8f row f2): bench.TX_BENCH_STEPS on the config 2 frames
+    ("tx_config2", dict(length=64), 1 << 20, 8, 20, 0, 1, 64),
 ]
 
 
@@ -40,11 +42,20 @@ def main():
             continue
         bs = bench.make_batches(dev, netif, n=n, rotate=rot, rank=0, **kw)
         out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        ops = None
+        if name.startswith("tx_"):
+            import numpy as np
+
+            ops = torch.from_numpy(bench.tx_ops_for(n).view(np.uint8)).to(dev)
         torch.cuda.synchronize()
         stream = torch.cuda.current_stream().cuda_stream
         for i in range(launches):
             fr = bs[i % len(bs)]
-            if slen:
+            if ops is not None:
+                rc = _lib.lib.halo_tx_fixup_batch_device(fr["bytes"].data_ptr(), fr["offsets_dw"].data_ptr(),
+                                                         fr["lens"].data_ptr(), n, ops.data_ptr(), flags, hint,
+                                                         out.data_ptr(), stream)
+            elif slen:
                 rc = _lib.lib.halo_rx_parse_strided_device(fr["bytes"].data_ptr(), slen, None, slen, n, flags, netif,
                                                            out.data_ptr(), None, stream)
             else:
