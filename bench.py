@@ -130,6 +130,12 @@ def bench_lib():
         L.halo_bench_tx_steps.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_uint32,
                                           ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp,
                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
+        i32, u32 = ctypes.c_int, ctypes.c_uint32
+        tail = [i32, i32, vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
+        L.halo_bench_flow_steps.restype = ctypes.c_int
+        L.halo_bench_flow_steps.argtypes = [i32, vp, u32, u32, u32, vp, u32, vp] + tail
+        L.halo_bench_xxh3_steps.restype = ctypes.c_int
+        L.halo_bench_xxh3_steps.argtypes = [i32, vp, vp, vp, u32, vp] + tail
         _BENCH_LIB = L
     return _BENCH_LIB
 
@@ -208,6 +214,83 @@ def time_tx_steps(batches, ops_dev, res_dev, *, flags, hint, steps, warmup, d: D
     torch.cuda.synchronize()
     d.barrier()
     return d.max(wall.value), region.value / steps
+
+
+def time_native(fn, *args, steps, warmup, d: Dist):
+    """One of the row-f3 native loops (halo_bench_flow_steps / halo_bench_xxh3_steps)."""
+    import ctypes
+
+    import torch
+
+    from halo_amd import _lib
+
+    region, wall = ctypes.c_float(), ctypes.c_double()
+    torch.cuda.synchronize()
+    d.barrier()
+    rc = fn(*args, warmup, steps, torch.cuda.current_stream().cuda_stream, ctypes.byref(region), ctypes.byref(wall))
+    _lib.check(fn.__name__, rc)
+    torch.cuda.synchronize()
+    d.barrier()
+    return d.max(wall.value), region.value / steps
+
+
+def flow_hash_secondary(batches, out_records, netif, steps, warmup, d: Dist):
+    """§8f f3 on the headline frames: parse each rotating batch once, then hash every record's NAT
+    flow key (NatWanFlowHash, symmetric NAT) with the hashmap bucket for a 2^20-entry table."""
+    import ctypes
+
+    import torch
+
+    from halo_amd import protocol
+
+    n = batches[0]["layout"]["n"]
+    recs = []
+    for b in batches:
+        o = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=out_records.device)
+        protocol.parse_frames_batch(b["bytes"], b["offsets_dw"], b["lens"], netif=netif, max_len_hint=64, out=o)
+        recs.append(o)
+    h = torch.empty(n, dtype=torch.int64, device=out_records.device)
+    bk = torch.empty(n, dtype=torch.int32, device=out_records.device)
+    arr = (ctypes.c_void_p * len(recs))(*[r.data_ptr() for r in recs])
+    w, k = time_native(bench_lib().halo_bench_flow_steps, len(recs), arr, n, 1, 0, h.data_ptr(), 1 << 20,
+                       bk.data_ptr(), steps=steps, warmup=warmup, d=d)
+    alg = n * (20 + 8 + 4)  # record bytes 0..19 in, 8 B hash + 4 B bucket out
+    res = {"mpps": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 5),
+           "roofline": roofline(alg, k, load_traffic("flow_hash_config2")), "alg_bytes_per_launch": alg,
+           "what": "NatWanFlowHash (13 B key) XXH3-64 + hash % 2^20 per record"}
+    del recs
+    return res
+
+
+def xxh3_secondary(dev, steps, warmup, d: Dist):
+    """§8f f3, GetHashCodeXXH3 over KCP-segment-sized strings (24..1400 B, unaligned offsets)."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    n = 1 << 20
+    rng = np.random.default_rng(0x4B4350)
+    bs = []
+    for _ in range(2):
+        lens = rng.integers(24, 1401, n).astype(np.uint32)
+        offs = np.zeros(n, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 1)
+        total = int(offs[-1]) + int(lens[-1]) + 8
+        data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev)
+        bs.append((data, torch.from_numpy(offs.view(np.int64)).to(dev), torch.from_numpy(lens.view(np.int32)).to(dev),
+                   int(lens.astype(np.int64).sum())))
+    h = torch.empty(n, dtype=torch.int64, device=dev)
+    arr = lambda xs: (ctypes.c_void_p * len(xs))(*xs)  # noqa: E731
+    w, k = time_native(bench_lib().halo_bench_xxh3_steps, len(bs), arr([b[0].data_ptr() for b in bs]),
+                       arr([b[1].data_ptr() for b in bs]), arr([b[2].data_ptr() for b in bs]), n, h.data_ptr(),
+                       steps=steps, warmup=warmup, d=d)
+    alg = bs[0][3] + n * (8 + 4 + 8)
+    res = {"strings": n, "mstrings_per_s": round(n * steps / w / 1e6, 1),
+           "gbytes_per_s": round(bs[0][3] * steps / w / 1e9, 1), "kernel_ms": round(k, 4),
+           "roofline": roofline(alg, k, load_traffic("xxh3_kcp_1M")), "alg_bytes_per_launch": alg}
+    del bs
+    return res
 
 
 def roofline(alg_bytes_per_launch, kernel_ms, traffic=None):
@@ -377,7 +460,11 @@ def main():
             "mpps": round(n * args.steps / wt / 1e6, 1), "kernel_ms": round(kt, 5),
             "roofline": roofline(algt, kt, load_traffic("tx_config2")), "alg_bytes_per_launch": algt,
             "steps": "NatChangeDst + NatChangeSrc + eth_tx DPDK fill, per-frame addresses/ports"}
-        del batches, ops_d, res_d
+        del ops_d, res_d
+        sec["flow_hash_config2_nat_wan"] = flow_hash_secondary(batches, out, netif, args.steps, args.warmup, d)
+        del batches
+        torch.cuda.empty_cache()
+        sec["xxh3_kcp_segments_1M"] = xxh3_secondary(dev, max(5, args.steps // 10), 2, d)
         torch.cuda.empty_cache()
         for name, kw, hint, strided_len, flags in [
             ("1500B_udp_1M", dict(length=1500), 1500, 0, 1),

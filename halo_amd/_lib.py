@@ -83,6 +83,8 @@ TX_OP_DTYPE = np.dtype([("steps", "u1"), ("pad", "u1"), ("dst_port", "<u2"), ("d
 assert TX_OP_DTYPE.itemsize == 16
 TX_NAT_DST, TX_TTL, TX_NAT_SRC, TX_RECALC, TX_DPDK_FILL = 0x01, 0x02, 0x04, 0x08, 0x10
 TX_R_TTL_ALIVE, TX_R_SKIPPED, TX_R_OVERRUN = 0x01, 0x02, 0x04
+FLOW_NAT_LAN, FLOW_NAT_WAN = 0, 1        # HALO_FLOW_*
+NAT_SYMMETRIC, NAT_FULL_CONE = 0, 1      # HALO_NAT_* (engine.NatTypeSymmetric / NatTypeFullCone)
 
 
 class NetIf(ctypes.Structure):
@@ -132,6 +134,9 @@ _PROTOS = {
     "halo_rx_dispatch_compact": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_tx_fixup_batch_device": (ctypes.c_int, [
         _u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
+    "halo_xxh3_64_batch_device": (ctypes.c_int, [_u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
+    "halo_flow_hash_device": (ctypes.c_int, [
+        _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_synth_layout": (ctypes.c_int, [
         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint64)]),

@@ -1,0 +1,308 @@
+// flow_hash.hip — SURVEY.md §8f row f3 on gfx950: XXH3-64 (hashcode/xxh3.go, the reference's
+// trimmed port of github.com/zeebo/xxh3 v1.1.0: default secret, seed 0) over batches of byte
+// strings, and the NAT flow-table keys of the forward path (NatFlowHash / NatWanFlowHash,
+// engine/ipv4_engine.go:451-479) hashed straight from parsed rx records.
+//
+// Shape. Short strings (<= 240 B: hashSmall / hashMedium / hashLarge, xxh3.go:59-129) are one
+// lane each. Long strings (hashLong, :132-209) are the 8-accumulator stripe loop, which maps
+// onto 8 lanes: lane j of a group owns accumulator j, reads bytes [8j, 8j+8) of each 64-byte
+// stripe (the group's load is one coalesced 64-byte access) and gets input word j^1 from its
+// neighbour with a DPP quad_perm swap; the merge folds lane pairs the same way. A wave first
+// hashes its short strings lane-per-string, then takes its long strings eight at a time (one
+// per 8-lane group), so ragged batches keep every lane busy.
+//
+// Data are read as aligned dwords merged with v_alignbyte: any byte offset works, and no read
+// touches a dword that holds none of the string's bytes (so never a page the string is not on).
+#include <hip/hip_runtime.h>
+
+#include "device_util.h"
+#include "halo_common.h"
+
+namespace halo {
+namespace {
+
+// hashcode/xxh3.go:27-40 (192 bytes) as little-endian dwords, + 2 zero dwords for the
+// unaligned-read overhang
+__constant__ uint32_t kSecretDw[50] = {
+    0x396cfeb8u, 0xbe4ba423u, 0x2c81017cu, 0x1cad21f7u, 0xe96dd4deu, 0xdb979083u, 0xa4a44072u, 0x1f67b3b7u,
+    0x4ee679cbu, 0x78e5c0ccu, 0x7dd05a82u, 0x2172ffccu, 0x744608b8u, 0x8e2443f7u, 0xe69035e0u, 0x4c263a81u,
+    0xbb52283cu, 0xcb00c391u, 0x8b65d088u, 0xa32e531bu, 0x97486471u, 0x4ef90da2u, 0x46ef1938u, 0xd8acdea9u,
+    0x3f76faa8u, 0x3f349ce3u, 0xc7bbdcf9u, 0x1d4f0bc7u, 0x4be0518au, 0x3159b4cdu, 0xc97e9fc8u, 0x647378d9u,
+    0x83acc5eau, 0xc3ebd334u, 0xffa081c5u, 0xeb6313fau, 0x51dd0d17u, 0x49daf0b7u, 0x265516d3u, 0x9e68d429u,
+    0x58be162bu, 0xfca1477du, 0xd1b8f88fu, 0xce31d07au, 0x8f3acb45u, 0x28041695u, 0xcafbd7afu, 0x7e404bbbu,
+    0u, 0u};
+
+constexpr uint64_t P32_1 = 2654435761ull, P32_2 = 2246822519ull, P32_3 = 3266489917ull;
+constexpr uint64_t P64_1 = 11400714785074694791ull, P64_2 = 14029467366897019727ull,
+                   P64_3 = 1609587929392839161ull, P64_4 = 9650029242287828579ull,
+                   P64_5 = 2870177450012600261ull;
+
+__device__ __forceinline__ uint64_t join64(uint32_t lo, uint32_t hi) { return (uint64_t)hi << 32 | lo; }
+
+// secret64(off) (xxh3.go:282-284) for any byte offset
+__device__ __forceinline__ uint64_t sec64(uint32_t off) {
+    const uint32_t a = off >> 2, s = off & 3u;
+    const uint32_t w0 = kSecretDw[a], w1 = kSecretDw[a + 1], w2 = kSecretDw[a + 2];
+    return join64(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s));
+}
+__device__ __forceinline__ uint32_t sec32(uint32_t off) { return (uint32_t)sec64(off); }
+
+typedef const __attribute__((address_space(1))) uint32_t gdw;
+
+// little-endian reads of string bytes at any address (xxh3.go:262-279)
+__device__ __forceinline__ uint64_t ld64(const uint8_t* p) {
+    const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+    gdw* q = (gdw*)(u & ~(uintptr_t)3);
+    const uint32_t s = (uint32_t)(u & 3u);
+    const uint32_t w0 = q[0], w1 = q[1];
+    const uint32_t w2 = s ? q[2] : 0u;
+    return join64(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s));
+}
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+    const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+    gdw* q = (gdw*)(u & ~(uintptr_t)3);
+    const uint32_t s = (uint32_t)(u & 3u);
+    const uint32_t w0 = q[0];
+    const uint32_t w1 = s ? q[1] : 0u;
+    return __builtin_amdgcn_alignbyte(w1, w0, s);
+}
+__device__ __forceinline__ uint32_t ld8(const uint8_t* p) {
+    return *(const __attribute__((address_space(1))) uint8_t*)p;
+}
+
+__device__ __forceinline__ uint64_t mul_fold64(uint64_t a, uint64_t b) { return (a * b) ^ __umul64hi(a, b); }
+__device__ __forceinline__ uint64_t avalanche_small(uint64_t v) {  // xxh3.go:228-235
+    v ^= v >> 33; v *= P64_2; v ^= v >> 29; v *= P64_3; v ^= v >> 32;
+    return v;
+}
+__device__ __forceinline__ uint64_t avalanche(uint64_t v) {  // xxh3.go:238-243
+    v ^= v >> 37; v *= 0x165667919e3779f9ull; v ^= v >> 32;
+    return v;
+}
+__device__ __forceinline__ uint64_t rotl64(uint64_t v, int r) { return (v << r) | (v >> (64 - r)); }
+__device__ __forceinline__ uint64_t rrmxmx(uint64_t v, uint64_t len) {  // xxh3.go:246-253
+    v ^= rotl64(v, 49) ^ rotl64(v, 24);
+    v *= 0x9fb21c651e98df25ull;
+    v ^= (v >> 35) + len;
+    v *= 0x9fb21c651e98df25ull;
+    v ^= v >> 28;
+    return v;
+}
+__device__ __forceinline__ uint64_t mix16(const uint8_t* d, uint32_t doff, uint32_t soff) {  // :221-225
+    return mul_fold64(ld64(d + doff) ^ sec64(soff), ld64(d + doff + 8) ^ sec64(soff + 8));
+}
+
+// hashSmall for 9..16 bytes given the two overlapping 8-byte words (xxh3.go:62-66)
+__device__ __forceinline__ uint64_t hash_9to16(uint64_t w_lo, uint64_t w_hi, uint32_t len) {
+    const uint64_t lo = w_lo ^ (sec64(24) ^ sec64(32));
+    const uint64_t hi = w_hi ^ (sec64(40) ^ sec64(48));
+    return avalanche((uint64_t)len + __builtin_bswap64(lo) + hi + mul_fold64(lo, hi));
+}
+
+// xxh3HashCode for len <= 240 (xxh3.go:43-129), one lane
+__device__ uint64_t hash_short(const uint8_t* d, uint32_t len) {
+    if (len <= 16) {
+        if (len > 8) return hash_9to16(ld64(d), ld64(d + len - 8), len);
+        if (len > 3) {
+            const uint64_t in = (uint64_t)ld32(d + len - 4) + ((uint64_t)ld32(d) << 32);
+            return rrmxmx(in ^ (sec64(8) ^ sec64(16)), len);
+        }
+        uint64_t acc;
+        if (len == 3) acc = ((uint64_t)(ld8(d) | ld8(d + 1) << 8) << 16) + ld8(d + 2) + (3u << 8);
+        else if (len == 2) acc = ((uint64_t)(ld8(d) | ld8(d + 1) << 8) * ((1u << 24) + 1) >> 8) + (2u << 8);
+        else if (len == 1) acc = (uint64_t)ld8(d) * ((1u << 24) + (1u << 16) + 1) + (1u << 8);
+        else return 0x2d06800538d394c2ull;
+        acc ^= (uint64_t)(sec32(0) ^ sec32(4));
+        return avalanche_small(acc);
+    }
+    uint64_t acc = (uint64_t)len * P64_1;
+    if (len <= 128) {  // hashMedium (xxh3.go:94-113)
+        if (len > 32) {
+            if (len > 64) {
+                if (len > 96) {
+                    acc += mix16(d, 48, 96);
+                    acc += mix16(d, len - 64, 112);
+                }
+                acc += mix16(d, 32, 64);
+                acc += mix16(d, len - 48, 80);
+            }
+            acc += mix16(d, 16, 32);
+            acc += mix16(d, len - 32, 48);
+        }
+        acc += mix16(d, 0, 0);
+        acc += mix16(d, len - 16, 16);
+        return avalanche(acc);
+    }
+    // hashLarge (xxh3.go:116-129)
+#pragma unroll
+    for (uint32_t off = 0; off < 128; off += 16) acc += mix16(d, off, off);
+    acc = avalanche(acc);
+    for (uint32_t off = 128, top = len & ~15u; off < top; off += 16) acc += mix16(d, off, off - 125);
+    acc += mix16(d, len - 16, 119);
+    return avalanche(acc);
+}
+
+// a 64-bit DPP move (both halves with the same control)
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+    return join64(lo, hi);
+}
+// 64-bit value of lane (lane ^ 1) within each quad (DPP quad_perm 1,0,3,2)
+__device__ __forceinline__ uint64_t swap_pair(uint64_t v) { return dpp64<0xB1>(v); }
+
+// accumulateStripe (xxh3.go:181-209) for accumulator j on lane j of the group
+__device__ __forceinline__ void stripe8(uint64_t& acc, const uint8_t* stripe, uint32_t sec_off, uint32_t j) {
+    const uint64_t in = ld64(stripe + 8 * j);
+    const uint64_t k = in ^ sec64(sec_off + 8 * j);
+    acc += swap_pair(in) + (uint64_t)(uint32_t)k * (k >> 32);
+}
+
+// hashLong (xxh3.go:132-178) on a group of 8 lanes; lane j = accumulator j. Result in every lane.
+__device__ uint64_t hash_long8(const uint8_t* d, uint32_t len, uint32_t j) {
+    constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+    uint64_t acc = kInit[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) acc = j == (uint32_t)q ? kInit[q] : acc;
+    const uint8_t* p = d;
+    uint32_t remaining = len;
+    while (remaining > 1024) {
+        for (uint32_t st = 0; st < 16; ++st) {
+            stripe8(acc, p, 8 * st, j);
+            p += 64;
+        }
+        remaining -= 1024;
+        acc ^= acc >> 47;  // scramble (xxh3.go:212-218)
+        acc ^= sec64(128 + 8 * j);
+        acc *= P32_1;
+    }
+    const uint32_t stripes = (remaining - 1) / 64;
+    for (uint32_t st = 0; st < stripes; ++st) {
+        stripe8(acc, p, 8 * st, j);
+        p += 64;
+    }
+    stripe8(acc, d + len - 64, 121, j);  // the last (overlapping) stripe, secret offset 121
+    // merge (xxh3.go:139-145): pairs (2i, 2i+1) with secret 11 + 16i, then sum over the pairs
+    const uint64_t mine = acc ^ sec64(11 + 8 * j);
+    const uint64_t other = swap_pair(mine);
+    uint64_t m = (j & 1u) ? 0ull : mul_fold64(mine, other);
+    // sum lanes 0, 2, 4, 6 of the group (odd lanes hold 0): butterfly over the 8 lanes
+    m += dpp64<0xB1>(m);   // quad_perm 1,0,3,2
+    m += dpp64<0x4E>(m);   // quad_perm 2,3,0,1
+    m += dpp64<0x141>(m);  // row_half_mirror: lane i <-> 7-i within each 8
+    return avalanche((uint64_t)len * P64_1 + m);
+}
+
+struct XxhParams {
+    const uint8_t* bytes;
+    const uint64_t* offsets;
+    const uint32_t* lens;
+    uint32_t n;
+    uint64_t* out;
+};
+
+__global__ void __launch_bounds__(256) xxh3_batch_kernel(const XxhParams p) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t base = wave * 64; base < p.n; base += nwaves * 64) {
+        const uint32_t i = base + lane;
+        const bool have = i < p.n;
+        const uint32_t len = have ? p.lens[i] : 0u;
+        const uint64_t off = have ? p.offsets[i] : 0ull;
+        if (have && len <= 240) p.out[i] = hash_short(p.bytes + off, len);
+        // long strings: eight at a time, one per 8-lane group
+        uint64_t pend = __ballot(have && len > 240);
+        const uint32_t g = lane >> 3, j = lane & 7u;
+        while (pend) {
+            uint32_t owner = 64;  // lane whose string group g takes this round
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) {
+                const uint32_t b = pend ? (uint32_t)__builtin_ctzll(pend) : 64u;
+                owner = q == g ? b : owner;
+                pend &= pend ? pend - 1 : 0ull;
+            }
+            const uint32_t src = owner < 64 ? owner : 0u;
+            const uint32_t o_lo = (uint32_t)__shfl((int)(uint32_t)off, (int)src, 64);
+            const uint32_t o_hi = (uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)src, 64);
+            const uint32_t o_len = (uint32_t)__shfl((int)len, (int)src, 64);
+            if (owner < 64) {  // uniform per group
+                const uint64_t h = hash_long8(p.bytes + join64(o_lo, o_hi), o_len, j);
+                if (j == 0) p.out[base + owner] = h;
+            }
+        }
+    }
+}
+
+// ---- NAT flow keys from parsed records ------------------------------------------------------
+struct FlowParams {
+    const halo_rx_result_t* recs;
+    uint32_t n, kind, nat_type, buckets;
+    uint64_t* hash;
+    uint32_t* bucket;
+};
+
+__global__ void __launch_bounds__(256) flow_hash_kernel(const FlowParams p) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += stride) {
+        // record bytes 0..15 (status..dst_ip) and 16..19 (sport, dport)
+        const uint4 a = reinterpret_cast<const uint4*>(p.recs)[2ull * i];
+        const uint32_t ports = reinterpret_cast<const uint32_t*>(p.recs)[8ull * i + 4];
+        const uint32_t proto = a.y & 0xFFu, src = a.z, dst = a.w;
+        const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16;
+        const bool wan = p.kind == HALO_FLOW_NAT_WAN;
+        // NatGetFlowByWan(src, sport, dst, dport) / NatGetFlowByHash(dst, dport, src, sport)
+        uint32_t rip = wan ? src : dst, rport = wan ? sport : dport;
+        const uint32_t lip = wan ? dst : src, lport = wan ? dport : sport;
+        if (p.nat_type != HALO_NAT_SYMMETRIC) { rip = 0; rport = 0; }  // :528-534
+        if (proto == kIpIcmp) rport = 0;                                  // :535-537
+        // 13-byte key (engine/ipv4_engine.go:452-458): rip | rport | lip | lport | proto, LE
+        const uint64_t w_lo = (uint64_t)rip | (uint64_t)rport << 32 | (uint64_t)(lip & 0xFFFFu) << 48;
+        const uint64_t w_hi = (uint64_t)(rport >> 8) | (uint64_t)lip << 8 | (uint64_t)lport << 40 |
+                              (uint64_t)proto << 56;  // key bytes 5..12
+        const uint64_t h = hash_9to16(w_lo, w_hi, 13);
+        p.hash[i] = h;
+        if (p.bucket) p.bucket[i] = (uint32_t)(h % p.buckets);  // hashmap/hashmap.go:64
+    }
+}
+
+uint32_t blocks_for(uint64_t threads) {
+    const uint64_t b = (threads + 255) / 256;
+    const uint64_t kMax = 256ull * 8 * 8;
+    return (uint32_t)(b > kMax ? kMax : (b ? b : 1));
+}
+
+}  // namespace
+}  // namespace halo
+
+extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const uint64_t* d_offsets,
+                                                  const uint32_t* d_lens, uint32_t n, uint64_t* d_hash,
+                                                  halo_stream_t stream) {
+    if (n == 0) return HALO_OK;
+    if (!d_offsets || !d_lens || !d_hash) return HALO_E_INVAL;
+    if (reinterpret_cast<uintptr_t>(d_hash) & 7u) return HALO_E_INVAL;
+    int rc = halo::check_device();
+    if (rc) return rc;
+    halo::XxhParams p{d_bytes, d_offsets, d_lens, n, d_hash};
+    hipLaunchKernelGGL(halo::xxh3_batch_kernel, dim3(halo::blocks_for(n)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+
+extern "C" HALO_API int halo_flow_hash_device(const halo_rx_result_t* d_records, uint32_t n, uint32_t kind,
+                                              uint32_t nat_type, uint64_t* d_hash, uint32_t bucket_count,
+                                              uint32_t* d_bucket, halo_stream_t stream) {
+    if (kind > HALO_FLOW_NAT_WAN) return HALO_E_INVAL;
+    if (d_bucket && bucket_count == 0) return HALO_E_INVAL;
+    if (n == 0) return HALO_OK;
+    if (!d_records || !d_hash) return HALO_E_INVAL;
+    if ((reinterpret_cast<uintptr_t>(d_records) & 15u) || (reinterpret_cast<uintptr_t>(d_hash) & 7u))
+        return HALO_E_INVAL;
+    int rc = halo::check_device();
+    if (rc) return rc;
+    halo::FlowParams p{d_records, n, kind, nat_type, bucket_count, d_hash, d_bucket};
+    hipLaunchKernelGGL(halo::flow_hash_kernel, dim3(halo::blocks_for(n)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}

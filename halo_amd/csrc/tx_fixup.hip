@@ -84,11 +84,11 @@ __device__ __forceinline__ void acc_tail(const uint32_t (&w)[4], uint32_t d0, ui
 }
 
 struct TxPlan {
-    uint32_t ip_hi;      // IPv4 header checksum over [14, ip_hi); 0: no sum
-    uint32_t l4_hi;      // L4 checksum over [34, l4_hi) + l4_extra; 0: no sum
-    uint32_t l4_extra;   // pseudo header, LE domain
-    uint32_t l4_field;   // frame offset of the L4 checksum field being summed (0: none)
-    bool udp_zero_ffff;  // DPDK: a zero UDP checksum is sent as 0xFFFF
+    uint32_t ip_hi;                        // IPv4 header checksum over [14, ip_hi); 0: none
+    uint32_t go_hi, go_extra, go_field;    // Go ReCalc L4 checksum over [34, go_hi) + pseudo; 0: none
+    uint32_t dp_hi, dp_extra, dp_field;    // DPDK L4 checksum over [34, dp_hi) + pseudo; 0: none
+    uint32_t dp_zero;                      // L4 field DPDK zeroes (before its sum, after the IPv4 sum)
+    bool udp_zero_ffff;                    // DPDK: a zero UDP checksum is sent as 0xFFFF
 };
 
 // Apply the steps to the header copy; returns the checksum plan. All lanes of a group run this
@@ -96,7 +96,7 @@ struct TxPlan {
 __device__ __forceinline__ TxPlan apply_steps(uint32_t (&m)[kHdrDw], uint32_t& dirty, uint32_t L, uint32_t steps,
                                               uint32_t dst_ip, uint32_t dst_port, uint32_t src_ip,
                                               uint32_t src_port, bool en, uint32_t& res) {
-    TxPlan pl{0, 0, 0, 0, false};
+    TxPlan pl{0, 0, 0, 0, 0, 0, 0, 0, false};
     bool skip = false;
     if (L < 14) {  // no IPv4 packet: every Go step returns on its length guard
         res = (steps & kGoSteps) ? HALO_TX_R_SKIPPED : 0u;
@@ -175,21 +175,23 @@ __device__ __forceinline__ TxPlan apply_steps(uint32_t (&m)[kHdrDw], uint32_t& d
     const uint32_t sum_addrs = (m[6] >> 16) + hsum(m[7]) + (m[8] & 0xFFFFu);  // pseudo src+dst
     if (l4_go == kIpIcmp) {
         SET_LE16(36, 0);
-        pl.l4_hi = L;
-        pl.l4_field = 36;
+        pl.go_hi = L;
+        pl.go_field = 36;
     } else if (l4_go) {
         const uint32_t f = l4_go == kIpTcp ? 50u : 40u;
         if (f == 50u) SET_LE16(50, 0);
         else SET_LE16(40, 0);
         if (en) {
             const uint32_t total_len = bswap16(m[4] & 0xFFFFu);  // frame bytes 16..17
-            pl.l4_hi = L;
-            pl.l4_field = f;
-            pl.l4_extra = sum_addrs + (l4_go << 8) + bswap16((total_len - 20u) & 0xFFFFu);  // Go int, 2 bytes
+            pl.go_hi = L;
+            pl.go_field = f;
+            pl.go_extra = sum_addrs + (l4_go << 8) + bswap16((total_len - 20u) & 0xFFFFu);  // Go int, 2 bytes
         }
     }
 
-    // eth_tx software fill (cgo/dpdk.c:333-365), after everything else
+    // eth_tx software fill (cgo/dpdk.c:333-365), after everything else. Its IPv4 sum covers
+    // IHL*4 bytes, which for IHL >= 7 include the UDP (>= 10: TCP) checksum field as the Go
+    // steps left it; the field is zeroed only after that sum (dpdk.c:345 then :350).
     if (alive && (steps & HALO_TX_DPDK_FILL) && (m[3] & 0xFFFFu) == 0x0008u) {
         if (L < 34) {
             res |= HALO_TX_R_OVERRUN;
@@ -203,18 +205,17 @@ __device__ __forceinline__ TxPlan apply_steps(uint32_t (&m)[kHdrDw], uint32_t& d
                 if (f + 2u > L) {
                     res |= HALO_TX_R_OVERRUN;  // (a Go L4 recalc cannot have run: its guard is stricter)
                 } else {
-                    if (f == 50u) SET_LE16(50, 0);
-                    else SET_LE16(40, 0);
-                    pl.l4_hi = 0; pl.l4_field = 0; pl.l4_extra = 0;  // DPDK's value replaces Go's
+                    pl.dp_zero = f;
+                    if (pl.ip_hi <= f) pl.go_hi = 0;  // the Go value is overwritten unseen
                     const uint32_t l3 = bswap16(m[4] & 0xFFFFu);
                     if (l3 >= ihl4) {
                         const uint32_t l4_len = l3 - ihl4;
                         if (34u + l4_len > L) {
                             res |= HALO_TX_R_OVERRUN;
                         } else {
-                            pl.l4_hi = 34u + l4_len;
-                            pl.l4_field = f;
-                            pl.l4_extra = sum_addrs + (proto << 8) + bswap16(l4_len);
+                            pl.dp_hi = 34u + l4_len;
+                            pl.dp_field = f;
+                            pl.dp_extra = sum_addrs + (proto << 8) + bswap16(l4_len);
                             pl.udp_zero_ffff = proto == kIpUdp;
                         }
                     }
@@ -260,14 +261,18 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
     const TxPlan pl = apply_steps(m, dirty, L, steps, op.y,
                                   op.x >> 16, op.w, op.z & 0xFFFFu, (p.flags & HALO_RX_CSUM_ENABLE) != 0, res);
 
-    // sums over the final bytes: the header copy + this lane's loaded dwords past it
-    uint64_t c_ip = 0, c_l4 = 0;
-    const uint32_t hi = pl.ip_hi > pl.l4_hi ? pl.ip_hi : pl.l4_hi;
+    // Sums over the final bytes: the header copy + this lane's loaded dwords past it. One pass
+    // accumulates the IPv4 tail (IHL >= 10 only) and the first L4 range; the second L4 range
+    // (Go value overwritten by DPDK but covered by an IHL >= 7 IPv4 sum) takes a second pass.
+    const uint32_t l4a = pl.go_hi ? pl.go_hi : pl.dp_hi;        // first L4 range
+    const uint32_t l4b = pl.go_hi ? pl.dp_hi : 0u;              // second (rare)
+    uint64_t c_ip = 0, c_a = 0, c_b = 0;
+    const uint32_t hi = pl.ip_hi > l4a ? pl.ip_hi : l4a;
     if (hi > 4 * kHdrDw) {
 #pragma unroll
         for (int u = 0; u < U0; ++u) {
-            acc_tail(buf[u], (u * G + gl) * 4, pl.ip_hi, c_ip);
-            acc_tail(buf[u], (u * G + gl) * 4, pl.l4_hi, c_l4);
+            if (pl.ip_hi > 4 * kHdrDw) acc_tail(buf[u], (u * G + gl) * 4, pl.ip_hi, c_ip);
+            acc_tail(buf[u], (u * G + gl) * 4, l4a, c_a);
         }
         const uint32_t seg_dw = (hi + 3) >> 2;
         for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
@@ -276,24 +281,45 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
             for (int u = 0; u < U; ++u) load4(frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                acc_tail(x[u], r0 + (u * G + gl) * 4, pl.ip_hi, c_ip);
-                acc_tail(x[u], r0 + (u * G + gl) * 4, pl.l4_hi, c_l4);
+                if (pl.ip_hi > 4 * kHdrDw) acc_tail(x[u], r0 + (u * G + gl) * 4, pl.ip_hi, c_ip);
+                acc_tail(x[u], r0 + (u * G + gl) * 4, l4a, c_a);
             }
         }
     }
+    if (l4b > 4 * kHdrDw) {
+        const uint32_t seg_dw = (l4b + 3) >> 2;
+        for (uint32_t r0 = 0; r0 < seg_dw; r0 += U * STEP) {
+            uint32_t x[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load4(frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc_tail(x[u], r0 + (u * G + gl) * 4, l4b, c_b);
+        }
+    }
     const uint32_t g_ip = group_sum<G>(fold64(c_ip));
-    const uint32_t g_l4 = group_sum<G>(fold64(c_l4));
+    const uint32_t g_a = group_sum<G>(fold64(c_a));
+    const uint32_t g_b = l4b ? group_sum<G>(fold64(c_b)) : 0u;
+    auto set_l4 = [&](uint32_t field, uint32_t v) {
+        if (field == 36u) SET_LE16(36, v);
+        else if (field == 40u) SET_LE16(40, v);
+        else SET_LE16(50, v);
+    };
+    // the reference's order: Go L4 (NAT / RECALC), then the IPv4 header, then DPDK's L4
+    if (pl.go_hi) {
+        const uint32_t s = fold16(fold64((uint64_t)g_a + header_sum(m, 34, pl.go_hi) + pl.go_extra));
+        set_l4(pl.go_field, ~s);
+    }
     if (pl.ip_hi) {
         const uint32_t s = fold16(fold64((uint64_t)g_ip + header_sum(m, 14, pl.ip_hi)));
         SET_LE16(24, ~s);
     }
-    if (pl.l4_hi) {
-        const uint32_t s = fold16(fold64((uint64_t)g_l4 + header_sum(m, 34, pl.l4_hi) + pl.l4_extra));
+    if (pl.dp_zero) set_l4(pl.dp_zero, 0u);
+    if (pl.dp_hi) {
+        const uint32_t g = pl.go_hi ? g_b : g_a;
+        const uint32_t s = fold16(fold64((uint64_t)g + header_sum(m, 34, pl.dp_hi) + pl.dp_extra));
         uint32_t f = (~s) & 0xFFFFu;
         if (pl.udp_zero_ffff && f == 0) f = 0xFFFFu;
-        if (pl.l4_field == 36u) SET_LE16(36, f);
-        else if (pl.l4_field == 40u) SET_LE16(40, f);
-        else SET_LE16(50, f);
+        set_l4(pl.dp_field, f);
     }
 
     if (present && gl == 0) {

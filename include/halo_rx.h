@@ -251,6 +251,32 @@ HALO_API int halo_tx_fixup_batch_device(uint8_t* d_bytes, const uint32_t* d_offs
                                         uint32_t max_len_hint, uint8_t* d_result,
                                         halo_stream_t stream);
 
+/* ---- flow-key hashing --------------------------------------------
+ * hashcode.GetHashCodeXXH3 (hashcode/hashcode.go:15-17 -> hashcode/xxh3.go:43-287, XXH3-64 with
+ * the default secret and seed 0, ported from github.com/zeebo/xxh3 v1.1.0) over a batch of byte
+ * strings, and the NAT flow-table keys the forward path hashes for every NATed packet. */
+#define HALO_FLOW_NAT_LAN 0u  /* NatFlowHash{remote=dst, dport, lan host=src, sport, proto} as
+                                 NatGetFlowByHash builds it (engine/ipv4_engine.go:524-551)   */
+#define HALO_FLOW_NAT_WAN 1u  /* NatWanFlowHash{remote=src, sport, wan=dst, dport, proto} as
+                                 NatGetFlowByWan builds it (engine/ipv4_engine.go:554-581)    */
+#define HALO_NAT_SYMMETRIC 0u /* NetIfConfig.NatType (engine/ipv4_engine.go:423-426): remote  */
+#define HALO_NAT_FULL_CONE 1u /* address/port kept (symmetric) or zeroed (any other value)   */
+
+/* d_hash[i] = XXH3-64(d_bytes[d_offsets[i] : d_offsets[i] + d_lens[i]]). Byte offsets, any
+ * alignment. Asynchronous on `stream`. */
+HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const uint64_t* d_offsets, const uint32_t* d_lens,
+                                       uint32_t n, uint64_t* d_hash, halo_stream_t stream);
+
+/* For each parsed record: build the 13-byte little-endian flow key of `kind` (the ICMP remote
+ * port is 0, the remote address and port are 0 unless nat_type is HALO_NAT_SYMMETRIC), hash it
+ * with XXH3-64 (NatFlowHash.GetHashCode, engine/ipv4_engine.go:451-459; NatWanFlowHash
+ * :471-479) into d_hash[i], and, when d_bucket is non-null, write the hashmap bucket
+ * hash % bucket_count (hashmap/hashmap.go:64) into d_bucket[i]. Records are used as they are;
+ * callers hash the records whose engine action is FORWARD. */
+HALO_API int halo_flow_hash_device(const halo_rx_result_t* d_records, uint32_t n, uint32_t kind, uint32_t nat_type,
+                                   uint64_t* d_hash, uint32_t bucket_count, uint32_t* d_bucket,
+                                   halo_stream_t stream);
+
 /* ---- the reference engine's per-frame decision (engine/ethernet_engine.go:13-31,
  *      engine/ipv4_engine.go:18-47, engine/{udp,tcp,icmp}_engine.go) ------------------ */
 typedef enum halo_rx_action {

@@ -44,7 +44,7 @@ class NetIf(ctypes.Structure):
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(HERE, f) for f in ("halo_rx_oracle.c", "halo_tx_oracle.c")]
+    srcs = [os.path.join(HERE, f) for f in ("halo_rx_oracle.c", "halo_tx_oracle.c", "halo_xxh3_oracle.c")]
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, srcs)):
         subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
     return LIB_PATH
@@ -76,6 +76,12 @@ def lib() -> ctypes.CDLL:
         L.ora_synth_frame.argtypes = [u64, u64, u32, ctypes.c_uint8, ctypes.POINTER(NetIf), vp]
         L.ora_tx_frame.restype = ctypes.c_uint8
         L.ora_tx_frame.argtypes = [vp, u32, vp, u32]
+        L.ora_xxh3_64.restype = ctypes.c_uint64
+        L.ora_xxh3_64.argtypes = [vp, ctypes.c_size_t]
+        L.ora_xxh3_batch.restype = None
+        L.ora_xxh3_batch.argtypes = [vp, vp, vp, u32, vp]
+        L.ora_flow_hash_batch.restype = None
+        L.ora_flow_hash_batch.argtypes = [vp, u32, u32, u32, vp, u32, vp]
         L.ora_tx_batch.restype = ctypes.c_int
         L.ora_tx_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, ctypes.c_int]
         _lib = L
@@ -175,3 +181,27 @@ def tx_batch(data: np.ndarray, offsets_dw: np.ndarray, lens: np.ndarray, ops: np
     ops_c = np.ascontiguousarray(ops, dtype=TX_OP_DTYPE)
     assert lib().ora_tx_batch(_p(out), _p(offs), _p(lens_c), n, _p(ops_c), flags, _p(res), threads) == 0
     return out, res
+
+
+def xxh3_64(data: bytes) -> int:
+    b = np.frombuffer(bytes(data) + b"\0", dtype=np.uint8)
+    return int(lib().ora_xxh3_64(_p(b), len(data)))
+
+
+def xxh3_batch(data: np.ndarray, offsets: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    n = int(lens.shape[0])
+    out = np.zeros(n, dtype=np.uint64)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    lib().ora_xxh3_batch(_p(data), _p(np.ascontiguousarray(offsets, np.uint64)),
+                         _p(np.ascontiguousarray(lens, np.uint32)), n, _p(out))
+    return out
+
+
+def flow_hash_batch(records: np.ndarray, kind: int, nat_type: int, bucket_count: int = 0):
+    """(hash u64[n], bucket u32[n] or None) for halo_rx_result_t records."""
+    recs = np.ascontiguousarray(records).view(RESULT_DTYPE)
+    n = recs.shape[0]
+    h = np.zeros(n, dtype=np.uint64)
+    b = np.zeros(n, dtype=np.uint32) if bucket_count else None
+    lib().ora_flow_hash_batch(_p(recs), n, kind, nat_type, _p(h), bucket_count, _p(b))
+    return h, b

@@ -1,0 +1,115 @@
+"""GPU parity for §8f row f3: halo_xxh3_64_batch_device and halo_flow_hash_device against the
+committed fixtures and the C oracle (itself pinned to the published XXH3-64 vectors), bit-exact."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    from halo_amd import _lib
+
+    _lib.check("halo_rx_init", _lib.lib.halo_rx_init(0))
+    return torch.device("cuda:0")
+
+
+def _xxh3_dev(dev, data, offs, lens):
+    import torch
+
+    from halo_amd import hashcode
+
+    d = torch.from_numpy(np.ascontiguousarray(data, np.uint8)).to(dev)
+    o = torch.from_numpy(np.ascontiguousarray(offs, np.uint64).view(np.int64)).to(dev)
+    ln = torch.from_numpy(np.ascontiguousarray(lens, np.uint32).view(np.int32)).to(dev)
+    h = hashcode.GetHashCodeXXH3(d, o, ln)
+    torch.cuda.synchronize()
+    return h.cpu().numpy().view(np.uint64)
+
+
+def test_xxh3_fixture_strings(dev):
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "flow_hash.json")))
+    stream = np.fromfile(os.path.join(ROOT, "tests", "golden", "hash_stream.bin"), dtype=np.uint8)
+    offs = np.array([s["offset"] for s in meta["strings"]], np.uint64)
+    lens = np.array([s["len"] for s in meta["strings"]], np.uint32)
+    got = _xxh3_dev(dev, stream, offs, lens)
+    want = np.array([int(s["hash"], 16) for s in meta["strings"]], np.uint64)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(lens[i]), int(offs[i])) for i in bad[:8]]
+
+
+@pytest.mark.parametrize("mix", ["short", "long", "ragged", "kcp"])
+def test_xxh3_random_batches_vs_oracle(dev, oracle_lib, mix):
+    """Unaligned byte offsets; short-only, long-only, every class mixed, KCP-segment sizes."""
+    rng = np.random.default_rng({"short": 1, "long": 2, "ragged": 3, "kcp": 4}[mix])
+    n = 20_000
+    if mix == "short":
+        lens = rng.integers(0, 241, n)
+    elif mix == "long":
+        lens = rng.integers(241, 5000, n)
+    elif mix == "ragged":
+        lens = np.where(rng.random(n) < 0.2, rng.integers(241, 9001, n), rng.integers(0, 241, n))
+    else:
+        lens = rng.integers(24, 1400, n)  # KCP segments (protocol/kcp, ByteCheckModeXXH3)
+    lens = lens.astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    gaps = rng.integers(0, 7, n)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1].astype(np.uint64))
+    offs += 3
+    data = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 8, dtype=np.uint8)
+    got = _xxh3_dev(dev, data, offs, lens)
+    want = oracle_lib.xxh3_batch(data, offs, lens)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(lens[i]), int(offs[i])) for i in bad[:8]]
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("nat_type", [0, 1, 7])
+def test_flow_hash_golden_and_imix_records(dev, oracle_lib, golden, kind, nat_type):
+    """NAT flow keys from GPU-parsed records (golden frames + 200k IMIX) vs the oracle."""
+    import torch
+
+    from halo_amd import hashcode, protocol, synth
+    from halo_amd._lib import NetIf
+    from tests.helpers import golden_arrays
+
+    meta, blob = golden
+    data, offs, lens, _ = golden_arrays(meta, blob)
+    out_g = protocol.parse_frames_batch(torch.from_numpy(data).to(dev),
+                                        torch.from_numpy(offs.view(np.int32)).to(dev),
+                                        torch.from_numpy(lens.view(np.int16)).to(dev), netif=NetIf.make())
+    lay = synth.layout(200_000, size_mode=1, proto_mode=3, mutate_shift=5, first_index=31337)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    out_i = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                        max_len_hint=1500)
+    for out in (out_g, out_i):
+        for buckets in (0, 1024, 1000003):
+            h, b = hashcode.flow_hash(out, kind, nat_type, buckets)
+            torch.cuda.synchronize()
+            recs = protocol.records(out)
+            wh, wb = oracle_lib.flow_hash_batch(recs, kind, nat_type, buckets)
+            assert np.array_equal(h.cpu().numpy().view(np.uint64), wh)
+            if buckets:
+                assert np.array_equal(b.cpu().numpy().view(np.uint32), wb)
+
+
+def test_flow_hash_validation(dev):
+    from halo_amd import _lib
+
+    L = _lib.lib
+    assert L.halo_flow_hash_device(None, 0, 0, 0, None, 0, None, None) == 0
+    assert L.halo_flow_hash_device(None, 0, 2, 0, None, 0, None, None) == _lib.HALO_E_INVAL  # unknown kind
+    import torch
+
+    r = torch.zeros(64, dtype=torch.uint8, device=dev)
+    h = torch.zeros(2, dtype=torch.int64, device=dev)
+    assert L.halo_flow_hash_device(r.data_ptr(), 2, 0, 0, h.data_ptr(), 0, h.data_ptr(), None) == _lib.HALO_E_INVAL

@@ -76,3 +76,48 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_tx_steps(
     (void)hipEventDestroy(e1);
     return rc;
 }
+
+// Generic timed loop over a launch callback (row f3 kernels: flow-key hashing, XXH3 batches).
+template <typename F>
+static int timed_loop(F launch, int warmup, int steps, hipStream_t s, float* region_ms, double* wall_s) {
+    if (steps <= 0 || !region_ms || !wall_s) return HALO_E_INVAL;
+    int rc = HALO_OK;
+    for (int k = 0; k < warmup && rc == HALO_OK; ++k) rc = launch(k);
+    if (rc) return rc;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return HALO_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return HALO_E_HIP;
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)hipEventRecord(e0, s);
+    for (int k = 0; k < steps && rc == HALO_OK; ++k) rc = launch(k);
+    (void)hipEventRecord(e1, s);
+    if (hipStreamSynchronize(s) != hipSuccess && rc == HALO_OK) rc = HALO_E_HIP;
+    const auto t1 = std::chrono::steady_clock::now();
+    *wall_s = std::chrono::duration<double>(t1 - t0).count();
+    *region_ms = -1.0f;
+    (void)hipEventElapsedTime(region_ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_flow_steps(
+    int nbatch, const halo_rx_result_t* const* recs, uint32_t n, uint32_t kind, uint32_t nat_type, uint64_t* hash,
+    uint32_t buckets, uint32_t* bucket, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0) return HALO_E_INVAL;
+    auto launch = [&](int k) {
+        return halo_flow_hash_device(recs[k % nbatch], n, kind, nat_type, hash, buckets, bucket, stream);
+    };
+    return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
+}
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_xxh3_steps(
+    int nbatch, const uint8_t* const* bytes, const uint64_t* const* offsets, const uint32_t* const* lens, uint32_t n,
+    uint64_t* hash, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0) return HALO_E_INVAL;
+    auto launch = [&](int k) {
+        const int b = k % nbatch;
+        return halo_xxh3_64_batch_device(bytes[b], offsets[b], lens[b], n, hash, stream);
+    };
+    return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
+}

@@ -21,6 +21,8 @@ step() {
 for s in "$@"; do
   case $s in
     test)  step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
+    ttx)   step pytest_tx 600 python -m pytest tests/test_gpu_tx.py -m gpu -q -rf -x ;;
+    thash) step pytest_hash 600 python -m pytest tests/test_gpu_flow_hash.py -m gpu -q -rf -x ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py ;;
     benchq) step benchq 600 python bench.py --no-secondary --cpu-seconds 4 ;;
@@ -30,10 +32,10 @@ for s in "$@"; do
     tune)  step tune 900 python tools/tune.py ;;
     dist2) step dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 50 --warmup 5 ;;
     list)  step counters 300 rocprofv3 -L ;;
-    kt)    step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 tools/prof_kernels.py ;;
-    kfetch) step kfetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/kfetch" -o run -- python3 tools/prof_kernels.py ;;
-    kwrite) step kwrite 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/kwrite" -o run -- python3 tools/prof_kernels.py ;;
-    ksq)   step ksq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ksq" -o run -- python3 tools/prof_kernels.py ;;
+    kt)    step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
+    kfetch) step kfetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/kfetch" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
+    kwrite) step kwrite 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/kwrite" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
+    ksq)   step ksq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ksq" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
     tuneq) step tuneq 600 python tools/tune.py --quick ;;
     *) echo "unknown step $s" ;;
   esac

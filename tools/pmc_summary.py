@@ -2,7 +2,9 @@
 """Summarise a tools/gpu_session.sh profiling session (kt, kfetch, kwrite, ksq steps) into
 per-workload numbers and write profiles/pmc_summary.json (read by bench.py for `traffic`).
 
-    python tools/pmc_summary.py gpurun_out/<tag> [--out profiles/pmc_summary.json]
+    python tools/pmc_summary.py gpurun_out/<tag> [--out profiles/pmc_summary.json] [--only W1,W2]
+
+(--only: the session ran tools/prof_kernels.py with that workload filter, PK_ARGS.)
 
 rx_* / tx_fixup_* dispatches are attributed to tools/prof_kernels.py's WORKLOADS in launch order.
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from separate
@@ -41,6 +43,9 @@ def alg_bytes():
         lay = synth.layout(n, **kw, ragged=not slen)
         frames = int(lay["lens"].astype("int64").sum())
         meta = 0 if slen else 6 * n
+        if name.startswith("flow_hash"):  # record bytes 0..19 in; hash + bucket out
+            out[name] = (20 * n, 12 * n)
+            continue
         if name.startswith("tx_"):  # + 16 B op in; 1 B result + 20 B of rewritten header out
             import bench
 
@@ -56,13 +61,25 @@ def main():
         ROOT, "profiles", "pmc_summary.json")
     from tools.prof_kernels import WORKLOADS
 
+    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     order = []
     for name, _kw, _n, _rot, launches, *_ in WORKLOADS:
-        order += [name] * launches
+        if only is None or name in only:
+            order += [name] * launches
+
+    def family(w):
+        return "flow_hash_kernel" if w.startswith("flow_hash") else ("tx_fixup" if w.startswith("tx_") else "rx_")
 
     def attribute(rows, key="Dispatch_Id"):
-        disp = sorted({int(r[key]) for r in rows if "rx_" in r["Kernel_Name"] or "tx_fixup" in r["Kernel_Name"]})
-        return {d: order[k] for k, d in enumerate(disp) if k < len(order)}
+        """dispatch id -> workload: each kernel family's dispatches in launch order."""
+        amap = {}
+        for fam in ("rx_", "tx_fixup", "flow_hash_kernel"):
+            disp = sorted({int(r[key]) for r in rows if fam in r["Kernel_Name"]})
+            ws = [w for w in order if family(w) == fam]
+            # (the flow-hash workload's one preparatory parse comes after every rx workload's
+            # launches, WORKLOADS order, so it falls outside ws and is not attributed)
+            amap.update({d: ws[k] for k, d in enumerate(disp) if k < len(ws)})
+        return amap
 
     res = defaultdict(lambda: defaultdict(list))
     kt = _rows(os.path.join(sess, "kt", "run_kernel_trace.csv"))
@@ -121,8 +138,16 @@ def main():
             s["eff_clock_GHz"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / avg["duration_ns"], 3)
         summary[w] = s
     os.makedirs(os.path.dirname(out_path), exist_ok=True)
+    merged = {}
+    if "--merge" in sys.argv and os.path.exists(out_path):  # keep other workloads' entries
+        merged = json.load(open(out_path))
+    merged.update(summary)
+    merged.setdefault("sessions", {})
+    for w in summary:
+        merged["sessions"][w] = os.path.basename(sess.rstrip("/"))
+    merged.pop("session", None)
     with open(out_path, "w") as fh:
-        json.dump({"session": os.path.basename(sess.rstrip("/")), **summary}, fh, indent=1)
+        json.dump(merged, fh, indent=1)
     for w, s in summary.items():
         print(w, json.dumps(s))
 

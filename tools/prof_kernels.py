@@ -23,6 +23,8 @@ WORKLOADS = [
     ("config5_jumbo_9000B_tcp_4M_ext", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, 3, 9000, 3, 0),
     # forward / transmit rewrite (§8f row f2): bench.TX_BENCH_STEPS on the config 2 frames
     ("tx_config2", dict(length=64), 1 << 20, 8, 20, 0, 1, 64),
+    # flow-key hashing (§8f row f3): NatWanFlowHash + bucket on the parsed config 2 records
+    ("flow_hash_config2", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
 ]
 
 
@@ -49,6 +51,23 @@ def main():
             ops = torch.from_numpy(bench.tx_ops_for(n).view(np.uint8)).to(dev)
         torch.cuda.synchronize()
         stream = torch.cuda.current_stream().cuda_stream
+        if name.startswith("flow_hash"):
+            from halo_amd import protocol
+
+            fr = bs[0]
+            protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=netif, max_len_hint=64,
+                                        out=out)
+            h = torch.empty(n, dtype=torch.int64, device=dev)
+            bk = torch.empty(n, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            for i in range(launches):
+                _lib.check("flow", _lib.lib.halo_flow_hash_device(out.data_ptr(), n, 1, 0, h.data_ptr(), 1 << 20,
+                                                                  bk.data_ptr(), stream))
+            torch.cuda.synchronize()
+            print(f"{name}: {launches} launches of {n} records", flush=True)
+            del bs, out
+            torch.cuda.empty_cache()
+            continue
         for i in range(launches):
             fr = bs[i % len(bs)]
             if ops is not None:
