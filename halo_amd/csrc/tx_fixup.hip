@@ -323,11 +323,24 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
     }
 
     if (present && gl == 0) {
+        // dirty header dwords back to the frame: 16-byte stores for dwords 4..7 and 8..11 when
+        // they lie inside the frame (fewer, wider store instructions; the clean dwords among
+        // them are rewritten with their own values), single dwords / bytes otherwise
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
         __attribute__((address_space(1))) uint32_t* fw =
             (__attribute__((address_space(1))) uint32_t*)reinterpret_cast<uint32_t*>(frame);
+        uint32_t rest = dirty;
+        if ((dirty & 0x0F0u) && L >= 32) {
+            *(__attribute__((address_space(1))) u32x4*)(fw + 4) = (u32x4){m[4], m[5], m[6], m[7]};
+            rest &= ~0x0F0u;
+        }
+        if ((dirty & 0xF00u) && L >= 48) {
+            *(__attribute__((address_space(1))) u32x4*)(fw + 8) = (u32x4){m[8], m[9], m[10], m[11]};
+            rest &= ~0xF00u;
+        }
 #pragma unroll
         for (uint32_t d = 3; d < kHdrDw; ++d) {
-            if (dirty & (1u << d)) {
+            if (rest & (1u << d)) {
                 if (4 * d + 4 <= L) {
                     fw[d] = m[d];
                 } else {
