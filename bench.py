@@ -134,6 +134,8 @@ def bench_lib():
         tail = [i32, i32, vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
         L.halo_bench_flow_steps.restype = ctypes.c_int
         L.halo_bench_flow_steps.argtypes = [i32, vp, u32, u32, u32, vp, u32, vp] + tail
+        L.halo_bench_route_steps.restype = ctypes.c_int
+        L.halo_bench_route_steps.argtypes = [i32, vp, vp, u32, vp] + tail
         L.halo_bench_xxh3_steps.restype = ctypes.c_int
         L.halo_bench_xxh3_steps.argtypes = [i32, vp, vp, vp, u32, vp] + tail
         _BENCH_LIB = L
@@ -289,6 +291,50 @@ def xxh3_secondary(dev, steps, warmup, d: Dist):
     res = {"strings": n, "mstrings_per_s": round(n * steps / w / 1e6, 1),
            "gbytes_per_s": round(bs[0][3] * steps / w / 1e9, 1), "kernel_ms": round(k, 4),
            "roofline": roofline(alg, k, load_traffic("xxh3_kcp_1M")), "alg_bytes_per_launch": alg}
+    del bs
+    return res
+
+
+def route_secondary(dev, steps, warmup, d: Dist):
+    """§8f f4, FindRoute on the GPU: a 500k-prefix table (BGP-like length mix, 1 in 8 prefixes
+    with a second ECMP next hop, a default route), 4M uniformly random destination addresses per
+    launch, route id out."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from halo_amd.route import RouteTable
+
+    rng = np.random.default_rng(0x524F5554)
+    n_pfx = 500_000
+    plen = rng.choice([8, 12, 16, 18, 19, 20, 21, 22, 23, 24, 24, 24, 24, 24, 24, 25, 26, 27, 28, 30, 32], n_pfx)
+    mask = ((0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF).astype(np.uint32)
+    dst = rng.integers(0, 1 << 32, n_pfx, dtype=np.uint64).astype(np.uint32) & mask
+    t = RouteTable(dev.index or 0)
+    t.AddRoute(t.entry(0, 0, 0xC0A86401, 0))
+    for k in range(n_pfx):
+        e = t.entry(int(dst[k]), int(mask[k]), k + 2, k & 3)
+        t.AddRoute(e)
+        if k % 8 == 0:
+            t.AddRoute(t.entry(int(dst[k]), int(mask[k]), k + 3, k & 3))
+    t0 = time.perf_counter()
+    t.sync()
+    sync_s = time.perf_counter() - t0
+    n = 4 << 20
+    bs = [torch.from_numpy(rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32).view(np.int32)).to(dev)
+          for _ in range(4)]
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    arr = (ctypes.c_void_p * len(bs))(*[b.data_ptr() for b in bs])
+    w, k = time_native(bench_lib().halo_bench_route_steps, len(bs), t._t, arr, n, out.data_ptr(), steps=steps,
+                       warmup=warmup, d=d)
+    alg = n * (4 + 4)
+    res = {"lookups": n, "mlookups_per_s": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 4),
+           "roofline": roofline(alg, k, load_traffic("route_lpm_4M")), "alg_bytes_per_launch": alg,
+           "table": f"{n_pfx} prefixes + default, DIR-24-8 (64 MB first level)", "sync_s": round(sync_s, 3),
+           "note": "alg bytes = address in + route id out; each lookup also reads 1-2 random 4 B table "
+                   "entries (tbl24 stays resident in the 256 MB Infinity Cache)"}
+    t.close()
     del bs
     return res
 
@@ -465,6 +511,8 @@ def main():
         del batches
         torch.cuda.empty_cache()
         sec["xxh3_kcp_segments_1M"] = xxh3_secondary(dev, max(5, args.steps // 10), 2, d)
+        torch.cuda.empty_cache()
+        sec["route_lpm_500k_prefixes"] = route_secondary(dev, max(10, args.steps // 4), 3, d)
         torch.cuda.empty_cache()
         for name, kw, hint, strided_len, flags in [
             ("1500B_udp_1M", dict(length=1500), 1500, 0, 1),

@@ -85,6 +85,8 @@ TX_NAT_DST, TX_TTL, TX_NAT_SRC, TX_RECALC, TX_DPDK_FILL = 0x01, 0x02, 0x04, 0x08
 TX_R_TTL_ALIVE, TX_R_SKIPPED, TX_R_OVERRUN = 0x01, 0x02, 0x04
 FLOW_NAT_LAN, FLOW_NAT_WAN = 0, 1        # HALO_FLOW_*
 NAT_SYMMETRIC, NAT_FULL_CONE = 0, 1      # HALO_NAT_* (engine.NatTypeSymmetric / NatTypeFullCone)
+ROUTE_DTYPE = np.dtype([("dst_ip", "<u4"), ("network_mask", "<u4"), ("next_hop", "<u4"), ("netif", "<u4")])
+ROUTE_NONE, ROUTE_PANIC = 0xFFFFFFFF, 0xFFFFFFFE  # HALO_ROUTE_*
 
 
 class NetIf(ctypes.Structure):
@@ -137,6 +139,14 @@ _PROTOS = {
     "halo_xxh3_64_batch_device": (ctypes.c_int, [_u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_flow_hash_device": (ctypes.c_int, [
         _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
+    "halo_route_table_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+    "halo_route_table_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "halo_route_update": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint32)]),
+    "halo_route_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, _u8p]),
+    "halo_route_sync_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "halo_route_lookup_device": (ctypes.c_int, [ctypes.c_void_p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
+    "halo_route_lookup_records_device": (ctypes.c_int, [
+        ctypes.c_void_p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_synth_layout": (ctypes.c_int, [
         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint64)]),

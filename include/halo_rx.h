@@ -277,6 +277,42 @@ HALO_API int halo_flow_hash_device(const halo_rx_result_t* d_records, uint32_t n
                                    uint64_t* d_hash, uint32_t bucket_count, uint32_t* d_bucket,
                                    halo_stream_t stream);
 
+/* ---- route lookup ---------------------------------------------------
+ * RouteTable (engine/ipv4_engine.go:270-390): a binary trie of route lists, longest-prefix
+ * FindRoute with an ECMP pick lastMatch[fnv32a(ip) % len] (engine/engine.go:159). The trie is
+ * the control plane and is kept on the host exactly as UpdateRoute builds it (including lists
+ * emptied by DeleteRoute, which still end a lookup); halo_route_sync_device compiles it into a
+ * DIR-24-8 table in HBM (a 2^24-entry first level, 256-entry second-level blocks for prefixes
+ * longer than /24) and lookups run on the GPU only. Route ids identify the RouteEntry objects:
+ * each insertion gets a fresh id. */
+typedef struct halo_route_table halo_route_table_t;
+typedef struct halo_route_entry {
+    uint32_t dst_ip;       /* IpAddrToU(DstIpAddr)   */
+    uint32_t network_mask; /* IpAddrToU(NetworkMask) */
+    uint32_t next_hop;     /* IpAddrToU(NextHop); 0 for nil (direct routes) */
+    uint32_t netif;        /* the caller's id for the NetIf name */
+} halo_route_entry_t;
+#define HALO_ROUTE_NONE 0xFFFFFFFFu  /* FindRoute returns nil (no route)                        */
+#define HALO_ROUTE_PANIC 0xFFFFFFFEu /* the longest match is a list DeleteRoute emptied: Go's
+                                        `% uint32(len(lastMatch))` divides by zero (:382)       */
+
+HALO_API int halo_route_table_create(halo_route_table_t** out);
+HALO_API int halo_route_table_destroy(halo_route_table_t* t);
+/* UpdateRoute(old, new) (:304-348): walks old's prefix, drops entries equal to old (dst, mask,
+ * next hop, netif), appends new (if non-null, with a fresh id written to *new_id). AddRoute is
+ * update(r, r), DeleteRoute is update(r, NULL) (:293-301). */
+HALO_API int halo_route_update(halo_route_table_t* t, const halo_route_entry_t* old_route,
+                               const halo_route_entry_t* new_route, uint32_t* new_id);
+HALO_API int halo_route_get(const halo_route_table_t* t, uint32_t id, halo_route_entry_t* out);
+/* Compile the trie into the device table on `device` (allocates / grows HBM; synchronous). */
+HALO_API int halo_route_sync_device(halo_route_table_t* t, int device);
+/* FindRoute for each address (IpAddrToU form) / each record's dst_ip: route id, HALO_ROUTE_NONE
+ * or HALO_ROUTE_PANIC. Asynchronous on `stream`; uses the last synced table. */
+HALO_API int halo_route_lookup_device(const halo_route_table_t* t, const uint32_t* d_ips, uint32_t n,
+                                      uint32_t* d_route_ids, halo_stream_t stream);
+HALO_API int halo_route_lookup_records_device(const halo_route_table_t* t, const halo_rx_result_t* d_records,
+                                              uint32_t n, uint32_t* d_route_ids, halo_stream_t stream);
+
 /* ---- the reference engine's per-frame decision (engine/ethernet_engine.go:13-31,
  *      engine/ipv4_engine.go:18-47, engine/{udp,tcp,icmp}_engine.go) ------------------ */
 typedef enum halo_rx_action {

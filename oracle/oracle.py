@@ -44,7 +44,8 @@ class NetIf(ctypes.Structure):
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(HERE, f) for f in ("halo_rx_oracle.c", "halo_tx_oracle.c", "halo_xxh3_oracle.c")]
+    srcs = [os.path.join(HERE, f) for f in ("halo_rx_oracle.c", "halo_tx_oracle.c", "halo_xxh3_oracle.c",
+                                            "halo_route_oracle.c")]
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, srcs)):
         subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
     return LIB_PATH
@@ -82,6 +83,16 @@ def lib() -> ctypes.CDLL:
         L.ora_xxh3_batch.argtypes = [vp, vp, vp, u32, vp]
         L.ora_flow_hash_batch.restype = None
         L.ora_flow_hash_batch.argtypes = [vp, u32, u32, u32, vp, u32, vp]
+        L.ora_route_create.restype = vp
+        L.ora_route_create.argtypes = []
+        L.ora_route_destroy.restype = None
+        L.ora_route_destroy.argtypes = [vp]
+        L.ora_route_update.restype = u32
+        L.ora_route_update.argtypes = [vp, vp, vp]
+        L.ora_route_find.restype = u32
+        L.ora_route_find.argtypes = [vp, u32]
+        L.ora_route_find_batch.restype = None
+        L.ora_route_find_batch.argtypes = [vp, vp, u32, vp]
         L.ora_tx_batch.restype = ctypes.c_int
         L.ora_tx_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, ctypes.c_int]
         _lib = L
@@ -205,3 +216,38 @@ def flow_hash_batch(records: np.ndarray, kind: int, nat_type: int, bucket_count:
     b = np.zeros(n, dtype=np.uint32) if bucket_count else None
     lib().ora_flow_hash_batch(_p(recs), n, kind, nat_type, _p(h), bucket_count, _p(b))
     return h, b
+
+
+ROUTE_DTYPE = np.dtype([("dst_ip", "<u4"), ("network_mask", "<u4"), ("next_hop", "<u4"), ("netif", "<u4")])
+
+
+class RouteTable:
+    """The C restatement of engine.RouteTable (oracle/halo_route_oracle.c)."""
+
+    def __init__(self):
+        self._t = lib().ora_route_create()
+
+    def __del__(self):
+        if getattr(self, "_t", None):
+            lib().ora_route_destroy(self._t)
+            self._t = None
+
+    def update(self, old, new=None) -> int:
+        o = np.array([tuple(old)], ROUTE_DTYPE)
+        n = None if new is None else np.array([tuple(new)], ROUTE_DTYPE)
+        return int(lib().ora_route_update(self._t, _p(o), _p(n)))
+
+    def add(self, r) -> int:
+        return self.update(r, r)
+
+    def delete(self, r) -> None:
+        self.update(r, None)
+
+    def find(self, ip: int) -> int:
+        return int(lib().ora_route_find(self._t, ip))
+
+    def find_batch(self, ips: np.ndarray) -> np.ndarray:
+        ips = np.ascontiguousarray(ips, np.uint32)
+        out = np.zeros(ips.shape[0], np.uint32)
+        lib().ora_route_find_batch(self._t, _p(ips), ips.shape[0], _p(out))
+        return out

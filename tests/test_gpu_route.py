@@ -1,0 +1,123 @@
+"""GPU parity for §8f row f4: the DIR-24-8 lookup compiled from the host trie
+(halo_route_sync_device + halo_route_lookup_*_device) against the committed fixtures and the C
+oracle, bit-exact route ids (incl. HALO_ROUTE_NONE / HALO_ROUTE_PANIC)."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    from halo_amd import _lib
+
+    _lib.check("halo_rx_init", _lib.lib.halo_rx_init(0))
+    return torch.device("cuda:0")
+
+
+def _replay_both(ops, oracle_lib):
+    from halo_amd.route import RouteTable
+
+    g, o = RouteTable(0), oracle_lib.RouteTable()
+    for op in ops:
+        if op[0] == "add":
+            assert g.AddRoute(RouteTable.entry(*op[1])) == o.add(op[1])
+        elif op[0] == "del":
+            g.DeleteRoute(RouteTable.entry(*op[1]))
+            o.delete(op[1])
+        else:
+            assert g.UpdateRoute(RouteTable.entry(*op[1]), RouteTable.entry(*op[2])) == o.update(op[1], op[2])
+    return g, o
+
+
+def _lookup(dev, g, ips):
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(ips, np.uint32).view(np.int32)).to(dev)
+    out = g.FindRoute(t)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+def test_route_fixture_scenarios(dev, oracle_lib):
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "route.json")))
+    for s in meta["scenarios"]:
+        g, _ = _replay_both(s["ops"], oracle_lib)
+        g.sync()
+        got = _lookup(dev, g, np.array(s["lookups"], np.uint32))
+        assert got.tolist() == s["expect"], s["name"]
+
+
+def test_route_large_table_and_resync(dev, oracle_lib):
+    """200k prefixes (BGP-like length mix, ECMP groups, /25-/32 under /24 blocks), 2M lookups;
+    then delete / update a slice and re-sync: the device table follows the trie."""
+    rng = np.random.default_rng(7)
+    n = 200_000
+    plen = rng.choice([8, 12, 16, 19, 20, 21, 22, 23, 24, 24, 24, 24, 25, 26, 28, 30, 32], n)
+    mask = np.where(plen > 0, (0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF, 0).astype(np.uint32)
+    dst = (rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) & mask)
+    ops = [("add", [0, 0, 1, 0])]
+    for k in range(n):
+        ops.append(("add", [int(dst[k]), int(mask[k]), int(k + 10), int(k % 4)]))
+        if k % 9 == 0:
+            ops.append(("add", [int(dst[k]), int(mask[k]), int(k + 11), int(k % 4)]))
+    g, o = _replay_both(ops, oracle_lib)
+    g.sync()
+    ips = np.concatenate([rng.integers(0, 1 << 32, 1 << 20, dtype=np.uint64).astype(np.uint32),
+                          (dst[rng.integers(0, n, 1 << 20)] | rng.integers(0, 256, 1 << 20).astype(np.uint32))])
+    assert np.array_equal(_lookup(dev, g, ips), o.find_batch(ips))
+    for k in range(0, n, 50):
+        r = [int(dst[k]), int(mask[k]), int(k + 10), int(k % 4)]
+        if k % 100 == 0:
+            g.DeleteRoute(g.entry(*r))
+            o.delete(r)
+        else:
+            new = [int(dst[k]), int(mask[k]), 7, 3]
+            assert g.UpdateRoute(g.entry(*r), g.entry(*new)) == o.update(r, new)
+    g.sync()
+    assert np.array_equal(_lookup(dev, g, ips), o.find_batch(ips))
+
+
+def test_route_lookup_from_records(dev, oracle_lib):
+    """FindRoute(ipv4DstAddr) straight from parsed rx records (IMIX batch)."""
+    import torch
+
+    from halo_amd import protocol, synth
+    from halo_amd._lib import NetIf
+
+    ops = [("add", [0, 0, 1, 0]), ("add", [0xC0A86400, 0xFFFFFF00, 0, 1]), ("add", [0xC0A86464, 0xFFFFFFFF, 0, 2]),
+           ("add", [0x0A000000, 0xFF000000, 5, 3]), ("add", [0x0A000000, 0xFF000000, 6, 3])]
+    g, o = _replay_both(ops, oracle_lib)
+    g.sync()
+    lay = synth.layout(100_000, size_mode=1, proto_mode=3, first_index=99)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    out = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                      max_len_hint=1500)
+    rid = g.FindRouteRecords(out)
+    torch.cuda.synchronize()
+    recs = protocol.records(out)
+    assert np.array_equal(rid.cpu().numpy().view(np.uint32), o.find_batch(recs["dst_ip"]))
+
+
+def test_route_validation(dev):
+    import ctypes
+
+    import torch
+
+    from halo_amd import _lib
+    from halo_amd.route import RouteTable
+
+    g = RouteTable(0)
+    ips = torch.zeros(8, dtype=torch.int32, device=dev)
+    rc = _lib.lib.halo_route_lookup_device(g._t, ips.data_ptr(), 8, ips.data_ptr(), None)
+    assert rc == _lib.HALO_E_INVAL  # not synced yet
+    assert _lib.lib.halo_route_get(g._t, 5, ctypes.c_void_p(ips.data_ptr())) == _lib.HALO_E_RANGE

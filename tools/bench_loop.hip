@@ -121,3 +121,11 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_xxh3_steps(
     };
     return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
 }
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_route_steps(
+    int nbatch, const halo_route_table_t* t, const uint32_t* const* ips, uint32_t n, uint32_t* out, int warmup,
+    int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0) return HALO_E_INVAL;
+    auto launch = [&](int k) { return halo_route_lookup_device(t, ips[k % nbatch], n, out, stream); };
+    return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
+}

@@ -23,6 +23,7 @@ for s in "$@"; do
     test)  step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
     ttx)   step pytest_tx 600 python -m pytest tests/test_gpu_tx.py -m gpu -q -rf -x ;;
     thash) step pytest_hash 600 python -m pytest tests/test_gpu_flow_hash.py -m gpu -q -rf -x ;;
+    troute) step pytest_route 600 python -m pytest tests/test_gpu_route.py -m gpu -q -rf -x ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py ;;
     benchq) step benchq 600 python bench.py --no-secondary --cpu-seconds 4 ;;
