@@ -7,9 +7,10 @@
 // lane each. Long strings (hashLong, :132-209) are the 8-accumulator stripe loop, which maps
 // onto 8 lanes: lane j of a group owns accumulator j, reads bytes [8j, 8j+8) of each 64-byte
 // stripe (the group's load is one coalesced 64-byte access) and gets input word j^1 from its
-// neighbour with a DPP quad_perm swap; the merge folds lane pairs the same way. A wave first
-// hashes its short strings lane-per-string, then takes its long strings eight at a time (one
-// per 8-lane group), so ragged batches keep every lane busy.
+// neighbour with a DPP quad_perm swap; the merge folds lane pairs the same way. Two kernels on
+// one stream: short strings lane-per-string, then long strings — each wave scans 64 strings and
+// takes its long ones eight at a time (one per 8-lane group), so ragged batches keep every lane
+// busy and neither path pays the other's register budget.
 //
 // Data are read as aligned dwords merged with v_alignbyte: any byte offset works, and no read
 // touches a dword that holds none of the string's bytes (so never a page the string is not on).
@@ -152,39 +153,75 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t v) {
 // 64-bit value of lane (lane ^ 1) within each quad (DPP quad_perm 1,0,3,2)
 __device__ __forceinline__ uint64_t swap_pair(uint64_t v) { return dpp64<0xB1>(v); }
 
-// accumulateStripe (xxh3.go:181-209) for accumulator j on lane j of the group
-__device__ __forceinline__ void stripe8(uint64_t& acc, const uint8_t* stripe, uint32_t sec_off, uint32_t j) {
-    const uint64_t in = ld64(stripe + 8 * j);
-    const uint64_t k = in ^ sec64(sec_off + 8 * j);
+// Secret words the long path needs, staged in LDS once per block: the 64-bit word at byte 8k
+// (k = 0..23: stripe secrets, k = 16 + j: scramble), at 121 + 8j (last stripe) and at 11 + 8j
+// (merge). Lane j of a group reads word st + j for stripe st: one ds_read_b64, no constant-cache
+// gathers.
+struct LongSecrets {
+    uint64_t w8[24];
+    uint64_t last[8];
+    uint64_t merge[8];
+};
+
+__device__ __forceinline__ void load_secrets(LongSecrets& s) {
+    const uint32_t t = threadIdx.x;
+    if (t < 24) s.w8[t] = sec64(8 * t);
+    else if (t < 32) s.last[t - 24] = sec64(121 + 8 * (t - 24));
+    else if (t < 40) s.merge[t - 32] = sec64(11 + 8 * (t - 32));
+}
+
+// accumulateStripe (xxh3.go:181-209) for accumulator j on lane j: `in` = input word j of the stripe
+__device__ __forceinline__ void stripe_acc(uint64_t& acc, uint64_t in, uint64_t secret) {
+    const uint64_t k = in ^ secret;
     acc += swap_pair(in) + (uint64_t)(uint32_t)k * (k >> 32);
 }
 
 // hashLong (xxh3.go:132-178) on a group of 8 lanes; lane j = accumulator j. Result in every lane.
-__device__ uint64_t hash_long8(const uint8_t* d, uint32_t len, uint32_t j) {
+// Stripe words are read as aligned dwords (three when the string is not 4-byte aligned) four
+// stripes at a time, so a lane has up to 12 loads in flight.
+__device__ uint64_t hash_long8(const uint8_t* d, uint32_t len, uint32_t j, const LongSecrets& sec) {
     constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
     uint64_t acc = kInit[0];
 #pragma unroll
     for (int q = 1; q < 8; ++q) acc = j == (uint32_t)q ? kInit[q] : acc;
-    const uint8_t* p = d;
-    uint32_t remaining = len;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(d);
+    const uint32_t sh = (uint32_t)(base & 3u);  // uniform per group
+    gdw* q0 = (gdw*)(base & ~(uintptr_t)3) + 2 * j;
+    auto word = [&](uint32_t stripe) -> uint64_t {  // input word j of stripe `stripe`
+        gdw* r = q0 + 16 * stripe;
+        const uint32_t w0 = r[0], w1 = r[1];
+        const uint32_t w2 = sh ? r[2] : 0u;
+        return join64(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh));
+    };
+    uint32_t stripe = 0, remaining = len;
     while (remaining > 1024) {
-        for (uint32_t st = 0; st < 16; ++st) {
-            stripe8(acc, p, 8 * st, j);
-            p += 64;
+#pragma unroll 1
+        for (uint32_t st = 0; st < 16; st += 4) {
+            uint64_t w[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w[u] = word(stripe + st + u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) stripe_acc(acc, w[u], sec.w8[st + u + j]);
         }
+        stripe += 16;
         remaining -= 1024;
         acc ^= acc >> 47;  // scramble (xxh3.go:212-218)
-        acc ^= sec64(128 + 8 * j);
+        acc ^= sec.w8[16 + j];
         acc *= P32_1;
     }
     const uint32_t stripes = (remaining - 1) / 64;
-    for (uint32_t st = 0; st < stripes; ++st) {
-        stripe8(acc, p, 8 * st, j);
-        p += 64;
+    uint32_t st = 0;
+    for (; st + 4 <= stripes; st += 4) {
+        uint64_t w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w[u] = word(stripe + st + u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) stripe_acc(acc, w[u], sec.w8[st + u + j]);
     }
-    stripe8(acc, d + len - 64, 121, j);  // the last (overlapping) stripe, secret offset 121
+    for (; st < stripes; ++st) stripe_acc(acc, word(stripe + st), sec.w8[st + j]);
+    stripe_acc(acc, ld64(d + len - 64 + 8 * j), sec.last[j]);  // last stripe, secret offset 121
     // merge (xxh3.go:139-145): pairs (2i, 2i+1) with secret 11 + 16i, then sum over the pairs
-    const uint64_t mine = acc ^ sec64(11 + 8 * j);
+    const uint64_t mine = acc ^ sec.merge[j];
     const uint64_t other = swap_pair(mine);
     uint64_t m = (j & 1u) ? 0ull : mul_fold64(mine, other);
     // sum lanes 0, 2, 4, 6 of the group (odd lanes hold 0): butterfly over the 8 lanes
@@ -202,19 +239,29 @@ struct XxhParams {
     uint64_t* out;
 };
 
-__global__ void __launch_bounds__(256) xxh3_batch_kernel(const XxhParams p) {
+// strings <= 240 B, one lane each (the long ones are left to xxh3_long_kernel)
+__global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += stride) {
+        const uint32_t len = p.lens[i];
+        if (len <= 240) p.out[i] = hash_short(p.bytes + p.offsets[i], len);
+    }
+}
+
+// strings > 240 B: each wave scans 64 strings and hashes its long ones eight at a time, one per
+// 8-lane group
+__global__ void __launch_bounds__(256) xxh3_long_kernel(const XxhParams p) {
+    __shared__ LongSecrets s_sec;
+    load_secrets(s_sec);
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = lane >> 3, j = lane & 7u;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t base = wave * 64; base < p.n; base += nwaves * 64) {
         const uint32_t i = base + lane;
-        const bool have = i < p.n;
-        const uint32_t len = have ? p.lens[i] : 0u;
-        const uint64_t off = have ? p.offsets[i] : 0ull;
-        if (have && len <= 240) p.out[i] = hash_short(p.bytes + off, len);
-        // long strings: eight at a time, one per 8-lane group
-        uint64_t pend = __ballot(have && len > 240);
-        const uint32_t g = lane >> 3, j = lane & 7u;
+        const uint32_t len = i < p.n ? p.lens[i] : 0u;
+        uint64_t pend = __ballot(len > 240);
         while (pend) {
             uint32_t owner = 64;  // lane whose string group g takes this round
 #pragma unroll
@@ -224,11 +271,10 @@ __global__ void __launch_bounds__(256) xxh3_batch_kernel(const XxhParams p) {
                 pend &= pend ? pend - 1 : 0ull;
             }
             const uint32_t src = owner < 64 ? owner : 0u;
-            const uint32_t o_lo = (uint32_t)__shfl((int)(uint32_t)off, (int)src, 64);
-            const uint32_t o_hi = (uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)src, 64);
             const uint32_t o_len = (uint32_t)__shfl((int)len, (int)src, 64);
             if (owner < 64) {  // uniform per group
-                const uint64_t h = hash_long8(p.bytes + join64(o_lo, o_hi), o_len, j);
+                const uint64_t off = p.offsets[base + owner];
+                const uint64_t h = hash_long8(p.bytes + off, o_len, j, s_sec);
                 if (j == 0) p.out[base + owner] = h;
             }
         }
@@ -285,8 +331,9 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
     int rc = halo::check_device();
     if (rc) return rc;
     halo::XxhParams p{d_bytes, d_offsets, d_lens, n, d_hash};
-    hipLaunchKernelGGL(halo::xxh3_batch_kernel, dim3(halo::blocks_for(n)), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), p);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(halo::xxh3_short_kernel, dim3(halo::blocks_for(n)), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(halo::xxh3_long_kernel, dim3(halo::blocks_for(n)), dim3(256), 0, s, p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 
