@@ -135,7 +135,7 @@ __device__ uint64_t hash_short(const uint8_t* d, uint32_t len) {
         return avalanche(acc);
     }
     // hashLarge (xxh3.go:116-129)
-#pragma unroll
+#pragma unroll 2
     for (uint32_t off = 0; off < 128; off += 16) acc += mix16(d, off, off);
     acc = avalanche(acc);
     for (uint32_t off = 128, top = len & ~15u; off < top; off += 16) acc += mix16(d, off, off - 125);
@@ -248,36 +248,44 @@ __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
     }
 }
 
-// strings > 240 B: each wave scans 64 strings and hashes its long ones eight at a time, one per
-// 8-lane group
+// strings > 240 B: each wave scans 64 strings, ranks its long ones by length (longest first) and
+// hashes them eight at a time, one per 8-lane group — rank order keeps the eight strings of a
+// round about equally long, so groups do not idle behind the round's longest string
 __global__ void __launch_bounds__(256) xxh3_long_kernel(const XxhParams p) {
     __shared__ LongSecrets s_sec;
+    __shared__ uint8_t s_order[4][64];  // per wave: lane holding the string of each rank
     load_secrets(s_sec);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = threadIdx.x >> 6;
     const uint32_t g = lane >> 3, j = lane & 7u;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t base = wave * 64; base < p.n; base += nwaves * 64) {
         const uint32_t i = base + lane;
-        const uint32_t len = i < p.n ? p.lens[i] : 0u;
-        uint64_t pend = __ballot(len > 240);
-        while (pend) {
-            uint32_t owner = 64;  // lane whose string group g takes this round
+        const uint32_t raw = i < p.n ? p.lens[i] : 0u;
+        const uint32_t len = raw > 240 ? raw : 0u;
+        const uint32_t nlong = (uint32_t)__popcll(__ballot(len != 0));
+        if (nlong == 0) continue;
+        // rank = number of lanes with a longer string, ties by lane
+        uint32_t rank = 0;
 #pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) {
-                const uint32_t b = pend ? (uint32_t)__builtin_ctzll(pend) : 64u;
-                owner = q == g ? b : owner;
-                pend &= pend ? pend - 1 : 0ull;
-            }
-            const uint32_t src = owner < 64 ? owner : 0u;
-            const uint32_t o_len = (uint32_t)__shfl((int)len, (int)src, 64);
-            if (owner < 64) {  // uniform per group
-                const uint64_t off = p.offsets[base + owner];
-                const uint64_t h = hash_long8(p.bytes + off, o_len, j, s_sec);
-                if (j == 0) p.out[base + owner] = h;
+        for (int k = 0; k < 64; ++k) {
+            const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
+            rank += (lk > len || (lk == len && (uint32_t)k < lane)) ? 1u : 0u;
+        }
+        if (len) s_order[w][rank] = (uint8_t)lane;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t r0 = 0; r0 < nlong; r0 += 8) {
+            const uint32_t rk = r0 + g;
+            if (rk < nlong) {  // uniform per group
+                const uint32_t owner = s_order[w][rk];
+                const uint32_t idx = base + owner;
+                const uint64_t h = hash_long8(p.bytes + p.offsets[idx], p.lens[idx], j, s_sec);
+                if (j == 0) p.out[idx] = h;
             }
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
