@@ -218,6 +218,20 @@ def time_tx_steps(batches, ops_dev, res_dev, *, flags, hint, steps, warmup, d: D
     return d.max(wall.value), region.value / steps
 
 
+def cpu_rate(fn, units: int, seconds: float, unit: str, sample: str):
+    """The oracle restatement of a row-f2..f4 function, one host thread, repeated for ~`seconds`."""
+    fn()  # warm
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(units * passes / el / 1e6, 3), "unit": unit, "cores": 1, "kind": "port",
+            "sample": f"{sample}; {passes} passes in {el:.1f}s, oracle/*.c -O2, one thread"}
+
+
 def time_native(fn, *args, steps, warmup, d: Dist):
     """One of the row-f3 native loops (halo_bench_flow_steps / halo_bench_xxh3_steps)."""
     import ctypes
@@ -236,7 +250,7 @@ def time_native(fn, *args, steps, warmup, d: Dist):
     return d.max(wall.value), region.value / steps
 
 
-def flow_hash_secondary(batches, out_records, netif, steps, warmup, d: Dist):
+def flow_hash_secondary(batches, out_records, netif, steps, warmup, d: Dist, with_cpu: bool = False):
     """§8f f3 on the headline frames: parse each rotating batch once, then hash every record's NAT
     flow key (NatWanFlowHash, symmetric NAT) with the hashmap bucket for a 2^20-entry table."""
     import ctypes
@@ -260,11 +274,17 @@ def flow_hash_secondary(batches, out_records, netif, steps, warmup, d: Dist):
     res = {"mpps": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 5),
            "roofline": roofline(alg, k, load_traffic("flow_hash_config2")), "alg_bytes_per_launch": alg,
            "what": "NatWanFlowHash (13 B key) XXH3-64 + hash % 2^20 per record"}
+    if with_cpu:
+        from oracle import oracle as O
+
+        host = protocol.records(recs[0])
+        res["cpu_baseline"] = cpu_rate(lambda: O.flow_hash_batch(host, 1, 0, 1 << 20), n, 2.0, "Mkeys/s",
+                                       f"{n} records of batch 0 (oracle/halo_xxh3_oracle.c)")
     del recs
     return res
 
 
-def xxh3_secondary(dev, steps, warmup, d: Dist):
+def xxh3_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
     """§8f f3, GetHashCodeXXH3 over KCP-segment-sized strings (24..1400 B, unaligned offsets)."""
     import ctypes
 
@@ -291,11 +311,20 @@ def xxh3_secondary(dev, steps, warmup, d: Dist):
     res = {"strings": n, "mstrings_per_s": round(n * steps / w / 1e6, 1),
            "gbytes_per_s": round(bs[0][3] * steps / w / 1e9, 1), "kernel_ms": round(k, 4),
            "roofline": roofline(alg, k, load_traffic("xxh3_kcp_1M")), "alg_bytes_per_launch": alg}
+    if with_cpu:
+        from oracle import oracle as O
+
+        m = 1 << 16
+        offs_h = bs[0][1][:m].cpu().numpy().view(np.uint64)
+        lens_h = bs[0][2][:m].cpu().numpy().view(np.uint32)
+        data_h = bs[0][0][:int(offs_h[-1]) + int(lens_h[-1])].cpu().numpy()
+        res["cpu_baseline"] = cpu_rate(lambda: O.xxh3_batch(data_h, offs_h, lens_h), m, 2.0, "Mstrings/s",
+                                       f"first {m} strings of batch 0 (oracle/halo_xxh3_oracle.c)")
     del bs
     return res
 
 
-def route_secondary(dev, steps, warmup, d: Dist):
+def route_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
     """§8f f4, FindRoute on the GPU: a 500k-prefix table (BGP-like length mix, 1 in 8 prefixes
     with a second ECMP next hop, a default route), 4M uniformly random destination addresses per
     launch, route id out."""
@@ -335,6 +364,19 @@ def route_secondary(dev, steps, warmup, d: Dist):
            "note": "alg bytes = address in + route id out; each lookup also reads 1-2 random 4 B table "
                    "entries (tbl24 stays resident in the 256 MB Infinity Cache)"}
     t.close()
+    if with_cpu:
+        from oracle import oracle as O
+
+        ot = O.RouteTable()
+        ot.add((0, 0, 0xC0A86401, 0))
+        for k in range(n_pfx):
+            ot.add((int(dst[k]), int(mask[k]), k + 2, k & 3))
+            if k % 8 == 0:
+                ot.add((int(dst[k]), int(mask[k]), k + 3, k & 3))
+        ips_h = bs[0][: 1 << 20].cpu().numpy().view(np.uint32)
+        res["cpu_baseline"] = cpu_rate(lambda: ot.find_batch(ips_h), 1 << 20, 2.0, "Mlookups/s",
+                                       "1M random addresses, the same table in the binary trie of "
+                                       "oracle/halo_route_oracle.c (the reference's structure)")
     del bs
     return res
 
@@ -506,13 +548,23 @@ def main():
             "mpps": round(n * args.steps / wt / 1e6, 1), "kernel_ms": round(kt, 5),
             "roofline": roofline(algt, kt, load_traffic("tx_config2")), "alg_bytes_per_launch": algt,
             "steps": "NatChangeDst + NatChangeSrc + eth_tx DPDK fill, per-frame addresses/ports"}
+        if not args.no_cpu:
+            from oracle import oracle as O
+
+            m = 1 << 18
+            lay0 = batches[0]["layout"]
+            host = batches[0]["bytes"][:int(lay0["offsets_dw"][m]) * 4].cpu().numpy()
+            sec["tx_fixup_config2_nat_dpdk"]["cpu_baseline"] = cpu_rate(
+                lambda: O.tx_batch(host, lay0["offsets_dw"][:m], lay0["lens"][:m], ops_h[:m], flags=1), m, 2.0, "Mpps",
+                f"{m} x 64B frames of batch 0, same ops (oracle/halo_tx_oracle.c)")
         del ops_d, res_d
-        sec["flow_hash_config2_nat_wan"] = flow_hash_secondary(batches, out, netif, args.steps, args.warmup, d)
+        sec["flow_hash_config2_nat_wan"] = flow_hash_secondary(batches, out, netif, args.steps, args.warmup, d,
+                                                               with_cpu=not args.no_cpu)
         del batches
         torch.cuda.empty_cache()
-        sec["xxh3_kcp_segments_1M"] = xxh3_secondary(dev, max(5, args.steps // 10), 2, d)
+        sec["xxh3_kcp_segments_1M"] = xxh3_secondary(dev, max(5, args.steps // 10), 2, d, with_cpu=not args.no_cpu)
         torch.cuda.empty_cache()
-        sec["route_lpm_500k_prefixes"] = route_secondary(dev, max(10, args.steps // 4), 3, d)
+        sec["route_lpm_500k_prefixes"] = route_secondary(dev, max(10, args.steps // 4), 3, d, with_cpu=not args.no_cpu)
         torch.cuda.empty_cache()
         for name, kw, hint, strided_len, flags in [
             ("1500B_udp_1M", dict(length=1500), 1500, 0, 1),
