@@ -1,0 +1,10 @@
+#!/bin/bash
+# Build an experimental libhalo_rx.so variant into tools/exp/libhalo_rx_<name>.so (tools only).
+# usage: tools/exp/build_variant.sh <name> [-DMACRO=1 ...]
+set -e
+cd "$(dirname "$0")/../.."
+name=$1; shift
+C=halo_amd/csrc
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fvisibility=hidden "$@" -Iinclude -I$C \
+  $C/rx_parse.hip $C/tx_fixup.hip $C/flow_hash.hip $C/route_lpm.hip $C/synth.hip $C/host_path.hip \
+  -o tools/exp/libhalo_rx_$name.so

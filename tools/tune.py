@@ -36,6 +36,9 @@ def main():
     ]
     if quick:
         workloads = workloads[:2] + workloads[3:5]
+    if "--only" in sys.argv:
+        keep = sys.argv[sys.argv.index("--only") + 1].split(",")
+        workloads = [w for w in workloads if w[0] in keep]
     res = {}
     for name, kw, n, rot, gs in workloads:
         bs = bench.make_batches(dev, netif, n=n, rotate=rot, rank=0, **kw)
