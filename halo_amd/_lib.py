@@ -87,6 +87,14 @@ FLOW_NAT_LAN, FLOW_NAT_WAN = 0, 1        # HALO_FLOW_*
 NAT_SYMMETRIC, NAT_FULL_CONE = 0, 1      # HALO_NAT_* (engine.NatTypeSymmetric / NatTypeFullCone)
 ROUTE_DTYPE = np.dtype([("dst_ip", "<u4"), ("network_mask", "<u4"), ("next_hop", "<u4"), ("netif", "<u4")])
 ROUTE_NONE, ROUTE_PANIC = 0xFFFFFFFF, 0xFFFFFFFE  # HALO_ROUTE_*
+# halo_rx_ring_scan_t (24 bytes) and HALO_RING_STOP_* / HALO_RING_REGISTER
+RING_SCAN_DTYPE = np.dtype([("n_frames", "<u4"), ("stop", "<u4"), ("end_bytes", "<u8"), ("max_len", "<u4"),
+                            ("pad", "<u4")])
+assert RING_SCAN_DTYPE.itemsize == 24
+RING_STOP_NAMES = ("EMPTY", "BAD_LEN", "PARTIAL", "CAPACITY", "MAX", "BAD_CURSOR")
+RING_STOP = {name: code for code, name in enumerate(RING_STOP_NAMES)}
+RING_REGISTER = 0x1
+RING_HEADER = 128  # sizeof(RingBuffer), mem/ring_buffer.go:18-26
 
 
 class NetIf(ctypes.Structure):
@@ -147,6 +155,23 @@ _PROTOS = {
     "halo_route_lookup_device": (ctypes.c_int, [ctypes.c_void_p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_route_lookup_records_device": (ctypes.c_int, [
         ctypes.c_void_p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
+    "halo_rx_shard_multi": (ctypes.c_int, [
+        _u8p, ctypes.c_uint32, _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p,
+        _u8p, _u8p]),
+    "halo_rx_ring_attach": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+        ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    "halo_rx_ring_detach": (ctypes.c_int, [ctypes.c_void_p]),
+    "halo_rx_ring_poll": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p, _u8p, _u8p]),
+    "halo_rx_ring_commit": (ctypes.c_int, [ctypes.c_void_p]),
+    "halo_rx_ring_scan_workspace": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32]),
+    "halo_rx_ring_scan_device": (ctypes.c_int, [
+        _u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, _u8p,
+        ctypes.c_uint64, ctypes.c_void_p]),
+    "halo_ring_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "halo_ring_write_batch": (ctypes.c_int, [
+        ctypes.c_void_p, _u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.POINTER(ctypes.c_uint32)]),
     "halo_synth_layout": (ctypes.c_int, [
         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint64)]),

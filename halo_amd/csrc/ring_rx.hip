@@ -1,0 +1,680 @@
+// ring_rx.hip — halo's SPSC packet ring as the source of a receive batch (SURVEY.md §8f row f1;
+// BASELINE config 1 drains exactly such a ring through engine.Wire).
+//
+// The reference drains the ring one record per call: ReadPacket (mem/ring_buffer.go:298-352, the
+// Go twin of cgo/ring_buffer.h:294-348) copies the next record into a reused 1514-byte buffer
+// (dpdk.EthQueueRxPkt, dpdk/dpdk.go:183-199; engine.Wire.Rx, engine/engine.go:535-545) and
+// PacketHandle parses it (engine/engine.go:339-351). Here a consumer takes everything between its
+// cursor and the producer's head in one poll: the span goes to HBM raw (one DMA, two around the
+// wrap), the GPU finds the record boundaries, the rx kernel (rx_parse.hip) parses the frames where
+// they lie, and the records come back in one copy. The host reads `head`, writes `tail`, and never
+// touches a frame byte.
+//
+// Record boundaries on the GPU. Walking records is a chain: the record whose length field is span
+// dword a continues at a + ceil((4 + len) / 4) (u32 length + bytes, 4-byte aligned:
+// mem/ring_buffer.go:47-50) unless ReadPacket would return false there. It is resolved in parallel:
+//   1. tile maps   — the span is cut into 4096-dword tiles. For EVERY dword position of a tile,
+//                    12 rounds of pointer jumping in LDS find where a walk starting there leaves the
+//                    tile (or stops) and how many records it takes. A walk can only enter a tile at
+//                    one of its first W positions (W = dwords of the longest record the receive
+//                    buffer accepts), so those W results are the tile's map.
+//   2. superblocks — the maps of S consecutive tiles are composed (S x W entries staged in LDS).
+//   3. chain       — one workgroup runs the superblock maps from the span's start: the entry and
+//                    the number of records before every superblock.
+//   4. emit        — every tile follows at most S-1 tile maps from its superblock's entry to its
+//                    own, then walks its own records in LDS and writes (dword offset, length).
+// Every step applies ReadPacket's checks in ReadPacket's order, so the frames taken, the stop and
+// the new tail are those of repeated ReadPacket calls (tests/test_gpu_ring.py, against the oracle,
+// which tests/test_ring_oracle.py checks against the reference's own cgo/ring_buffer.h).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "halo_common.h"
+
+namespace halo {
+namespace {
+
+constexpr uint32_t kTile = 4096;                 // span dwords per tile (16 KB)
+constexpr uint32_t kThreads = 256;
+constexpr uint32_t kJumpRounds = 12;             // a walk inside a tile takes <= kTile/2 = 2^11 records
+constexpr uint32_t kLdsStop = 0x8000u;           // jump-table target: the walk stops inside the tile
+constexpr uint32_t kMapStop = 0xFFFFFFFFu;       // tile / superblock map entry: the walk stops
+constexpr uint32_t kMapLds = 8192;               // map entries (uint2) staged in LDS: 64 KB
+constexpr uint32_t kMaxCapacity = 4 * kTile - 8; // the longest record must fit a tile's entry window
+constexpr uint32_t kRbHeader = 128;              // sizeof(RingBuffer), mem/ring_buffer.go:18-26
+constexpr uint64_t kMaxSpan = (16ull << 30) - (64ull << 10);  // dword offsets stay below 2^32
+constexpr uint64_t kPieceBytes = 16ull << 20;    // DMA piece (1024 tiles) whose maps start on arrival
+constexpr uint32_t kParseChunk = 1u << 20;       // frames per parse launch / record copy
+
+struct Scan {
+    const uint32_t* span;   // the ring bytes [tail, tail + used) in stream order, as dwords
+    uint32_t n_dw;          // used / 4
+    uint32_t n_tiles;
+    uint32_t cap;           // receive buffer capacity: len(data) of ReadPacket
+    uint32_t W;             // entry window: dwords of the longest acceptable record
+    uint32_t S;             // tiles per superblock
+    uint32_t n_sb;
+    uint32_t max_frames;
+    uint64_t half;          // RingBuffer.size / 2
+    uint2* tile_map;        // [n_tiles][W]: (entry into the next tile | kMapStop, records taken)
+    uint2* sb_map;          // [n_sb][W]
+    uint2* sb_entry;        // [n_sb]: (entry | kMapStop, records before the superblock)
+    uint32_t* total;        // records the walk takes before it stops (max_frames ignored)
+    halo_rx_ring_scan_t* info;
+    uint32_t* off_dw;       // frame i's bytes start at span dword off_dw[i]
+    uint16_t* lens;
+};
+
+// Dwords of the record whose length field is span dword a (value `len`), or 0 where ReadPacket
+// returns false, with the reason: the checks of mem/ring_buffer.go:309-335, in that order.
+__device__ __forceinline__ uint32_t record_dwords(const Scan& s, uint32_t a, uint32_t len, uint32_t& why) {
+    if (a >= s.n_dw) { why = HALO_RING_STOP_EMPTY; return 0; }                                  // usedSpace < 4
+    if (len == 0 || (uint64_t)len > s.half) { why = HALO_RING_STOP_BAD_LEN; return 0; }
+    const uint64_t bytes = (4ull + len + 3ull) & ~3ull;                                         // ringBufferRecordSize
+    if ((uint64_t)(s.n_dw - a) * 4ull < bytes) { why = HALO_RING_STOP_PARTIAL; return 0; }      // usedSpace < totalSize
+    if (len > s.cap) { why = HALO_RING_STOP_CAPACITY; return 0; }                              // len(data) < packetLen
+    return (uint32_t)(bytes >> 2);
+}
+
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// Span dwords of tile t into LDS (16-byte loads inside the span), zero past its end.
+__device__ __forceinline__ void load_tile(const Scan& s, uint32_t t, uint32_t* dw) {
+    const uint32_t base = t * kTile;
+    for (uint32_t q = 4 * threadIdx.x; q < kTile; q += 4 * kThreads) {
+        const uint32_t a = base + q;
+        uint4 v;
+        if (a + 4 <= s.n_dw) {
+            const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + a);
+            v = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            v.x = a < s.n_dw ? s.span[a] : 0u;
+            v.y = a + 1 < s.n_dw ? s.span[a + 1] : 0u;
+            v.z = a + 2 < s.n_dw ? s.span[a + 2] : 0u;
+            v.w = a + 3 < s.n_dw ? s.span[a + 3] : 0u;
+        }
+        *reinterpret_cast<uint4*>(dw + q) = v;
+    }
+}
+
+// 1. Tile maps for tiles [tile0, tile0 + gridDim.x). Jump-table entry: bits 0-15 target position
+// (< kTile: inside the tile; kTile..2*kTile-1: the next tile's position + kTile; kLdsStop: the
+// walk stops), bits 16-31 records taken on the way.
+__global__ void __launch_bounds__(kThreads) ring_tile_map_kernel(const Scan s, uint32_t tile0) {
+    __shared__ __align__(16) uint32_t jt[2][kTile];
+    const uint32_t t = tile0 + blockIdx.x;
+    load_tile(s, t, jt[1]);
+    __syncthreads();
+    const uint32_t base = t * kTile;
+    for (uint32_t q = threadIdx.x; q < kTile; q += kThreads) {
+        uint32_t why;
+        const uint32_t step = record_dwords(s, base + q, jt[1][q], why);
+        jt[0][q] = step ? ((q + step) | (1u << 16)) : kLdsStop;
+    }
+    __syncthreads();
+    uint32_t cur = 0;
+    for (uint32_t r = 0; r < kJumpRounds; ++r) {
+        for (uint32_t q = threadIdx.x; q < kTile; q += kThreads) {
+            const uint32_t v = jt[cur][q];
+            const uint32_t tg = v & 0xFFFFu;
+            uint32_t nv = v;
+            if (tg < kTile) {
+                const uint32_t w = jt[cur][tg];
+                nv = (w & 0xFFFFu) | ((v & 0xFFFF0000u) + (w & 0xFFFF0000u));
+            }
+            jt[cur ^ 1][q] = nv;
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    uint2* out = s.tile_map + (uint64_t)t * s.W;
+    for (uint32_t e = threadIdx.x; e < s.W; e += kThreads) {
+        const uint32_t v = jt[cur][e];
+        const uint32_t tg = v & 0xFFFFu;
+        out[e] = make_uint2((tg & kLdsStop) ? kMapStop : tg - kTile, v >> 16);
+    }
+}
+
+// 2. Compose the maps of superblock blockIdx.x's tiles.
+__global__ void __launch_bounds__(kThreads) ring_sb_compose_kernel(const Scan s) {
+    __shared__ uint2 m[kMapLds];
+    const uint32_t sb = blockIdx.x;
+    const uint32_t t0 = sb * s.S;
+    const uint32_t nt = min(s.S, s.n_tiles - t0);
+    const uint2* src = s.tile_map + (uint64_t)t0 * s.W;
+    for (uint32_t k = threadIdx.x; k < nt * s.W; k += kThreads) m[k] = src[k];
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < s.W; e += kThreads) {
+        uint32_t cur = e, taken = 0;
+        for (uint32_t k = 0; k < nt && cur != kMapStop; ++k) {
+            const uint2 v = m[k * s.W + cur];
+            taken += v.y;
+            cur = v.x;
+        }
+        s.sb_map[(uint64_t)sb * s.W + e] = make_uint2(cur, taken);
+    }
+}
+
+// 3. Chain the superblocks from the span's start (one workgroup; maps staged in LDS in chunks).
+__global__ void __launch_bounds__(kThreads) ring_chain_kernel(const Scan s) {
+    __shared__ uint2 m[kMapLds];
+    const uint32_t per = kMapLds / s.W;
+    uint32_t entry = 0, taken = 0;  // thread 0's walk
+    for (uint32_t c0 = 0; c0 < s.n_sb; c0 += per) {
+        const uint32_t nc = min(per, s.n_sb - c0);
+        __syncthreads();
+        const uint2* src = s.sb_map + (uint64_t)c0 * s.W;
+        for (uint32_t k = threadIdx.x; k < nc * s.W; k += kThreads) m[k] = src[k];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (uint32_t k = 0; k < nc; ++k) {
+                s.sb_entry[c0 + k] = make_uint2(entry, taken);
+                if (entry != kMapStop) {
+                    const uint2 v = m[k * s.W + entry];
+                    taken += v.y;
+                    entry = v.x;
+                }
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t n = min(taken, s.max_frames);
+        *s.total = taken;
+        halo_rx_ring_scan_t info;
+        info.n_frames = n;
+        info.stop = n < taken ? HALO_RING_STOP_MAX : HALO_RING_STOP_EMPTY;  // a tile refines EMPTY
+        info.end_bytes = 0;
+        info.max_len = 0;
+        info.pad = 0;
+        *s.info = info;
+    }
+}
+
+// 4. Tile blockIdx.x: its entry, then its records.
+__global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
+    __shared__ __align__(16) uint32_t dw[kTile];
+    __shared__ uint32_t r_off[kTile / 2];
+    __shared__ uint16_t r_len[kTile / 2];
+    __shared__ uint32_t s_entry, s_base, s_cnt;
+    const uint32_t t = blockIdx.x;
+    const uint32_t n = s.info->n_frames;
+    if (threadIdx.x == 0) {
+        const uint32_t sb = t / s.S;
+        const uint2 e = s.sb_entry[sb];
+        uint32_t entry = e.x, base = e.y;
+        for (uint32_t k = sb * s.S; k < t && entry != kMapStop && base <= n; ++k) {
+            const uint2 v = s.tile_map[(uint64_t)k * s.W + entry];
+            base += v.y;
+            entry = v.x;
+        }
+        s_entry = entry;
+        s_base = base;
+    }
+    __syncthreads();
+    const uint32_t entry = s_entry, base = s_base;
+    if (entry == kMapStop || base > n) return;
+    load_tile(s, t, dw);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t total = *s.total;
+        uint32_t q = entry, k = base, c = 0, max_len = 0;
+        while (q < kTile) {
+            uint32_t why = HALO_RING_STOP_EMPTY;
+            const uint32_t step = record_dwords(s, t * kTile + q, dw[q], why);
+            if (k == n || !step) {
+                // the walk ends at this record: say why, unless max_frames cut it (MAX, set)
+                if (!step && n == total) s.info->stop = why;
+                break;
+            }
+            r_off[c] = t * kTile + q + 1;
+            r_len[c] = (uint16_t)dw[q];
+            max_len = max(max_len, dw[q]);
+            ++c;
+            ++k;
+            q += step;
+            if (k == n) s.info->end_bytes = 4ull * (t * kTile + q);
+        }
+        s_cnt = c;
+        if (max_len) atomicMax(&s.info->max_len, max_len);
+    }
+    __syncthreads();
+    const uint32_t c = s_cnt;
+    for (uint32_t j = threadIdx.x; j < c; j += kThreads) {
+        s.off_dw[base + j] = r_off[j];
+        s.lens[base + j] = r_len[j];
+    }
+}
+
+struct Geom {
+    uint32_t n_dw, n_tiles, W, S, n_sb;
+    uint64_t tile_map_off, sb_map_off, sb_entry_off, total_off, bytes;
+};
+
+Geom geometry(uint64_t used, uint32_t cap) {
+    Geom g{};
+    g.n_dw = (uint32_t)(used >> 2);
+    g.n_tiles = std::max<uint32_t>(1, (g.n_dw + kTile - 1) / kTile);
+    g.W = (cap + 7) / 4;  // ceil((4 + cap) / 4)
+    g.S = std::max<uint32_t>(1, kMapLds / g.W);
+    g.n_sb = (g.n_tiles + g.S - 1) / g.S;
+    uint64_t o = 0;
+    g.tile_map_off = o;
+    o += (uint64_t)g.n_tiles * g.W * sizeof(uint2);
+    g.sb_map_off = o;
+    o += (uint64_t)g.n_sb * g.W * sizeof(uint2);
+    g.sb_entry_off = o;
+    o += (uint64_t)g.n_sb * sizeof(uint2);
+    g.total_off = o;
+    o += 256;
+    g.bytes = o;
+    return g;
+}
+
+Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_t cap, uint32_t max_frames,
+               uint8_t* ws, halo_rx_ring_scan_t* d_info, uint32_t* d_off, uint16_t* d_len) {
+    Scan s{};
+    s.span = reinterpret_cast<const uint32_t*>(d_span);
+    s.n_dw = g.n_dw;
+    s.n_tiles = g.n_tiles;
+    s.cap = cap;
+    s.W = g.W;
+    s.S = g.S;
+    s.n_sb = g.n_sb;
+    s.max_frames = max_frames ? max_frames : 0xFFFFFFFFu;
+    s.half = ring_size / 2;
+    s.tile_map = reinterpret_cast<uint2*>(ws + g.tile_map_off);
+    s.sb_map = reinterpret_cast<uint2*>(ws + g.sb_map_off);
+    s.sb_entry = reinterpret_cast<uint2*>(ws + g.sb_entry_off);
+    s.total = reinterpret_cast<uint32_t*>(ws + g.total_off);
+    s.info = d_info;
+    s.off_dw = d_off;
+    s.lens = d_len;
+    return s;
+}
+
+int launch_tile_maps(const Scan& s, uint32_t t0, uint32_t t1, hipStream_t st) {
+    if (t1 > t0) hipLaunchKernelGGL(ring_tile_map_kernel, dim3(t1 - t0), dim3(kThreads), 0, st, s, t0);
+    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+
+int launch_finish(const Scan& s, hipStream_t st) {
+    hipLaunchKernelGGL(ring_sb_compose_kernel, dim3(s.n_sb), dim3(kThreads), 0, st, s);
+    hipLaunchKernelGGL(ring_chain_kernel, dim3(1), dim3(kThreads), 0, st, s);
+    hipLaunchKernelGGL(ring_emit_kernel, dim3(s.n_tiles), dim3(kThreads), 0, st, s);
+    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+
+bool pow2(uint64_t x) { return x >= 8 && (x & (x - 1)) == 0; }
+
+// ring_buffer_mapping + ring_buffer_consumer_init (cgo/ring_buffer.h:158-204, :228-246).
+int validate_ring(const uint8_t* mem, int64_t offset, uint64_t* size, uint64_t* tail) {
+    if (!mem || (reinterpret_cast<uintptr_t>(mem) & 7u)) return HALO_E_INVAL;
+    if (mem[8] != 1) return HALO_E_INVAL;  // layout version
+    for (int i = 9; i <= 63; ++i)
+        if (mem[i] != 0xAA) return HALO_E_INVAL;
+    for (int i = 96; i <= 127; ++i)
+        if (mem[i] != 0xFF) return HALO_E_INVAL;
+    uint64_t sz, mask, stored;
+    memcpy(&sz, mem + 72, 8);
+    memcpy(&mask, mem + 80, 8);
+    memcpy(&stored, mem + 88, 8);
+    if (!stored || !pow2(sz) || sz > (1ull << 62) || mask != sz - 1) return HALO_E_INVAL;
+    const uint64_t t = __atomic_load_n(reinterpret_cast<const uint64_t*>(mem + 64), __ATOMIC_ACQUIRE);
+    const uint64_t h = __atomic_load_n(reinterpret_cast<const uint64_t*>(mem), __ATOMIC_ACQUIRE);
+    if (h - t > sz) return HALO_E_INVAL;
+    // ring_buffer_local_data: the caller's offset must match this mapping
+    const uint64_t local = reinterpret_cast<uintptr_t>(mem + kRbHeader);
+    if ((int64_t)(local - stored) != offset) return HALO_E_INVAL;
+    *size = sz;
+    *tail = t;
+    return HALO_OK;
+}
+
+}  // namespace
+}  // namespace halo
+
+using halo::Geom;
+using halo::Scan;
+
+struct halo_rx_ring {
+    int device = 0;
+    uint8_t* mem = nullptr;   // the RingBuffer header; the data area follows
+    uint8_t* data = nullptr;
+    uint64_t size = 0;
+    uint64_t cursor = 0;      // stream position after the frames polled so far
+    uint32_t cap = 0, max_frames = 0;
+    uint64_t max_bytes = 0;
+    bool registered = false;
+    Geom g{};                 // workspace geometry for max_bytes
+    hipStream_t s_copy = nullptr, s_comp = nullptr;
+    std::vector<hipEvent_t> ev;
+    uint8_t* d_span = nullptr;
+    uint8_t* d_ws = nullptr;
+    uint32_t* d_off = nullptr;
+    uint16_t* d_len = nullptr;
+    halo_rx_result_t* d_res = nullptr;
+    uint32_t* d_hist = nullptr;
+    halo_rx_ring_scan_t* d_info = nullptr;
+    halo_rx_ring_scan_t* h_info = nullptr;  // pinned
+    uint32_t* h_off = nullptr;              // pinned
+};
+
+namespace {
+void free_ring(halo_rx_ring* r) {
+    for (hipEvent_t e : r->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (r->s_copy) (void)hipStreamDestroy(r->s_copy);
+    if (r->s_comp) (void)hipStreamDestroy(r->s_comp);
+    if (r->d_span) (void)hipFree(r->d_span);
+    if (r->d_ws) (void)hipFree(r->d_ws);
+    if (r->d_off) (void)hipFree(r->d_off);
+    if (r->d_len) (void)hipFree(r->d_len);
+    if (r->d_res) (void)hipFree(r->d_res);
+    if (r->d_hist) (void)hipFree(r->d_hist);
+    if (r->d_info) (void)hipFree(r->d_info);
+    if (r->h_info) (void)hipHostFree(r->h_info);
+    if (r->h_off) (void)hipHostFree(r->h_off);
+    if (r->registered) (void)hipHostUnregister(r->mem);
+    delete r;
+}
+}  // namespace
+
+extern "C" HALO_API uint64_t halo_rx_ring_scan_workspace(uint64_t used, uint32_t capacity) {
+    if (capacity == 0) capacity = halo::kEthMax;
+    if (capacity > halo::kMaxCapacity || used > halo::kMaxSpan) return 0;
+    return halo::geometry(used, capacity).bytes;
+}
+
+extern "C" HALO_API int halo_rx_ring_scan_device(const uint8_t* d_span, uint64_t used, uint64_t ring_size,
+                                                 uint32_t capacity, uint32_t max_frames, uint32_t* d_offsets_dw,
+                                                 uint16_t* d_lens, halo_rx_ring_scan_t* d_info, void* d_workspace,
+                                                 uint64_t workspace_bytes, halo_stream_t stream) {
+    if (!d_info) return HALO_E_INVAL;
+    if (capacity == 0) capacity = halo::kEthMax;
+    if (capacity > halo::kMaxCapacity || !halo::pow2(ring_size)) return HALO_E_INVAL;
+    if ((used & 3u) || used > ring_size || used > halo::kMaxSpan) return HALO_E_INVAL;
+    const Geom g = halo::geometry(used, capacity);
+    if (used && (!d_span || !d_offsets_dw || !d_lens || (reinterpret_cast<uintptr_t>(d_span) & 3u) ||
+                 !d_workspace || workspace_bytes < g.bytes))
+        return HALO_E_INVAL;
+    int rc = halo::check_device();
+    if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (used == 0)
+        return hipMemsetAsync(d_info, 0, sizeof(halo_rx_ring_scan_t), st) == hipSuccess ? HALO_OK : HALO_E_HIP;
+    const Scan s = halo::make_scan(g, d_span, ring_size, capacity, max_frames, static_cast<uint8_t*>(d_workspace),
+                                   d_info, d_offsets_dw, d_lens);
+    if ((rc = halo::launch_tile_maps(s, 0, g.n_tiles, st))) return rc;
+    return halo::launch_finish(s, st);
+}
+
+extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t offset, uint32_t capacity,
+                                            uint64_t max_bytes, uint32_t max_frames, uint32_t attach_flags,
+                                            halo_rx_ring_t** out) {
+    if (!out) return HALO_E_INVAL;
+    *out = nullptr;
+    uint64_t size = 0, tail = 0;
+    uint8_t* mem = static_cast<uint8_t*>(ring_mem);
+    int rc = halo::validate_ring(mem, offset, &size, &tail);
+    if (rc) return rc;
+    if (attach_flags & ~HALO_RING_REGISTER) return HALO_E_INVAL;
+    if (capacity == 0) capacity = halo::kEthMax;
+    if (capacity > halo::kMaxCapacity) return HALO_E_INVAL;
+    if (max_bytes == 0) max_bytes = std::min<uint64_t>(size, 256ull << 20);
+    max_bytes = std::min<uint64_t>(std::min<uint64_t>(max_bytes, size), halo::kMaxSpan) & ~3ull;
+    if (max_bytes < 8) return HALO_E_INVAL;
+    if (max_frames == 0 || max_frames > max_bytes / 8) max_frames = (uint32_t)std::min<uint64_t>(max_bytes / 8, 0xFFFFFFFFull);
+    if ((rc = halo_rx_init(device))) return rc;
+    auto* r = new (std::nothrow) halo_rx_ring;
+    if (!r) return HALO_E_NOMEM;
+    r->device = device;
+    r->mem = mem;
+    r->data = mem + halo::kRbHeader;
+    r->size = size;
+    r->cursor = tail;
+    r->cap = capacity;
+    r->max_frames = max_frames;
+    r->max_bytes = max_bytes;
+    r->g = halo::geometry(max_bytes, capacity);
+    const size_t n_ev = (size_t)((max_bytes + halo::kPieceBytes - 1) / halo::kPieceBytes) +
+                        (max_frames + halo::kParseChunk - 1) / halo::kParseChunk;
+    r->ev.assign(n_ev, nullptr);
+    bool ok = hipStreamCreateWithFlags(&r->s_copy, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&r->s_comp, hipStreamNonBlocking) == hipSuccess;
+    for (auto& e : r->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipMalloc((void**)&r->d_span, max_bytes + 16) == hipSuccess;
+    ok = ok && hipMalloc((void**)&r->d_ws, r->g.bytes) == hipSuccess;
+    ok = ok && hipMalloc((void**)&r->d_off, 4ull * max_frames) == hipSuccess;
+    ok = ok && hipMalloc((void**)&r->d_len, 2ull * max_frames) == hipSuccess;
+    ok = ok && hipMalloc((void**)&r->d_res, sizeof(halo_rx_result_t) * (uint64_t)max_frames) == hipSuccess;
+    ok = ok && hipMalloc((void**)&r->d_hist, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
+    ok = ok && hipMemset(r->d_hist, 0, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
+    ok = ok && hipMalloc((void**)&r->d_info, sizeof(halo_rx_ring_scan_t)) == hipSuccess;
+    ok = ok && hipHostMalloc((void**)&r->h_info, sizeof(halo_rx_ring_scan_t), hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipHostMalloc((void**)&r->h_off, 4ull * max_frames, hipHostMallocDefault) == hipSuccess;
+    if (ok && (attach_flags & HALO_RING_REGISTER)) {
+        ok = hipHostRegister(mem, halo::kRbHeader + size, hipHostRegisterDefault) == hipSuccess;
+        r->registered = ok;
+    }
+    if (!ok) {
+        free_ring(r);
+        return HALO_E_NOMEM;
+    }
+    *out = r;
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_ring_detach(halo_rx_ring_t* r) {
+    if (!r) return HALO_E_INVAL;
+    (void)hipSetDevice(r->device);
+    if (r->s_copy) (void)hipStreamSynchronize(r->s_copy);
+    if (r->s_comp) (void)hipStreamSynchronize(r->s_comp);
+    free_ring(r);
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, const halo_rx_netif_t* netif,
+                                          halo_rx_result_t* out, uint32_t* status_hist, uint64_t* positions,
+                                          halo_rx_ring_scan_t* info) {
+    if (!r || !netif || !out || !info) return HALO_E_INVAL;
+    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT)) return HALO_E_INVAL;
+    if (hipSetDevice(r->device) != hipSuccess) return HALO_E_NODEV;
+    memset(info, 0, sizeof *info);
+    const uint64_t head = __atomic_load_n(reinterpret_cast<const uint64_t*>(r->mem), __ATOMIC_ACQUIRE);
+    uint64_t used = head - r->cursor;
+    if (used > r->size) {  // ReadPacket: usedSpace > size -> false
+        info->stop = HALO_RING_STOP_BAD_CURSOR;
+        return HALO_OK;
+    }
+    used = std::min(used, r->max_bytes) & ~3ull;
+    if (used == 0) return HALO_OK;  // EMPTY
+    const Geom g = halo::geometry(used, r->cap);
+    const Scan s = halo::make_scan(g, r->d_span, r->size, r->cap, r->max_frames, r->d_ws, r->d_info, r->d_off,
+                                   r->d_len);
+    // DMA the span piece by piece; each piece's tile maps start as soon as it has landed
+    const uint64_t mask = r->size - 1, pos = r->cursor & mask;
+    uint32_t tiles_done = 0;
+    size_t k = 0;
+    int rc = HALO_OK;
+    for (uint64_t b0 = 0; b0 < used && rc == HALO_OK; b0 += halo::kPieceBytes, ++k) {
+        const uint64_t b1 = std::min(used, b0 + halo::kPieceBytes);
+        uint64_t src = (pos + b0) & mask, len = b1 - b0, dst = b0;
+        while (len && rc == HALO_OK) {  // at most two pieces: up to the end of the data area, then from 0
+            const uint64_t c = std::min(len, r->size - src);
+            if (hipMemcpyAsync(r->d_span + dst, r->data + src, c, hipMemcpyHostToDevice, r->s_copy) != hipSuccess)
+                rc = HALO_E_HIP;
+            dst += c;
+            len -= c;
+            src = 0;
+        }
+        if (rc) break;
+        if (hipEventRecord(r->ev[k], r->s_copy) != hipSuccess || hipStreamWaitEvent(r->s_comp, r->ev[k], 0) != hipSuccess)
+            rc = HALO_E_HIP;
+        const uint32_t t1 = b1 == used ? g.n_tiles : (uint32_t)(b1 / (4ull * halo::kTile));
+        if (!rc) rc = halo::launch_tile_maps(s, tiles_done, t1, r->s_comp);
+        tiles_done = t1;
+    }
+    if (!rc) rc = halo::launch_finish(s, r->s_comp);
+    if (!rc && hipMemcpyAsync(r->h_info, r->d_info, sizeof *info, hipMemcpyDeviceToHost, r->s_comp) != hipSuccess)
+        rc = HALO_E_HIP;
+    if (hipStreamSynchronize(r->s_comp) != hipSuccess && !rc) rc = HALO_E_HIP;
+    if (rc) {
+        (void)hipStreamSynchronize(r->s_copy);
+        return rc;
+    }
+    *info = *r->h_info;
+    const uint32_t n = info->n_frames;
+    // parse the frames where they lie; the records of chunk c copy back while chunk c+1 parses
+    for (uint32_t f0 = 0; f0 < n && rc == HALO_OK; f0 += halo::kParseChunk, ++k) {
+        const uint32_t cnt = std::min(halo::kParseChunk, n - f0);
+        rc = halo_rx_parse_batch_device(r->d_span, r->d_off + f0, r->d_len + f0, cnt, flags, netif, info->max_len,
+                                        r->d_res + f0, status_hist ? r->d_hist : nullptr, r->s_comp);
+        if (rc) break;
+        if (hipEventRecord(r->ev[k], r->s_comp) != hipSuccess || hipStreamWaitEvent(r->s_copy, r->ev[k], 0) != hipSuccess ||
+            hipMemcpyAsync(out + f0, r->d_res + f0, sizeof(halo_rx_result_t) * cnt, hipMemcpyDeviceToHost,
+                           r->s_copy) != hipSuccess)
+            rc = HALO_E_HIP;
+    }
+    if (!rc && positions && n &&
+        hipMemcpyAsync(r->h_off, r->d_off, 4ull * n, hipMemcpyDeviceToHost, r->s_copy) != hipSuccess)
+        rc = HALO_E_HIP;
+    if (hipStreamSynchronize(r->s_copy) != hipSuccess && !rc) rc = HALO_E_HIP;
+    if (hipStreamSynchronize(r->s_comp) != hipSuccess && !rc) rc = HALO_E_HIP;
+    if (rc) return rc;
+    if (positions)
+        for (uint32_t i = 0; i < n; ++i) positions[i] = r->cursor + 4ull * (r->h_off[i] - 1u);
+    if (status_hist && n) {
+        uint32_t h[HALO_RX_STATUS_COUNT];
+        if (hipMemcpy(h, r->d_hist, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemset(r->d_hist, 0, sizeof h) != hipSuccess)
+            return HALO_E_HIP;
+        for (int j = 0; j < HALO_RX_STATUS_COUNT; ++j) status_hist[j] += h[j];
+    }
+    r->cursor += info->end_bytes;
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_ring_commit(halo_rx_ring_t* r) {
+    if (!r) return HALO_E_INVAL;
+    __atomic_store_n(reinterpret_cast<uint64_t*>(r->mem + 64), r->cursor, __ATOMIC_RELEASE);
+    return HALO_OK;
+}
+
+// ---- producer side (engine.NewWire / Wire.Tx) ------------------------------------------------
+extern "C" HALO_API int halo_ring_create(void* memory, uint64_t bytes) {
+    uint8_t* m = static_cast<uint8_t*>(memory);
+    if (!m || (reinterpret_cast<uintptr_t>(m) & 63u) || bytes < halo::kRbHeader + 8) return HALO_E_INVAL;
+    const uint64_t size = bytes - halo::kRbHeader;
+    if (!halo::pow2(size) || size > (1ull << 62)) return HALO_E_INVAL;
+    memset(m, 0, halo::kRbHeader);
+    const uint64_t mask = size - 1;
+    const uintptr_t buffer = reinterpret_cast<uintptr_t>(m + halo::kRbHeader);
+    memcpy(m + 72, &size, 8);
+    memcpy(m + 80, &mask, 8);
+    memcpy(m + 88, &buffer, 8);
+    m[8] = 1;  // layout version
+    memset(m + 9, 0xAA, 55);
+    memset(m + 96, 0xFF, 32);
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_ring_write_batch(void* memory, const uint8_t* bytes, const uint64_t* offsets,
+                                              const uint16_t* lens, uint32_t n, uint8_t* accepted,
+                                              uint32_t* written) {
+    uint64_t size = 0, tail_unused = 0;
+    uint8_t* m = static_cast<uint8_t*>(memory);
+    if (!m) return HALO_E_INVAL;
+    uint64_t stored;
+    memcpy(&stored, m + 88, 8);
+    int rc = halo::validate_ring(m, (int64_t)(reinterpret_cast<uintptr_t>(m + halo::kRbHeader) - stored), &size,
+                                 &tail_unused);
+    if (rc) return rc;
+    if (n && (!bytes || !offsets || !lens)) return HALO_E_INVAL;
+    uint64_t* head_p = reinterpret_cast<uint64_t*>(m);
+    const uint64_t* tail_p = reinterpret_cast<const uint64_t*>(m + 64);
+    uint8_t* data = m + halo::kRbHeader;
+    const uint64_t mask = size - 1;
+    uint64_t head = __atomic_load_n(head_p, __ATOMIC_RELAXED);  // this process is the producer
+    uint64_t cached_tail = __atomic_load_n(tail_p, __ATOMIC_ACQUIRE);
+    uint32_t count = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t len = lens[i];
+        bool ok = len != 0 && (uint64_t)len <= size / 2;
+        const uint64_t total = (4ull + len + 3ull) & ~3ull;
+        if (ok) {  // WritePacket's space check, re-reading the tail only when short
+            uint64_t used = head - cached_tail;
+            if (used > size || size - used < total) {
+                cached_tail = __atomic_load_n(tail_p, __ATOMIC_ACQUIRE);
+                used = head - cached_tail;
+                ok = used <= size && size - used >= total;
+            }
+        }
+        if (ok) {
+            const uint64_t pos = head & mask;
+            memcpy(data + pos, &len, 4);
+            const uint64_t dpos = (pos + 4) & mask, after = size - dpos;
+            const uint8_t* src = bytes + offsets[i];
+            if (after >= len) {
+                memcpy(data + dpos, src, len);
+            } else {
+                memcpy(data + dpos, src, after);
+                memcpy(data, src + after, len - after);
+            }
+            head += total;
+            __atomic_store_n(head_p, head, __ATOMIC_RELEASE);
+            ++count;
+        }
+        if (accepted) accepted[i] = ok ? 1 : 0;
+    }
+    if (written) *written = count;
+    return HALO_OK;
+}
+
+// ---- several devices, one host batch ------------------------------------------
+extern "C" HALO_API int halo_rx_shard_multi(halo_rx_host_ctx_t* const* ctxs, uint32_t n_ctx, const uint8_t* bytes,
+                                            const uint64_t* offsets, const uint16_t* lens, uint32_t n, uint32_t flags,
+                                            const halo_rx_netif_t* netif, halo_rx_result_t* out,
+                                            uint32_t* status_hist, uint32_t* shard_first) {
+    if (!ctxs || n_ctx == 0 || n_ctx > 1024 || !netif) return HALO_E_INVAL;
+    for (uint32_t k = 0; k < n_ctx; ++k)
+        if (!ctxs[k]) return HALO_E_INVAL;
+    if (n && (!bytes || !offsets || !lens || !out)) return HALO_E_INVAL;
+    // contiguous index ranges balanced by frame bytes
+    std::vector<uint32_t> first(n_ctx + 1, n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += lens[i];
+    first[0] = 0;
+    uint64_t acc = 0;
+    uint32_t k = 1;
+    for (uint32_t i = 0; i < n && k < n_ctx; ++i) {
+        while (k < n_ctx && acc >= total * k / n_ctx) first[k++] = i;
+        acc += lens[i];
+    }
+    while (k < n_ctx) first[k++] = n;
+    if (shard_first)
+        for (uint32_t j = 0; j <= n_ctx; ++j) shard_first[j] = first[j];
+    std::vector<int> rcs(n_ctx, HALO_OK);
+    std::vector<std::vector<uint32_t>> hists(n_ctx, std::vector<uint32_t>(HALO_RX_STATUS_COUNT, 0));
+    auto run = [&](uint32_t j) {
+        const uint32_t f0 = first[j], cnt = first[j + 1] - first[j];
+        if (cnt)
+            rcs[j] = halo_rx_parse_batch_host(ctxs[j], bytes, offsets + f0, lens + f0, cnt, flags, netif, out + f0,
+                                              status_hist ? hists[j].data() : nullptr);
+    };
+    std::vector<std::thread> th;
+    th.reserve(n_ctx);
+    for (uint32_t j = 1; j < n_ctx; ++j) th.emplace_back(run, j);
+    run(0);
+    for (auto& t : th) t.join();
+    for (uint32_t j = 0; j < n_ctx; ++j)
+        if (rcs[j]) return rcs[j];
+    if (status_hist)
+        for (uint32_t j = 0; j < n_ctx; ++j)
+            for (int s = 0; s < HALO_RX_STATUS_COUNT; ++s) status_hist[s] += hists[j][s];
+    return HALO_OK;
+}

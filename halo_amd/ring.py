@@ -1,0 +1,154 @@
+"""halo's SPSC packet ring as the receive source of GPU batches.
+
+The reference moves received frames from the DPDK lcore to Go through ``mem.RingBuffer``
+(mem/ring_buffer.go:18-352, the Go twin of cgo/ring_buffer.h), and ``engine.Wire``
+(engine/engine.go:507-559) is the same ring used as an in-memory link. Its consumer reads one
+record per ``ReadPacket`` call into a 1514-byte buffer and ``PacketHandle`` parses it.
+
+* ``RingBuffer`` — ``RingBufferCreate`` over host memory this object owns, and a batch producer
+  (``WritePacket`` per frame: ``halo_ring_write_batch``).
+* ``RingConsumer`` — ``NewRingBufferConsumer`` + batched ``ReadPacket``: ``poll`` parses every
+  frame between the consumer's cursor and the producer's head on the GPU
+  (``halo_rx_ring_poll``: raw DMA of the span, record boundaries found on the GPU, parse in
+  place, one record per frame), ``commit`` releases them (``tail`` store-release).
+* ``Wire`` — ``engine.NewWire`` (an 8 MiB ring) with ``Tx`` and a GPU ``rx_batch``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import RESULT_DTYPE, RING_HEADER, RING_REGISTER, RING_SCAN_DTYPE, RING_STOP_NAMES, NetIf
+from .protocol import flags_word
+
+WIRE_MAX_PACKET_SIZE = 1514  # engine/engine.go:507
+MAX_PACKET_SIZE = 1514       # dpdk/dpdk.go:20 (EthQueueRxPkt's receive buffer)
+
+
+def _aligned(nbytes: int, align: int = 64) -> np.ndarray:
+    raw = np.zeros(nbytes + align, dtype=np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nbytes]
+
+
+class RingBuffer:
+    """A RingBuffer (128-byte header + ``data_size``-byte power-of-two data area) in host memory."""
+
+    def __init__(self, data_size: int = 8 << 20):
+        self.mem = _aligned(RING_HEADER + data_size)
+        _lib.check("halo_ring_create", _lib.lib.halo_ring_create(self.mem.ctypes.data, self.mem.nbytes))
+        self.size = data_size
+
+    @property
+    def head(self) -> int:
+        return int(self.mem[0:8].view(np.uint64)[0])
+
+    @property
+    def tail(self) -> int:
+        return int(self.mem[64:72].view(np.uint64)[0])
+
+    @property
+    def data(self) -> np.ndarray:
+        return self.mem[RING_HEADER:]
+
+    def write_batch(self, data: np.ndarray, offsets: np.ndarray, lens: np.ndarray,
+                    accepted: Optional[np.ndarray] = None) -> int:
+        """WritePacket for every frame data[offsets[i]:offsets[i]+lens[i]]; refused frames are
+        dropped (accepted[i] = 0). Returns the number written."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        written = ctypes.c_uint32()
+        rc = _lib.lib.halo_ring_write_batch(self.mem.ctypes.data, _lib.ptr(data), _lib.ptr(offsets), _lib.ptr(lens),
+                                            lens.shape[0], _lib.ptr(accepted), ctypes.byref(written))
+        _lib.check("halo_ring_write_batch", rc)
+        return int(written.value)
+
+    def write(self, frames) -> int:
+        frames = [bytes(f) for f in frames]
+        if not frames:
+            return 0
+        lens = np.fromiter((len(f) for f in frames), dtype=np.uint16, count=len(frames))
+        offs = np.zeros(len(frames), dtype=np.uint64)
+        np.cumsum(lens[:-1], out=offs[1:])
+        return self.write_batch(np.frombuffer(b"".join(frames) + b"\0", np.uint8), offs, lens)
+
+    def length_at(self, position: int) -> int:
+        """The u32 length field of the record at stream position `position`."""
+        p = position % self.size  # records are 4-byte aligned: the field never wraps
+        return int(self.data[p:p + 4].view(np.uint32)[0])
+
+    def frame_at(self, position: int, length: int) -> bytes:
+        """The frame whose record sits at stream position `position` (unwrapped)."""
+        start = (position + 4) % self.size
+        idx = (start + np.arange(length)) % self.size
+        return self.data[idx].tobytes()
+
+
+class RingConsumer:
+    """The GPU consumer of one ring (halo_rx_ring_attach). ``capacity`` is ReadPacket's
+    ``len(data)`` (1514 in the DPDK driver and Wire)."""
+
+    def __init__(self, ring: RingBuffer, device: int = 0, capacity: int = MAX_PACKET_SIZE, max_bytes: int = 0,
+                 max_frames: int = 0, register: bool = True):
+        self.ring = ring
+        h = ctypes.c_void_p()
+        rc = _lib.lib.halo_rx_ring_attach(device, ring.mem.ctypes.data, 0, capacity, max_bytes, max_frames,
+                                          RING_REGISTER if register else 0, ctypes.byref(h))
+        _lib.check("halo_rx_ring_attach", rc)
+        self._h = h
+        cap = max_bytes or min(ring.size, 256 << 20)
+        self.max_frames = max_frames or min(cap, ring.size) // 8
+        self._out = np.zeros(self.max_frames, dtype=RESULT_DTYPE)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib.halo_rx_ring_detach(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def poll(self, netif: NetIf, check_sum_enable: bool = True, jumbo: bool = False, hist=None,
+             positions: bool = False):
+        """Parse the next frames. Returns (records view, info dict, positions or None); the records
+        view is reused by the next poll."""
+        info = np.zeros(1, dtype=RING_SCAN_DTYPE)
+        pos = np.zeros(self.max_frames, dtype=np.uint64) if positions else None
+        rc = _lib.lib.halo_rx_ring_poll(self._h, flags_word(check_sum_enable, jumbo), netif, self._out.ctypes.data,
+                                        _lib.ptr(hist), _lib.ptr(pos), info.ctypes.data)
+        _lib.check("halo_rx_ring_poll", rc)
+        n = int(info["n_frames"][0])
+        d = {"n_frames": n, "stop": RING_STOP_NAMES[int(info["stop"][0])], "end_bytes": int(info["end_bytes"][0]),
+             "max_len": int(info["max_len"][0])}
+        return self._out[:n], d, (pos[:n] if positions else None)
+
+    def commit(self):
+        _lib.check("halo_rx_ring_commit", _lib.lib.halo_rx_ring_commit(self._h))
+
+
+class Wire:
+    """engine.Wire (engine/engine.go:507-559): a ring with an 8 MiB data area as a virtual link."""
+
+    def __init__(self, device: int = 0, data_size: int = 8 << 20):
+        self.ring = RingBuffer(data_size)
+        self.consumer = RingConsumer(self.ring, device=device, capacity=WIRE_MAX_PACKET_SIZE)
+
+    def Tx(self, pkt: bytes) -> None:  # engine/engine.go:548-553
+        if len(pkt) == 0 or len(pkt) > WIRE_MAX_PACKET_SIZE:
+            return
+        self.ring.write([pkt])
+
+    def rx_batch(self, netif: NetIf, check_sum_enable: bool = True):
+        """Every frame Wire.Rx would return until it returns nil, parsed: (records, frames)."""
+        recs, info, pos = self.consumer.poll(netif, check_sum_enable, positions=True)
+        frames = [self.ring.frame_at(int(p), self.ring.length_at(int(p))) for p in pos]
+        out = recs.copy()
+        self.consumer.commit()
+        return out, frames
+
+    def Destroy(self):
+        self.consumer.close()

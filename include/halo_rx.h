@@ -209,6 +209,89 @@ HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* by
 HALO_API int halo_rx_host_register(const void* ptr, uint64_t bytes);
 HALO_API int halo_rx_host_unregister(const void* ptr);
 
+/* Multi-GPU host batch: frames [0, n) are split into n_ctx contiguous index
+ * ranges balanced by bytes; ctxs[k] (one host context per device, or several on one device)
+ * parses range k on its own host thread with halo_rx_parse_batch_host. Records land in out[i]
+ * in frame order; `status_hist` gets the sum. No data crosses devices, no collective.
+ * `shard_first` (optional, n_ctx + 1 entries) receives the range boundaries.              */
+HALO_API int halo_rx_shard_multi(halo_rx_host_ctx_t* const* ctxs, uint32_t n_ctx, const uint8_t* bytes,
+                                 const uint64_t* offsets, const uint16_t* lens, uint32_t n, uint32_t flags,
+                                 const halo_rx_netif_t* netif, halo_rx_result_t* out, uint32_t* status_hist,
+                                 uint32_t* shard_first);
+
+/* ---- halo's SPSC packet ring as the batch source --------------------
+ * The ring is the reference's own shared-memory layout (mem/ring_buffer.go:18-26 =
+ * cgo/ring_buffer.h:20-55): a 128-byte header (head @0, layout version 1 @8, tail @64,
+ * size @72, mask @80, buffer @88) followed by a power-of-two data area of records
+ * `u32 len` + bytes, each padded to 4 bytes (mem/ring_buffer.go:47-50). The DPDK lcore
+ * (cgo/dpdk.c:280-307) or engine.Wire.Tx (engine/engine.go:548-553) is the producer.
+ *
+ * A consumer replaces the per-record ReadPacket (mem/ring_buffer.go:298-352) + EthRxFunc +
+ * RxEthernet loop: each poll takes every record between its cursor and the producer's head
+ * (at most max_bytes / max_frames) and returns one record per frame, exactly the frames and
+ * the order repeated ReadPacket(buf[capacity]) calls would return. The span goes to HBM raw,
+ * record boundaries are found on the GPU, the frames are parsed where they lie; the host only
+ * reads `head` and, on commit, writes `tail` (release), as ReadPacket does.              */
+#define HALO_RING_STOP_EMPTY 0u      /* every record in the span was taken (usedSpace < 4)        */
+#define HALO_RING_STOP_BAD_LEN 1u    /* record length 0 or > size/2: ReadPacket returns false     */
+#define HALO_RING_STOP_PARTIAL 2u    /* next record not wholly in the span (usedSpace < totalSize;
+                                        also when max_bytes cut it)                              */
+#define HALO_RING_STOP_CAPACITY 3u   /* record longer than the receive buffer (len(data)):
+                                        ReadPacket leaves it, and the tail, in place              */
+#define HALO_RING_STOP_MAX 4u        /* max_frames taken, more records available                  */
+#define HALO_RING_STOP_BAD_CURSOR 5u /* head - tail > size: ReadPacket returns false              */
+#define HALO_RING_REGISTER 0x1u      /* attach: hipHostRegister the ring for full-rate DMA         */
+
+typedef struct halo_rx_ring_scan {
+    uint32_t n_frames;  /* frames taken                                                      */
+    uint32_t stop;      /* HALO_RING_STOP_*: why the walk ended                              */
+    uint64_t end_bytes; /* ring bytes the frames occupy: the tail advance                    */
+    uint32_t max_len;   /* longest frame taken                                               */
+    uint32_t pad;
+} halo_rx_ring_scan_t;
+
+typedef struct halo_rx_ring halo_rx_ring_t;
+
+/* Attach as the ring's consumer: ring_buffer_mapping + ring_buffer_consumer_init
+ * (cgo/ring_buffer.h:158-204, :228-246; mem/ring_buffer.go:150-200, :226-246): layout version,
+ * fill bytes, size/mask, head - tail <= size, and `offset` == this mapping's data address minus
+ * the stored buffer pointer (0 in the creating process). capacity = the receive buffer's
+ * len(data) (0: 1514, dpdk/dpdk.go:139; at most 16376); max_bytes (0: min(size, 256 MiB)) and
+ * max_frames (0: max_bytes / 8) bound one poll. The header is validated before any device call. */
+HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t offset, uint32_t capacity,
+                                 uint64_t max_bytes, uint32_t max_frames, uint32_t attach_flags,
+                                 halo_rx_ring_t** out);
+HALO_API int halo_rx_ring_detach(halo_rx_ring_t* ring);
+/* Parse the next frames (flags: HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT; full records). They
+ * stay in the ring until commit: positions[i] (optional) is frame i's record position in the
+ * stream (the tail value before its ReadPacket; the frame's bytes start 4 bytes later, modulo
+ * the size). Polls without a commit continue after the previous poll's frames. Synchronous. */
+HALO_API int halo_rx_ring_poll(halo_rx_ring_t* ring, uint32_t flags, const halo_rx_netif_t* netif,
+                               halo_rx_result_t* out, uint32_t* status_hist, uint64_t* positions,
+                               halo_rx_ring_scan_t* info);
+/* Release everything polled so far to the producer: tail = cursor (store-release). */
+HALO_API int halo_rx_ring_commit(halo_rx_ring_t* ring);
+
+/* The record walk alone, device-resident: `used` bytes of ring data in stream order at d_span
+ * (4-byte aligned; used a multiple of 4, <= ring_size), ring_size = RingBuffer.size. Writes
+ * n = info.n_frames (offset in dwords, length) pairs and *d_info. Workspace: at least
+ * halo_rx_ring_scan_workspace(used, capacity) bytes of device memory. Asynchronous.       */
+HALO_API uint64_t halo_rx_ring_scan_workspace(uint64_t used, uint32_t capacity);
+HALO_API int halo_rx_ring_scan_device(const uint8_t* d_span, uint64_t used, uint64_t ring_size,
+                                      uint32_t capacity, uint32_t max_frames, uint32_t* d_offsets_dw,
+                                      uint16_t* d_lens, halo_rx_ring_scan_t* d_info, void* d_workspace,
+                                      uint64_t workspace_bytes, halo_stream_t stream);
+
+/* The producer side, for rings this process creates (engine.NewWire / Wire.Tx,
+ * engine/engine.go:520-553): RingBufferCreate (mem/ring_buffer.go:93-126) over `bytes` of
+ * 64-byte-aligned memory (128-byte header + a power-of-two data area), and WritePacket
+ * (mem/ring_buffer.go:249-295) for every frame in order — a frame the ring refuses (full,
+ * empty, longer than size/2) is dropped, as the DPDK rx lcore drops it (cgo/dpdk.c:288-305).
+ * accepted[i] (optional) = 1 if frame i was written; *written = the count. Host only.      */
+HALO_API int halo_ring_create(void* memory, uint64_t bytes);
+HALO_API int halo_ring_write_batch(void* memory, const uint8_t* bytes, const uint64_t* offsets,
+                                   const uint16_t* lens, uint32_t n, uint8_t* accepted, uint32_t* written);
+
 /* ---- forward / transmit direction: in-place header rewrite + checksum fill --------------
  * (SURVEY.md §8f row f2). Frame i's IPv4 packet is pkt = frame[14 : len] — exactly the slice
  * engine.RxIpv4 hands to Ipv4RouteForward (engine/ipv4_engine.go:31-37) — and each frame gets

@@ -45,7 +45,7 @@ class NetIf(ctypes.Structure):
 
 def build(force: bool = False) -> str:
     srcs = [os.path.join(HERE, f) for f in ("halo_rx_oracle.c", "halo_tx_oracle.c", "halo_xxh3_oracle.c",
-                                            "halo_route_oracle.c")]
+                                            "halo_route_oracle.c", "halo_ring_oracle.c")]
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, srcs)):
         subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
     return LIB_PATH
@@ -95,6 +95,21 @@ def lib() -> ctypes.CDLL:
         L.ora_route_find_batch.argtypes = [vp, vp, u32, vp]
         L.ora_tx_batch.restype = ctypes.c_int
         L.ora_tx_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, ctypes.c_int]
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        L.ora_ring_create.restype = ctypes.c_int
+        L.ora_ring_create.argtypes = [vp, u64]
+        L.ora_ring_cursor.restype = None
+        L.ora_ring_cursor.argtypes = [vp, ctypes.c_int, u64p, u64p]
+        L.ora_ring_write.restype = ctypes.c_int
+        L.ora_ring_write.argtypes = [vp, u64p, u64p, vp, u32]
+        L.ora_ring_read.restype = ctypes.c_int
+        L.ora_ring_read.argtypes = [vp, u64p, u64p, vp, u32, u32p]
+        L.ora_ring_packet_handle.restype = u32
+        L.ora_ring_packet_handle.argtypes = [vp, u64p, u64p, u32, u32, u32, ctypes.POINTER(NetIf), vp, vp, vp, vp,
+                                             vp]
+        L.ora_ring_scan.restype = u32
+        L.ora_ring_scan.argtypes = [vp, u64, u64, u32, u32, vp, vp, u32p, u64p, u32p]
         _lib = L
     return _lib
 
@@ -251,3 +266,95 @@ class RouteTable:
         out = np.zeros(ips.shape[0], np.uint32)
         lib().ora_route_find_batch(self._t, _p(ips), ips.shape[0], _p(out))
         return out
+
+
+# ---- halo's SPSC packet ring (oracle/halo_ring_oracle.c) ---------------------------------------
+RING_HEADER = 128
+RING_STOP = {"EMPTY": 0, "BAD_LEN": 1, "PARTIAL": 2, "CAPACITY": 3, "MAX": 4, "BAD_CURSOR": 5}
+
+
+def aligned_zeros(nbytes: int, align: int = 64) -> np.ndarray:
+    raw = np.zeros(nbytes + align, dtype=np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nbytes]
+
+
+class Ring:
+    """A RingBuffer (mem/ring_buffer.go:18-26) in host memory owned by this object, with one
+    producer and one consumer cursor (WritePacket / ReadPacket restated in C)."""
+
+    def __init__(self, data_size: int = 8 << 20, mem: np.ndarray | None = None):
+        self.mem = aligned_zeros(RING_HEADER + data_size) if mem is None else mem
+        self.size = self.mem.nbytes - RING_HEADER
+        if mem is None:
+            assert lib().ora_ring_create(_p(self.mem), self.mem.nbytes) == 0
+        self._ph, self._pt = ctypes.c_uint64(), ctypes.c_uint64()
+        self._ct, self._ch = ctypes.c_uint64(), ctypes.c_uint64()
+        lib().ora_ring_cursor(_p(self.mem), 0, ctypes.byref(self._ph), ctypes.byref(self._pt))
+        lib().ora_ring_cursor(_p(self.mem), 1, ctypes.byref(self._ct), ctypes.byref(self._ch))
+
+    @property
+    def head(self) -> int:
+        return int(self.mem[0:8].view(np.uint64)[0])
+
+    @property
+    def tail(self) -> int:
+        return int(self.mem[64:72].view(np.uint64)[0])
+
+    def set_cursors(self, pos: int):
+        """An empty ring whose head and tail both sit at stream position `pos` (a restarted
+        producer/consumer pair that already moved pos bytes through)."""
+        self.mem[0:8].view(np.uint64)[0] = pos
+        self.mem[64:72].view(np.uint64)[0] = pos
+        self._ph.value = self._pt.value = self._ct.value = self._ch.value = pos
+
+    def write(self, frame: bytes) -> bool:
+        b = np.frombuffer(bytes(frame) + b"\0", dtype=np.uint8)
+        return bool(lib().ora_ring_write(_p(self.mem), ctypes.byref(self._ph), ctypes.byref(self._pt), _p(b),
+                                         len(frame)))
+
+    def write_raw(self, length_field: int, payload: bytes = b"") -> None:
+        """A record whose length field is `length_field` whatever the payload (corrupt records),
+        then head advanced by the record size the field implies, capped at the ring size."""
+        pos = self.head & (self.size - 1)
+        self.mem[RING_HEADER + pos:RING_HEADER + pos + 4] = np.frombuffer(
+            np.uint32(length_field).tobytes(), np.uint8)
+        for k, byte in enumerate(payload):
+            self.mem[RING_HEADER + (pos + 4 + k) % self.size] = byte
+        adv = min(((4 + length_field + 3) & ~3), self.size - (self.head - self.tail))
+        self.mem[0:8].view(np.uint64)[0] = self.head + adv
+        self._ph.value = self.head
+
+    def read(self, capacity: int = 1514):
+        """(ok, frame bytes or None, length)"""
+        buf = np.zeros(max(1, capacity), np.uint8)
+        ln = ctypes.c_uint32()
+        ok = lib().ora_ring_read(_p(self.mem), ctypes.byref(self._ct), ctypes.byref(self._ch), _p(buf), capacity,
+                                 ctypes.byref(ln))
+        return bool(ok), (buf[:ln.value].tobytes() if ok else None), int(ln.value)
+
+    def packet_handle(self, netif: NetIf, flags: int = 1, capacity: int = 1514, max_frames: int = 0xFFFFFFFF,
+                      actions: bool = True, frames: bool = False):
+        """BASELINE config 1's loop (ora_ring_packet_handle): (records, actions, positions, frames)."""
+        n_max = min(max_frames, self.size // 8)
+        out = np.zeros(n_max, RESULT_DTYPE)
+        act = np.zeros(n_max, np.uint8) if actions else None
+        pos = np.zeros(n_max, np.uint64)
+        fb = np.zeros(self.size + 16, np.uint8) if frames else None
+        fo = np.zeros(n_max, np.uint32) if frames else None
+        n = lib().ora_ring_packet_handle(_p(self.mem), ctypes.byref(self._ct), ctypes.byref(self._ch), capacity,
+                                         n_max, flags, netif, _p(out), _p(act), _p(pos), _p(fb), _p(fo))
+        return out[:n], (act[:n] if actions else None), pos[:n], ((fb, fo[:n]) if frames else None)
+
+
+def ring_scan(span: np.ndarray, used: int, ring_size: int, capacity: int = 1514, max_frames: int = 0xFFFFFFFF):
+    """ora_ring_scan: (off_dw, lens, stop, end_bytes, max_len)."""
+    n_max = max(1, used // 8)
+    off = np.zeros(n_max, np.uint32)
+    lens = np.zeros(n_max, np.uint16)
+    stop, ml = ctypes.c_uint32(), ctypes.c_uint32()
+    end = ctypes.c_uint64()
+    span = np.ascontiguousarray(span, np.uint8)
+    n = lib().ora_ring_scan(_p(span), used, ring_size, capacity, max_frames, _p(off), _p(lens), ctypes.byref(stop),
+                            ctypes.byref(end), ctypes.byref(ml))
+    return off[:n], lens[:n], int(stop.value), int(end.value), int(ml.value)

@@ -1,0 +1,275 @@
+"""GPU: halo's SPSC packet ring as the batch source, bit-exact.
+
+The oracle side is oracle/halo_ring_oracle.c — ReadPacket / the config-1 PacketHandle loop /
+the record walk — which tests/test_ring_oracle.py pins against the reference's own
+cgo/ring_buffer.h. Here the GPU consumer (halo_rx_ring_poll: raw span DMA, record boundaries
+found on the GPU, parse in place) and the device-resident walk (halo_rx_ring_scan_device) must
+return exactly the frames, records, positions, stop reason and new tail of that loop: wrap-around,
+corrupt and oversize records, max_bytes / max_frames cuts, tile-boundary and dense-record spans.
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import pytest
+
+from tests.helpers import assert_records_equal, golden_arrays
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    from halo_amd import _lib
+
+    _lib.check("halo_rx_init", _lib.lib.halo_rx_init(0))
+    return torch.device("cuda:0")
+
+
+def _seek(ring, pos: int):
+    """Move an empty ring's head and tail to stream position `pos`."""
+    ring.mem[0:8].view(np.uint64)[0] = pos
+    ring.mem[64:72].view(np.uint64)[0] = pos
+
+
+def _oracle_drain(O, mem, netif, flags, capacity, max_frames=0xFFFFFFFF):
+    r2 = O.Ring(mem=mem.copy())
+    recs, acts, pos, _ = r2.packet_handle(netif, flags, capacity=capacity, max_frames=max_frames)
+    return recs, acts, pos, r2._ct.value
+
+
+def _span(ring, start, used):
+    idx = (start % ring.size + np.arange(used)) % ring.size
+    return ring.mem[128:][idx]
+
+
+@pytest.mark.parametrize("flags", [0, 1, 3])
+def test_poll_golden_frames_across_the_wrap(dev, golden, oracle_lib, flags):
+    from halo_amd._lib import NetIf
+    from halo_amd.engine import dispatch
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    O = oracle_lib
+    meta, blob = golden
+    data, offs, lens, names = golden_arrays(meta, blob)
+    ring = RingBuffer(1 << 16)
+    _seek(ring, (1 << 40) + (1 << 16) - 2048)  # the batch wraps around the data area's end
+    small = (lens > 0) & (lens <= 1514)  # WritePacket refuses empty frames
+    n_w = ring.write_batch(data, offs[small].astype(np.uint64) * 4, lens[small])
+    assert n_w == int(small.sum())
+    want, acts, pos, tail = _oracle_drain(O, ring.mem, O.NetIf.make(), flags, 1514)
+    assert len(want) == n_w
+    cons = RingConsumer(ring, capacity=1514)
+    got, info, gpos = cons.poll(NetIf.make(), check_sum_enable=bool(flags & 1), jumbo=bool(flags & 2),
+                                positions=True)
+    assert_records_equal(got.copy(), want, [n for n, s in zip(names, small) if s], f"ring flags={flags}")
+    assert np.array_equal(gpos, pos)
+    assert info["stop"] == "EMPTY" and info["end_bytes"] == tail - ring.tail
+    assert np.array_equal(dispatch(got.copy(), NetIf.make()), acts)
+    assert ring.tail == (1 << 40) + (1 << 16) - 2048
+    cons.commit()
+    assert ring.tail == tail
+    got2, info2, _ = cons.poll(NetIf.make())
+    assert info2["n_frames"] == 0 and info2["stop"] == "EMPTY"
+    cons.close()
+
+
+def test_poll_stops_like_readpacket(dev, golden, oracle_lib):
+    """An oversize record (> capacity) stops the drain and stays; a corrupt length stops it for
+    good; max_frames and max_bytes cut it. Every poll is compared with the oracle loop."""
+    from halo_amd._lib import NetIf
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    O = oracle_lib
+    meta, blob = golden
+    data, offs, lens, _ = golden_arrays(meta, blob)
+    rng = np.random.default_rng(5)
+    netif, onetif = NetIf.make(), O.NetIf.make()
+    for case in ("capacity", "corrupt", "max_frames", "max_bytes"):
+        ring = RingBuffer(1 << 20)
+        _seek(ring, int(rng.integers(0, 1 << 30)) * 4)
+        sel = rng.permutation(np.nonzero(lens <= 1514)[0])[:120]
+        ring.write_batch(data, offs[sel].astype(np.uint64) * 4, lens[sel])
+        if case == "capacity":  # a 2000-byte record (ReadPacket leaves it: capacity 1514)
+            big = np.zeros(2000, np.uint8)
+            ring.write_batch(big, np.zeros(1, np.uint64), np.array([2000], np.uint16))
+        if case == "corrupt":  # a record whose length field is 0
+            pos = ring.head % ring.size
+            ring.mem[128 + (pos + np.arange(8)) % ring.size] = 0
+            ring.mem[0:8].view(np.uint64)[0] = ring.head + 8
+        ring.write_batch(data, offs[sel].astype(np.uint64) * 4, lens[sel])
+        kw = dict(max_frames=50) if case == "max_frames" else dict(max_bytes=6000) if case == "max_bytes" else {}
+        cons = RingConsumer(ring, capacity=1514, **kw)
+        mem_before = ring.mem.copy()
+        got_all = []
+        for _ in range(200):
+            got, info, _ = cons.poll(netif)
+            if info["n_frames"] == 0:
+                break
+            got_all.append(got.copy())
+            cons.commit()
+        got_all = np.concatenate(got_all) if got_all else np.zeros(0, got.dtype)
+        want, _, _, tail = _oracle_drain(O, mem_before, onetif, 1, 1514)
+        assert_records_equal(got_all, want, None, f"ring stop case {case}")
+        assert ring.tail == tail, case
+        assert info["stop"] == {"capacity": "CAPACITY", "corrupt": "BAD_LEN"}.get(case, "EMPTY"), (case, info)
+        cons.close()
+
+
+def _records_span(rng, lens, corrupt_at=None, corrupt_val=0):
+    """A ring span in stream order holding records of `lens` (+ random bytes)."""
+    lens = np.asarray(lens, np.int64)
+    sizes = (4 + lens + 3) & ~3
+    starts = np.zeros(len(lens), np.int64)
+    starts[1:] = np.cumsum(sizes)[:-1]
+    used = int(sizes.sum())
+    span = rng.integers(0, 256, used + 16, dtype=np.uint8)
+    words = span[:used].view(np.uint32)
+    words[starts // 4] = lens.astype(np.uint32)
+    if corrupt_at is not None:
+        words[starts[corrupt_at] // 4] = corrupt_val
+    return span, used
+
+
+SCAN_CASES = [
+    # name, lens generator, capacity, max_frames, corrupt (index, value)
+    ("empty", lambda r: [], 1514, 0, None),
+    ("one", lambda r: [60], 1514, 0, None),
+    ("64B_x300k", lambda r: [64] * 300_000, 1514, 0, None),
+    ("dense_1to4B", lambda r: r.integers(1, 5, 200_000), 1514, 0, None),
+    ("imix", lambda r: r.choice([64, 570, 1500], 100_000, p=[7 / 12, 4 / 12, 1 / 12]), 1514, 0, None),
+    ("uniform_to_cap", lambda r: r.integers(1, 1515, 60_000), 1514, 0, None),
+    ("jumbo_cap", lambda r: r.integers(1, 9015, 20_000), 9014, 0, None),
+    ("max_window", lambda r: r.integers(1, 16377, 8_000), 16376, 0, None),
+    ("oversize_mid", lambda r: list(r.integers(1, 1515, 40_000)) + [1515] + [64] * 1000, 1514, 0, None),
+    ("bad_len_mid", lambda r: r.integers(1, 1515, 50_000), 1514, 0, (31_337, 0)),
+    ("huge_len_mid", lambda r: r.integers(1, 200, 50_000), 1514, 0, (20_001, 0xFFFFFFFF)),
+    ("max_frames_cut", lambda r: r.integers(1, 1515, 50_000), 1514, 12_345, None),
+    ("max_frames_exact", lambda r: [64] * 5000, 1514, 5000, None),
+    ("max_frames_one", lambda r: [64] * 5000, 1514, 1, None),
+]
+
+
+@pytest.mark.parametrize("name,gen,cap,max_frames,corrupt", SCAN_CASES, ids=[c[0] for c in SCAN_CASES])
+def test_scan_device_matches_walk(dev, oracle_lib, name, gen, cap, max_frames, corrupt):
+    import torch
+
+    from halo_amd import _lib
+
+    O = oracle_lib
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    lens = gen(rng)
+    span, used = _records_span(rng, lens, *(corrupt or (None, 0)))
+    ring_size = 1 << max(12, int(np.ceil(np.log2(max(used, 8)))) + 1)
+    for trim in (0, 4, 12) if used > 64 else (0,):  # also spans that end inside a record
+        u = max(0, used - trim)
+        mf = max_frames or 0xFFFFFFFF
+        w_off, w_len, w_stop, w_end, w_ml = O.ring_scan(span, u, ring_size, cap, mf)
+        d_span = torch.from_numpy(span).to(dev)
+        n_max = max(1, u // 8)
+        d_off = torch.zeros(n_max, dtype=torch.int32, device=dev)
+        d_len = torch.zeros(n_max, dtype=torch.int16, device=dev)
+        info = torch.zeros(24, dtype=torch.uint8, device=dev)
+        ws_bytes = _lib.lib.halo_rx_ring_scan_workspace(u, cap)
+        ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=dev)
+        rc = _lib.lib.halo_rx_ring_scan_device(d_span.data_ptr(), u, ring_size, cap, max_frames, d_off.data_ptr(),
+                                               d_len.data_ptr(), info.data_ptr(), ws.data_ptr(), ws_bytes,
+                                               torch.cuda.current_stream().cuda_stream)
+        _lib.check("halo_rx_ring_scan_device", rc)
+        torch.cuda.synchronize()
+        inf = info.cpu().numpy().view(_lib.RING_SCAN_DTYPE)[0]
+        n = int(inf["n_frames"])
+        assert n == len(w_off), (name, trim, n, len(w_off))
+        assert (int(inf["stop"]), int(inf["end_bytes"]), int(inf["max_len"])) == (w_stop, w_end, w_ml), (name, trim)
+        assert np.array_equal(d_off[:n].cpu().numpy().view(np.uint32), w_off), name
+        assert np.array_equal(d_len[:n].cpu().numpy().view(np.uint16), w_len), name
+
+
+def test_poll_large_imix_ring(dev, oracle_lib):
+    """A 256 MiB ring holding ~700k synthetic IMIX frames (1/16 bit-flipped), drained in one poll
+    (hundreds of superblocks): records == the per-frame oracle; histogram == records."""
+    import torch
+
+    from halo_amd import synth
+    from halo_amd._lib import NetIf
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    O = oracle_lib
+    n = 700_000
+    lay = synth.layout(n, size_mode=synth.SIZE_IMIX, proto_mode=synth.PROTO_MIX, mutate_shift=4)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    host = fr["bytes"].cpu().numpy()
+    ring = RingBuffer(256 << 20)
+    _seek(ring, (256 << 20) - 4096)
+    assert ring.write_batch(host, lay["offsets_dw"].astype(np.uint64) * 4, lay["lens"]) == n
+    cons = RingConsumer(ring, capacity=1514, max_bytes=256 << 20)
+    hist = np.zeros(14, np.uint32)
+    got, info, _ = cons.poll(NetIf.make(), hist=hist)
+    assert info["n_frames"] == n and info["stop"] == "EMPTY"
+    want, whist = O.rx_batch(host, lay["lens"], O.NetIf.make(), 1, offsets_dw=lay["offsets_dw"])
+    assert_records_equal(got.copy(), want, None, "256 MiB IMIX ring")
+    assert np.array_equal(hist, whist)
+    mutated = (lay["kinds"] & 0x80) != 0
+    assert np.all(got["status"][~mutated] == 0) and np.all(got["status"][mutated] != 0)
+    cons.commit()
+    assert ring.tail == ring.head
+    cons.close()
+    del fr
+    torch.cuda.empty_cache()
+
+
+def test_wire_rx_batch(dev, golden, oracle_lib):
+    """engine.Wire: Tx drops empty and > 1514 B frames; rx_batch returns what Wire.Rx would."""
+    from halo_amd._lib import NetIf
+    from halo_amd.ring import Wire
+
+    O = oracle_lib
+    meta, blob = golden
+    data, offs, lens, _ = golden_arrays(meta, blob)
+    w = Wire()
+    frames = [data[int(o) * 4:int(o) * 4 + int(ln)].tobytes() for o, ln in zip(offs, lens)]
+    for f in frames:
+        w.Tx(f)
+    kept = [f for f in frames if 0 < len(f) <= 1514]
+    recs, got_frames = w.rx_batch(NetIf.make())
+    assert got_frames == kept
+    want = np.concatenate([O.rx_frame(f, O.NetIf.make(), 1).reshape(1) for f in kept])
+    assert recs.tobytes() == want.tobytes()
+    w.Destroy()
+
+
+def test_shard_multi_two_contexts_one_device(dev, oracle_lib):
+    """halo_rx_shard_multi with two host contexts (on the one device here): byte-balanced index
+    ranges, records in frame order == one context == the oracle."""
+    import ctypes
+
+    from halo_amd import _lib, synth
+    from halo_amd._lib import NetIf
+    from halo_amd.engine import HostBatcher
+
+    O = oracle_lib
+    lay = synth.layout(50_000, size_mode=synth.SIZE_IMIX, proto_mode=synth.PROTO_MIX, mutate_shift=3)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    host = fr["bytes"].cpu().numpy()
+    offs = lay["offsets_dw"].astype(np.uint64) * 4
+    a, b = HostBatcher(0), HostBatcher(0)
+    ctxs = (ctypes.c_void_p * 2)(a._ctx, b._ctx)
+    out = np.zeros(50_000, _lib.RESULT_DTYPE)
+    hist = np.zeros(14, np.uint32)
+    first = np.zeros(3, np.uint32)
+    rc = _lib.lib.halo_rx_shard_multi(ctxs, 2, host.ctypes.data, offs.ctypes.data, lay["lens"].ctypes.data, 50_000, 1,
+                                      NetIf.make(), out.ctypes.data, hist.ctypes.data, first.ctypes.data)
+    _lib.check("halo_rx_shard_multi", rc)
+    want, whist = O.rx_batch(host, lay["lens"], O.NetIf.make(), 1, offsets_dw=lay["offsets_dw"])
+    assert_records_equal(out, want, None, "shard_multi")
+    assert np.array_equal(hist, whist)
+    assert first[0] == 0 and first[2] == 50_000
+    half = int(lay["lens"][:first[1]].astype(np.int64).sum())
+    total = int(lay["lens"].astype(np.int64).sum())
+    assert abs(half - total / 2) <= 1514
+    a.close()
+    b.close()
