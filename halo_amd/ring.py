@@ -101,13 +101,19 @@ class RingConsumer:
         _lib.check("halo_rx_ring_attach", rc)
         self._h = h
         cap = max_bytes or min(ring.size, 256 << 20)
-        self.max_frames = max_frames or min(cap, ring.size) // 8
+        self.max_frames = min(max_frames or (1 << 32) - 1, min(cap, ring.size) // 8)
         self._out = np.zeros(self.max_frames, dtype=RESULT_DTYPE)
+        # the records come back by DMA straight into this array: pin it too
+        self._out_registered = register and _lib.lib.halo_rx_host_register(self._out.ctypes.data,
+                                                                           self._out.nbytes) == 0
 
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib.halo_rx_ring_detach(self._h)
             self._h = None
+            if self._out_registered:
+                _lib.lib.halo_rx_host_unregister(self._out.ctypes.data)
+                self._out_registered = False
 
     def __del__(self):
         self.close()

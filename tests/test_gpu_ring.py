@@ -56,8 +56,8 @@ def test_poll_golden_frames_across_the_wrap(dev, golden, oracle_lib, flags):
     O = oracle_lib
     meta, blob = golden
     data, offs, lens, names = golden_arrays(meta, blob)
-    ring = RingBuffer(1 << 16)
-    _seek(ring, (1 << 40) + (1 << 16) - 2048)  # the batch wraps around the data area's end
+    ring = RingBuffer(1 << 18)
+    _seek(ring, (1 << 40) + (1 << 18) - 2048)  # the batch wraps around the data area's end
     small = (lens > 0) & (lens <= 1514)  # WritePacket refuses empty frames
     n_w = ring.write_batch(data, offs[small].astype(np.uint64) * 4, lens[small])
     assert n_w == int(small.sum())
@@ -70,7 +70,7 @@ def test_poll_golden_frames_across_the_wrap(dev, golden, oracle_lib, flags):
     assert np.array_equal(gpos, pos)
     assert info["stop"] == "EMPTY" and info["end_bytes"] == tail - ring.tail
     assert np.array_equal(dispatch(got.copy(), NetIf.make()), acts)
-    assert ring.tail == (1 << 40) + (1 << 16) - 2048
+    assert ring.tail == (1 << 40) + (1 << 18) - 2048
     cons.commit()
     assert ring.tail == tail
     got2, info2, _ = cons.poll(NetIf.make())
