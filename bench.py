@@ -138,6 +138,9 @@ def bench_lib():
         L.halo_bench_route_steps.argtypes = [i32, vp, vp, u32, vp] + tail
         L.halo_bench_xxh3_steps.restype = ctypes.c_int
         L.halo_bench_xxh3_steps.argtypes = [i32, vp, vp, vp, u32, vp] + tail
+        u64 = ctypes.c_uint64
+        L.halo_bench_ring_scan_steps.restype = ctypes.c_int
+        L.halo_bench_ring_scan_steps.argtypes = [i32, vp, u64, u64, u32, vp, vp, vp, vp, u64] + tail
         _BENCH_LIB = L
     return _BENCH_LIB
 
@@ -381,6 +384,116 @@ def route_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
     return res
 
 
+def ring_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = False):
+    """§8f f1 and BASELINE config 1: halo's SPSC packet ring (mem/ring_buffer.go) drained by the GPU.
+
+    (a) ring_scan_device: the record walk alone on a device-resident span of 1M 64 B records;
+    (b) ring_e2e: a producer fills a registered 128 MiB ring with 1M 64 B frames (untimed), the
+        consumer polls (span DMA + walk + parse + records back) and commits (timed);
+    (c) config1_wire_1k: 1k x 64 B frames through an engine.Wire-sized ring (8 MiB), poll + commit
+        per batch, beside the oracle's PacketHandle loop over the same ring on one core."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from halo_amd import _lib
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    res = {}
+    n = 1 << 20
+    fr = make_batches(dev, netif, n=n, rotate=1, rank=0)[0]
+    lay = fr["layout"]
+    host = fr["bytes"].cpu().numpy()
+    offs = lay["offsets_dw"].astype(np.uint64) * 4
+    lens = lay["lens"]
+    del fr
+    ring = RingBuffer(128 << 20)
+    assert ring.write_batch(host, offs, lens) == n
+    used = ring.head - ring.tail
+
+    # (a) the walk alone, device-resident
+    span = torch.from_numpy(ring.data[:used].copy()).to(dev)
+    d_off = torch.empty(n, dtype=torch.int32, device=dev)
+    d_len = torch.empty(n, dtype=torch.int16, device=dev)
+    info = torch.zeros(24, dtype=torch.uint8, device=dev)
+    ws_bytes = _lib.lib.halo_rx_ring_scan_workspace(used, 1514)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    arr = (ctypes.c_void_p * 1)(span.data_ptr())
+    w, k = time_native(bench_lib().halo_bench_ring_scan_steps, 1, arr, used, ring.size, 1514, d_off.data_ptr(),
+                       d_len.data_ptr(), info.data_ptr(), ws.data_ptr(), ws_bytes, steps=steps, warmup=warmup, d=d)
+    got_n = int(info.cpu().numpy().view(_lib.RING_SCAN_DTYPE)[0]["n_frames"])
+    alg = used + n * 6  # the span read once, (u32 offset + u16 length) written per frame
+    res["ring_scan_device_1M_64B"] = {
+        "records": got_n, "mrecords_per_s": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 4),
+        "roofline": roofline(alg, k, load_traffic("ring_scan_1M_64B")), "alg_bytes_per_launch": alg,
+        "what": "record boundaries of a 68 MB ring span (4 kernels: tile maps by pointer jumping, superblock "
+                "compose, chain, emit)"}
+    del span, d_off, d_len, ws
+    torch.cuda.empty_cache()
+
+    # (b) end to end from the ring in host memory
+    cons = RingConsumer(ring, capacity=1514, max_frames=n + 64, register=True)
+    times, ok = [], True
+    for s in range(max(3, steps // 20) + 1):
+        if s:
+            assert ring.write_batch(host, offs, lens) == n
+        t0 = time.perf_counter()
+        recs, inf, _ = cons.poll(netif)
+        cons.commit()
+        el = time.perf_counter() - t0
+        ok = ok and inf["n_frames"] == n and bool((recs["status"] == 0).all())
+        if s:
+            times.append(el)
+    el = float(np.median(times))
+    fb = int(lens.astype(np.int64).sum())
+    res["ring_e2e_64B_1M_registered"] = {
+        "frames": n, "mpps": round(n / el / 1e6, 1), "gbit_s": round(fb * 8 / el / 1e9, 1),
+        "ms_per_batch": round(el * 1e3, 3), "ok": ok, "ring_bytes": used,
+        "what": "poll (raw span DMA + GPU record walk + parse in place + records DMA) + commit; median of batches"}
+    cons.close()
+    del ring
+
+    # (c) BASELINE config 1: 1k x 64 B frames through an engine.Wire-sized ring
+    m = 1000
+    wring = RingBuffer(8 << 20)
+    wcons = RingConsumer(wring, capacity=1514, max_frames=4096, register=True)
+    times = []
+    for s in range(201):
+        assert wring.write_batch(host, offs[:m], lens[:m]) == m
+        t0 = time.perf_counter()
+        recs, inf, _ = wcons.poll(netif)
+        wcons.commit()
+        el = time.perf_counter() - t0
+        assert inf["n_frames"] == m
+        if s:
+            times.append(el)
+    el = float(np.median(times))
+    res["config1_wire_1k_64B"] = {"frames": m, "mpps": round(m / el / 1e6, 3), "us_per_batch": round(el * 1e6, 1),
+                                  "what": "engine.Wire ring (8 MiB), 1k x 64 B UDP, GPU poll + commit per batch "
+                                          "(latency-bound: ~6 dependent launches + 3 copies)"}
+    wcons.close()
+    if with_cpu:
+        from oracle import oracle as O
+
+        onet = O.NetIf.make()
+        oring = O.Ring(8 << 20)
+        total, passes = 0.0, 0
+        while total < 2.0:
+            for k in range(m):
+                oring.write(host[int(offs[k]):int(offs[k]) + int(lens[k])].tobytes())
+            t0 = time.perf_counter()
+            recs, _, _, _ = oring.packet_handle(onet, 1, capacity=1514, max_frames=m, actions=True)
+            total += time.perf_counter() - t0
+            passes += 1
+            assert len(recs) == m
+        res["config1_wire_1k_64B"]["cpu_baseline"] = {
+            "value": round(m * passes / total / 1e6, 3), "unit": "Mpps", "cores": 1, "kind": "port",
+            "sample": f"{passes} passes of the same 1k frames: ReadPacket -> RxEthernet -> RxIpv4 -> RxUdp per frame "
+                      "(oracle/halo_ring_oracle.c + halo_rx_oracle.c -O2, one thread; the reference is Go)"}
+    return res
+
+
 def roofline(alg_bytes_per_launch, kernel_ms, traffic=None):
     achieved = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -592,6 +705,9 @@ def main():
         # buffered in 64 MB chunks by halo_rx_parse_batch_host; the frame buffer is registered
         # (pinned in place) so each chunk is one DMA straight from it
         sec.update(e2e_host(dev, netif, steps=max(3, args.steps // 40)))
+        # halo's SPSC packet ring as the source (BASELINE config 1 over a Wire)
+        sec.update(ring_secondary(dev, netif, max(10, args.steps // 4), 3, d, with_cpu=not args.no_cpu))
+        torch.cuda.empty_cache()
         line["secondary"] = sec
     if d.world == 1 and not args.no_cpu:  # rank 0 at N=1 only
         bs = make_batches(dev, netif, n=n, rotate=1, rank=0)

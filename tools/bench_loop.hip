@@ -129,3 +129,16 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_route_steps(
     auto launch = [&](int k) { return halo_route_lookup_device(t, ips[k % nbatch], n, out, stream); };
     return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
 }
+
+// Row f1: the device-resident record walk of halo's packet ring (halo_rx_ring_scan_device).
+extern "C" __attribute__((visibility("default"))) int halo_bench_ring_scan_steps(
+    int nbatch, const uint8_t* const* spans, uint64_t used, uint64_t ring_size, uint32_t capacity, uint32_t* off,
+    uint16_t* lens, halo_rx_ring_scan_t* info, void* ws, uint64_t ws_bytes, int warmup, int steps, void* stream,
+    float* region_ms, double* wall_s) {
+    if (nbatch <= 0) return HALO_E_INVAL;
+    auto launch = [&](int k) {
+        return halo_rx_ring_scan_device(spans[k % nbatch], used, ring_size, capacity, 0, off, lens, info, ws, ws_bytes,
+                                        stream);
+    };
+    return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
+}

@@ -25,6 +25,8 @@ WORKLOADS = [
     ("tx_config2", dict(length=64), 1 << 20, 8, 20, 0, 1, 64),
     # flow-key hashing (§8f row f3): NatWanFlowHash + bucket on the parsed config 2 records
     ("flow_hash_config2", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
+    # halo's packet ring (§8f row f1): the record walk over 1M 64 B records (68 MB span)
+    ("ring_scan_1M_64B", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
 ]
 
 
@@ -51,6 +53,32 @@ def main():
             ops = torch.from_numpy(bench.tx_ops_for(n).view(np.uint8)).to(dev)
         torch.cuda.synchronize()
         stream = torch.cuda.current_stream().cuda_stream
+        if name.startswith("ring_scan"):
+            import numpy as np
+
+            from halo_amd.ring import RingBuffer
+
+            fr = bs[0]
+            lay = fr["layout"]
+            ring = RingBuffer(128 << 20)
+            ring.write_batch(fr["bytes"].cpu().numpy(), lay["offsets_dw"].astype(np.uint64) * 4, lay["lens"])
+            used = ring.head - ring.tail
+            span = torch.from_numpy(ring.data[:used].copy()).to(dev)
+            d_off = torch.empty(n, dtype=torch.int32, device=dev)
+            d_len = torch.empty(n, dtype=torch.int16, device=dev)
+            info = torch.zeros(24, dtype=torch.uint8, device=dev)
+            wsb = _lib.lib.halo_rx_ring_scan_workspace(used, 1514)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            for i in range(launches):
+                _lib.check("ring_scan", _lib.lib.halo_rx_ring_scan_device(
+                    span.data_ptr(), used, ring.size, 1514, 0, d_off.data_ptr(), d_len.data_ptr(), info.data_ptr(),
+                    ws.data_ptr(), wsb, stream))
+            torch.cuda.synchronize()
+            print(f"{name}: {launches} walks of {used} bytes", flush=True)
+            del bs, out, span, ws
+            torch.cuda.empty_cache()
+            continue
         if name.startswith("flow_hash"):
             from halo_amd import protocol
 
