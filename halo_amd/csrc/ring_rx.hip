@@ -49,7 +49,6 @@ constexpr uint32_t kMaxCapacity = 4 * kTile - 8; // the longest record must fit 
 constexpr uint32_t kRbHeader = 128;              // sizeof(RingBuffer), mem/ring_buffer.go:18-26
 constexpr uint64_t kMaxSpan = (16ull << 30) - (64ull << 10);  // dword offsets stay below 2^32
 constexpr uint64_t kPieceBytes = 16ull << 20;    // DMA piece (1024 tiles) whose maps start on arrival
-constexpr uint32_t kParseChunk = 1u << 20;       // frames per parse launch / record copy
 
 struct Scan {
     const uint32_t* span;   // the ring bytes [tail, tail + used) in stream order, as dwords
@@ -58,12 +57,16 @@ struct Scan {
     uint32_t cap;           // receive buffer capacity: len(data) of ReadPacket
     uint32_t W;             // entry window: dwords of the longest acceptable record
     uint32_t S;             // tiles per superblock
-    uint32_t n_sb;
+    uint32_t n_sb;          // superblocks: S tiles each
+    uint32_t n_ss;          // super-superblocks: S superblocks each
     uint32_t max_frames;
     uint64_t half;          // RingBuffer.size / 2
     uint2* tile_map;        // [n_tiles][W]: (entry into the next tile | kMapStop, records taken)
     uint2* sb_map;          // [n_sb][W]
+    uint2* ss_map;          // [n_ss][W]
+    uint2* ss_entry;        // [n_ss]: (entry | kMapStop, records before it)
     uint2* sb_entry;        // [n_sb]: (entry | kMapStop, records before the superblock)
+    uint2* tile_entry;      // [n_tiles]: (entry | kMapStop, records before the tile)
     uint32_t* total;        // records the walk takes before it stops (max_frames ignored)
     halo_rx_ring_scan_t* info;
     uint32_t* off_dw;       // frame i's bytes start at span dword off_dw[i]
@@ -83,54 +86,105 @@ __device__ __forceinline__ uint32_t record_dwords(const Scan& s, uint32_t a, uin
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
-// Span dwords of tile t into LDS (16-byte loads inside the span), zero past its end.
-__device__ __forceinline__ void load_tile(const Scan& s, uint32_t t, uint32_t* dw) {
-    const uint32_t base = t * kTile;
-    for (uint32_t q = 4 * threadIdx.x; q < kTile; q += 4 * kThreads) {
-        const uint32_t a = base + q;
-        uint4 v;
-        if (a + 4 <= s.n_dw) {
-            const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + a);
-            v = make_uint4(x.x, x.y, x.z, x.w);
-        } else {
-            v.x = a < s.n_dw ? s.span[a] : 0u;
-            v.y = a + 1 < s.n_dw ? s.span[a + 1] : 0u;
-            v.z = a + 2 < s.n_dw ? s.span[a + 2] : 0u;
-            v.w = a + 3 < s.n_dw ? s.span[a + 3] : 0u;
-        }
-        *reinterpret_cast<uint4*>(dw + q) = v;
+// Span dwords [a, a+4) (zero past the span's end).
+__device__ __forceinline__ uint4 span_quad(const Scan& s, uint32_t a) {
+    if (a + 4 <= s.n_dw) {
+        const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + a);
+        return make_uint4(x.x, x.y, x.z, x.w);
     }
+    return make_uint4(a < s.n_dw ? s.span[a] : 0u, a + 1 < s.n_dw ? s.span[a + 1] : 0u,
+                      a + 2 < s.n_dw ? s.span[a + 2] : 0u, a + 3 < s.n_dw ? s.span[a + 3] : 0u);
+}
+
+// Span dwords of tile t into LDS: every thread's four 16-byte loads in flight at once (the branch on
+// the span's end is uniform over the block, so the loads are not serialised behind it).
+__device__ __forceinline__ void load_tile(const Scan& s, uint32_t t, uint32_t* dw) {
+    constexpr int kPer = kTile / (4 * kThreads);
+    const uint32_t base = t * kTile;
+    uint4 v[kPer];
+    if (base + kTile <= s.n_dw) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + base + 4 * (threadIdx.x + u * kThreads));
+            v[u] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) v[u] = span_quad(s, base + 4 * (threadIdx.x + u * kThreads));
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) *reinterpret_cast<uint4*>(dw + 4 * (threadIdx.x + u * kThreads)) = v[u];
+}
+
+// Stage `count` map entries src[0..count) into LDS with 8 loads in flight per thread.
+__device__ __forceinline__ void stage_maps(const uint2* src, uint32_t count, uint2* m) {
+    for (uint32_t k0 = 0; k0 < count; k0 += 8 * kThreads) {
+        uint2 r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t k = k0 + u * kThreads + threadIdx.x;
+            if (k < count) r[u] = src[k];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t k = k0 + u * kThreads + threadIdx.x;
+            if (k < count) m[k] = r[u];
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t b) {
+    return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
 }
 
 // 1. Tile maps for tiles [tile0, tile0 + gridDim.x). Jump-table entry: bits 0-15 target position
 // (< kTile: inside the tile; kTile..2*kTile-1: the next tile's position + kTile; kLdsStop: the
-// walk stops), bits 16-31 records taken on the way.
+// walk stops), bits 16-31 records taken on the way. Only positions whose first step stays inside
+// the tile can change, and in ring data nearly every position that is not a record start fails
+// ReadPacket's checks at once (a random dword is rarely a length <= capacity), so the rounds run
+// over a compacted list of those positions and stop as soon as a round changes nothing.
 __global__ void __launch_bounds__(kThreads) ring_tile_map_kernel(const Scan s, uint32_t tile0) {
     __shared__ __align__(16) uint32_t jt[2][kTile];
+    __shared__ uint16_t act[kTile];
+    __shared__ uint32_t n_act;
     const uint32_t t = tile0 + blockIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (threadIdx.x == 0) n_act = 0;
     load_tile(s, t, jt[1]);
     __syncthreads();
     const uint32_t base = t * kTile;
-    for (uint32_t q = threadIdx.x; q < kTile; q += kThreads) {
+    for (uint32_t q = threadIdx.x; q < kTile; q += kThreads) {  // uniform trip count
         uint32_t why;
         const uint32_t step = record_dwords(s, base + q, jt[1][q], why);
-        jt[0][q] = step ? ((q + step) | (1u << 16)) : kLdsStop;
+        const uint32_t v = step ? ((q + step) | (1u << 16)) : kLdsStop;
+        const bool active = step && q + step < kTile;
+        const uint64_t b = __ballot(active);
+        uint32_t slot = 0;
+        if (lane == 0) slot = atomicAdd(&n_act, (uint32_t)__popcll(b));
+        slot = (uint32_t)__shfl((int)slot, 0, 64);
+        if (active) act[slot + lane_rank(b)] = (uint16_t)q;
+        jt[0][q] = v;
+        jt[1][q] = v;  // this thread's own raw dword is consumed: both buffers start equal
     }
     __syncthreads();
+    const uint32_t na = n_act;
     uint32_t cur = 0;
     for (uint32_t r = 0; r < kJumpRounds; ++r) {
-        for (uint32_t q = threadIdx.x; q < kTile; q += kThreads) {
+        int changed = 0;
+        for (uint32_t i = threadIdx.x; i < na; i += kThreads) {
+            const uint32_t q = act[i];
             const uint32_t v = jt[cur][q];
             const uint32_t tg = v & 0xFFFFu;
             uint32_t nv = v;
             if (tg < kTile) {
                 const uint32_t w = jt[cur][tg];
                 nv = (w & 0xFFFFu) | ((v & 0xFFFF0000u) + (w & 0xFFFF0000u));
+                changed = 1;
             }
             jt[cur ^ 1][q] = nv;
         }
-        __syncthreads();
         cur ^= 1;
+        if (!__syncthreads_or(changed)) break;
     }
     uint2* out = s.tile_map + (uint64_t)t * s.W;
     for (uint32_t e = threadIdx.x; e < s.W; e += kThreads) {
@@ -140,40 +194,39 @@ __global__ void __launch_bounds__(kThreads) ring_tile_map_kernel(const Scan s, u
     }
 }
 
-// 2. Compose the maps of superblock blockIdx.x's tiles.
-__global__ void __launch_bounds__(kThreads) ring_sb_compose_kernel(const Scan s) {
+// 2. Compose groups of S consecutive maps (tiles -> superblocks -> super-superblocks): block b
+// composes src maps [b*S, b*S + S).
+__global__ void __launch_bounds__(kThreads) ring_compose_kernel(const uint2* src, uint32_t n_src, uint2* dst,
+                                                                uint32_t W, uint32_t S) {
     __shared__ uint2 m[kMapLds];
-    const uint32_t sb = blockIdx.x;
-    const uint32_t t0 = sb * s.S;
-    const uint32_t nt = min(s.S, s.n_tiles - t0);
-    const uint2* src = s.tile_map + (uint64_t)t0 * s.W;
-    for (uint32_t k = threadIdx.x; k < nt * s.W; k += kThreads) m[k] = src[k];
+    const uint32_t g0 = blockIdx.x * S;
+    const uint32_t nt = min(S, n_src - g0);
+    stage_maps(src + (uint64_t)g0 * W, nt * W, m);
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < s.W; e += kThreads) {
+    for (uint32_t e = threadIdx.x; e < W; e += kThreads) {
         uint32_t cur = e, taken = 0;
         for (uint32_t k = 0; k < nt && cur != kMapStop; ++k) {
-            const uint2 v = m[k * s.W + cur];
+            const uint2 v = m[k * W + cur];
             taken += v.y;
             cur = v.x;
         }
-        s.sb_map[(uint64_t)sb * s.W + e] = make_uint2(cur, taken);
+        dst[(uint64_t)blockIdx.x * W + e] = make_uint2(cur, taken);
     }
 }
 
-// 3. Chain the superblocks from the span's start (one workgroup; maps staged in LDS in chunks).
+// 3. Chain the top-level maps from the span's start (one workgroup; maps staged in LDS in chunks).
 __global__ void __launch_bounds__(kThreads) ring_chain_kernel(const Scan s) {
     __shared__ uint2 m[kMapLds];
     const uint32_t per = kMapLds / s.W;
     uint32_t entry = 0, taken = 0;  // thread 0's walk
-    for (uint32_t c0 = 0; c0 < s.n_sb; c0 += per) {
-        const uint32_t nc = min(per, s.n_sb - c0);
+    for (uint32_t c0 = 0; c0 < s.n_ss; c0 += per) {
+        const uint32_t nc = min(per, s.n_ss - c0);
         __syncthreads();
-        const uint2* src = s.sb_map + (uint64_t)c0 * s.W;
-        for (uint32_t k = threadIdx.x; k < nc * s.W; k += kThreads) m[k] = src[k];
+        stage_maps(s.ss_map + (uint64_t)c0 * s.W, nc * s.W, m);
         __syncthreads();
         if (threadIdx.x == 0) {
             for (uint32_t k = 0; k < nc; ++k) {
-                s.sb_entry[c0 + k] = make_uint2(entry, taken);
+                s.ss_entry[c0 + k] = make_uint2(entry, taken);
                 if (entry != kMapStop) {
                     const uint2 v = m[k * s.W + entry];
                     taken += v.y;
@@ -195,64 +248,106 @@ __global__ void __launch_bounds__(kThreads) ring_chain_kernel(const Scan s) {
     }
 }
 
-// 4. Tile blockIdx.x: its entry, then its records.
-__global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
-    __shared__ __align__(16) uint32_t dw[kTile];
-    __shared__ uint32_t r_off[kTile / 2];
-    __shared__ uint16_t r_len[kTile / 2];
-    __shared__ uint32_t s_entry, s_base, s_cnt;
-    const uint32_t t = blockIdx.x;
-    const uint32_t n = s.info->n_frames;
-    if (threadIdx.x == 0) {
-        const uint32_t sb = t / s.S;
-        const uint2 e = s.sb_entry[sb];
-        uint32_t entry = e.x, base = e.y;
-        for (uint32_t k = sb * s.S; k < t && entry != kMapStop && base <= n; ++k) {
-            const uint2 v = s.tile_map[(uint64_t)k * s.W + entry];
+// 4. Entries one level down: thread p follows the maps of parent p's (up to S) children from the
+// parent's entry, writing each child's entry and the records before it.
+__global__ void __launch_bounds__(kThreads) ring_expand_kernel(const uint2* parent_entry, uint32_t n_parent,
+                                                               const uint2* child_map, uint32_t n_child,
+                                                               uint2* child_entry, uint32_t W, uint32_t S) {
+    const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= n_parent) return;
+    const uint2 e = parent_entry[p];
+    uint32_t entry = e.x, base = e.y;
+    const uint32_t c1 = min((p + 1) * S, n_child);
+    for (uint32_t k = p * S; k < c1; ++k) {
+        child_entry[k] = make_uint2(entry, base);
+        if (entry != kMapStop) {
+            const uint2 v = child_map[(uint64_t)k * W + entry];
             base += v.y;
             entry = v.x;
         }
-        s_entry = entry;
-        s_base = base;
-    }
-    __syncthreads();
-    const uint32_t entry = s_entry, base = s_base;
-    if (entry == kMapStop || base > n) return;
-    load_tile(s, t, dw);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t total = *s.total;
-        uint32_t q = entry, k = base, c = 0, max_len = 0;
-        while (q < kTile) {
-            uint32_t why = HALO_RING_STOP_EMPTY;
-            const uint32_t step = record_dwords(s, t * kTile + q, dw[q], why);
-            if (k == n || !step) {
-                // the walk ends at this record: say why, unless max_frames cut it (MAX, set)
-                if (!step && n == total) s.info->stop = why;
-                break;
-            }
-            r_off[c] = t * kTile + q + 1;
-            r_len[c] = (uint16_t)dw[q];
-            max_len = max(max_len, dw[q]);
-            ++c;
-            ++k;
-            q += step;
-            if (k == n) s.info->end_bytes = 4ull * (t * kTile + q);
-        }
-        s_cnt = c;
-        if (max_len) atomicMax(&s.info->max_len, max_len);
-    }
-    __syncthreads();
-    const uint32_t c = s_cnt;
-    for (uint32_t j = threadIdx.x; j < c; j += kThreads) {
-        s.off_dw[base + j] = r_off[j];
-        s.lens[base + j] = r_len[j];
     }
 }
 
+// 5. Emit: one wave per tile. The lanes tabulate every position's next record position (or its
+// stop reason) in LDS; lane 0 follows the chain from the tile's entry (one dependent LDS read per
+// record); the lanes then write the records' (offset, length) pairs.
+constexpr uint32_t kEmitWaves = kThreads / 64;
+__global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
+    __shared__ uint16_t nxt[kEmitWaves][kTile];
+    __shared__ uint16_t list[kEmitWaves][kTile / 2];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t t = blockIdx.x * kEmitWaves + w;
+    if (t >= s.n_tiles) return;  // wave-uniform
+    const uint32_t n = s.info->n_frames;
+    const uint2 te = s.tile_entry[t];
+    const uint32_t entry = te.x, base = te.y;
+    if (entry == kMapStop || base > n) return;  // wave-uniform
+    const uint32_t tbase = t * kTile;
+    // the wave's 16 KB in two rounds of eight 16-byte loads in flight per lane
+    const bool whole = tbase + kTile <= s.n_dw;  // wave-uniform
+    for (uint32_t r0 = 0; r0 < kTile; r0 += 8 * 4 * 64) {
+        uint4 v[8];
+        if (whole) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + tbase + r0 + 4 * (lane + 64 * u));
+                v[u] = make_uint4(x.x, x.y, x.z, x.w);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = span_quad(s, tbase + r0 + 4 * (lane + 64 * u));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t q = r0 + 4 * (lane + 64 * u);
+            const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t why;
+                const uint32_t step = record_dwords(s, tbase + q + j, d[j], why);
+                nxt[w][q + j] = (uint16_t)(step ? q + j + step : (kLdsStop | why));
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // the walk: every lane follows the same chain (values made scalar), so the loop is uniform
+    // control flow around one dependent LDS read per record
+    const uint32_t limit = min(n - base, kTile / 2);  // records this tile may still take
+    uint32_t c = 0, q = entry, v = 0;
+    while (c < limit && q < kTile) {
+        v = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt[w][q]);
+        if (v & kLdsStop) break;
+        list[w][c++] = (uint16_t)q;
+        q = v;
+    }
+    if (lane == 0) {
+        if (base + c == n && c) s.info->end_bytes = 4ull * (tbase + q);
+        // where the walk ends inside this tile: say why, unless max_frames cut it (MAX, set)
+        if (q < kTile && n == *s.total) {
+            if (c == limit) v = nxt[w][q];
+            if (v & kLdsStop) s.info->stop = v & 0xFFu;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t max_len = 0;
+    for (uint32_t j = lane; j < c; j += 64) {
+        const uint32_t a = tbase + list[w][j];
+        const uint32_t len = s.span[a];
+        s.off_dw[base + j] = a + 1;
+        s.lens[base + j] = (uint16_t)len;
+        max_len = max(max_len, len);
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) max_len = max(max_len, (uint32_t)__shfl_xor((int)max_len, m, 64));
+    if (lane == 0 && max_len) atomicMax(&s.info->max_len, max_len);
+}
+
 struct Geom {
-    uint32_t n_dw, n_tiles, W, S, n_sb;
-    uint64_t tile_map_off, sb_map_off, sb_entry_off, total_off, bytes;
+    uint32_t n_dw, n_tiles, W, S, n_sb, n_ss;
+    uint64_t tile_map_off, sb_map_off, ss_map_off, ss_entry_off, sb_entry_off, tile_entry_off, total_off, bytes;
 };
 
 Geom geometry(uint64_t used, uint32_t cap) {
@@ -262,13 +357,20 @@ Geom geometry(uint64_t used, uint32_t cap) {
     g.W = (cap + 7) / 4;  // ceil((4 + cap) / 4)
     g.S = std::max<uint32_t>(1, kMapLds / g.W);
     g.n_sb = (g.n_tiles + g.S - 1) / g.S;
+    g.n_ss = (g.n_sb + g.S - 1) / g.S;
     uint64_t o = 0;
     g.tile_map_off = o;
     o += (uint64_t)g.n_tiles * g.W * sizeof(uint2);
     g.sb_map_off = o;
     o += (uint64_t)g.n_sb * g.W * sizeof(uint2);
+    g.ss_map_off = o;
+    o += (uint64_t)g.n_ss * g.W * sizeof(uint2);
+    g.ss_entry_off = o;
+    o += (uint64_t)g.n_ss * sizeof(uint2);
     g.sb_entry_off = o;
     o += (uint64_t)g.n_sb * sizeof(uint2);
+    g.tile_entry_off = o;
+    o += (uint64_t)g.n_tiles * sizeof(uint2);
     g.total_off = o;
     o += 256;
     g.bytes = o;
@@ -285,11 +387,15 @@ Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_
     s.W = g.W;
     s.S = g.S;
     s.n_sb = g.n_sb;
-    s.max_frames = max_frames ? max_frames : 0xFFFFFFFFu;
+    s.n_ss = g.n_ss;
+    s.max_frames = max_frames;  // 0: no frame may be taken
     s.half = ring_size / 2;
     s.tile_map = reinterpret_cast<uint2*>(ws + g.tile_map_off);
     s.sb_map = reinterpret_cast<uint2*>(ws + g.sb_map_off);
+    s.ss_map = reinterpret_cast<uint2*>(ws + g.ss_map_off);
+    s.ss_entry = reinterpret_cast<uint2*>(ws + g.ss_entry_off);
     s.sb_entry = reinterpret_cast<uint2*>(ws + g.sb_entry_off);
+    s.tile_entry = reinterpret_cast<uint2*>(ws + g.tile_entry_off);
     s.total = reinterpret_cast<uint32_t*>(ws + g.total_off);
     s.info = d_info;
     s.off_dw = d_off;
@@ -303,9 +409,15 @@ int launch_tile_maps(const Scan& s, uint32_t t0, uint32_t t1, hipStream_t st) {
 }
 
 int launch_finish(const Scan& s, hipStream_t st) {
-    hipLaunchKernelGGL(ring_sb_compose_kernel, dim3(s.n_sb), dim3(kThreads), 0, st, s);
-    hipLaunchKernelGGL(ring_chain_kernel, dim3(1), dim3(kThreads), 0, st, s);
-    hipLaunchKernelGGL(ring_emit_kernel, dim3(s.n_tiles), dim3(kThreads), 0, st, s);
+    const dim3 blk(kThreads);
+    hipLaunchKernelGGL(ring_compose_kernel, dim3(s.n_sb), blk, 0, st, s.tile_map, s.n_tiles, s.sb_map, s.W, s.S);
+    hipLaunchKernelGGL(ring_compose_kernel, dim3(s.n_ss), blk, 0, st, s.sb_map, s.n_sb, s.ss_map, s.W, s.S);
+    hipLaunchKernelGGL(ring_chain_kernel, dim3(1), blk, 0, st, s);
+    hipLaunchKernelGGL(ring_expand_kernel, dim3((s.n_ss + kThreads - 1) / kThreads), blk, 0, st, s.ss_entry, s.n_ss,
+                       s.sb_map, s.n_sb, s.sb_entry, s.W, s.S);
+    hipLaunchKernelGGL(ring_expand_kernel, dim3((s.n_sb + kThreads - 1) / kThreads), blk, 0, st, s.sb_entry, s.n_sb,
+                       s.tile_map, s.n_tiles, s.tile_entry, s.W, s.S);
+    hipLaunchKernelGGL(ring_emit_kernel, dim3((s.n_tiles + kEmitWaves - 1) / kEmitWaves), dim3(kThreads), 0, st, s);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 
@@ -351,8 +463,8 @@ struct halo_rx_ring {
     uint64_t max_bytes = 0;
     bool registered = false;
     Geom g{};                 // workspace geometry for max_bytes
-    hipStream_t s_copy = nullptr, s_comp = nullptr;
-    std::vector<hipEvent_t> ev;
+    hipStream_t s_copy = nullptr, s_comp = nullptr, s_d2h = nullptr;
+    std::vector<hipEvent_t> ev;  // per piece: copy landed, parse done
     uint8_t* d_span = nullptr;
     uint8_t* d_ws = nullptr;
     uint32_t* d_off = nullptr;
@@ -370,6 +482,7 @@ void free_ring(halo_rx_ring* r) {
         if (e) (void)hipEventDestroy(e);
     if (r->s_copy) (void)hipStreamDestroy(r->s_copy);
     if (r->s_comp) (void)hipStreamDestroy(r->s_comp);
+    if (r->s_d2h) (void)hipStreamDestroy(r->s_d2h);
     if (r->d_span) (void)hipFree(r->d_span);
     if (r->d_ws) (void)hipFree(r->d_ws);
     if (r->d_off) (void)hipFree(r->d_off);
@@ -407,8 +520,8 @@ extern "C" HALO_API int halo_rx_ring_scan_device(const uint8_t* d_span, uint64_t
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (used == 0)
         return hipMemsetAsync(d_info, 0, sizeof(halo_rx_ring_scan_t), st) == hipSuccess ? HALO_OK : HALO_E_HIP;
-    const Scan s = halo::make_scan(g, d_span, ring_size, capacity, max_frames, static_cast<uint8_t*>(d_workspace),
-                                   d_info, d_offsets_dw, d_lens);
+    const Scan s = halo::make_scan(g, d_span, ring_size, capacity, max_frames ? max_frames : 0xFFFFFFFFu,
+                                   static_cast<uint8_t*>(d_workspace), d_info, d_offsets_dw, d_lens);
     if ((rc = halo::launch_tile_maps(s, 0, g.n_tiles, st))) return rc;
     return halo::launch_finish(s, st);
 }
@@ -440,12 +553,11 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     r->cap = capacity;
     r->max_frames = max_frames;
     r->max_bytes = max_bytes;
-    r->g = halo::geometry(max_bytes, capacity);
-    const size_t n_ev = (size_t)((max_bytes + halo::kPieceBytes - 1) / halo::kPieceBytes) +
-                        (max_frames + halo::kParseChunk - 1) / halo::kParseChunk;
-    r->ev.assign(n_ev, nullptr);
+    r->g = halo::geometry(std::min<uint64_t>(max_bytes, halo::kPieceBytes + 4ull * halo::kTile), capacity);  // a piece + a cut record
+    r->ev.assign(2 * (size_t)((max_bytes + halo::kPieceBytes - 1) / halo::kPieceBytes), nullptr);
     bool ok = hipStreamCreateWithFlags(&r->s_copy, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&r->s_comp, hipStreamNonBlocking) == hipSuccess;
+              hipStreamCreateWithFlags(&r->s_comp, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&r->s_d2h, hipStreamNonBlocking) == hipSuccess;
     for (auto& e : r->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipMalloc((void**)&r->d_span, max_bytes + 16) == hipSuccess;
     ok = ok && hipMalloc((void**)&r->d_ws, r->g.bytes) == hipSuccess;
@@ -474,10 +586,16 @@ extern "C" HALO_API int halo_rx_ring_detach(halo_rx_ring_t* r) {
     (void)hipSetDevice(r->device);
     if (r->s_copy) (void)hipStreamSynchronize(r->s_copy);
     if (r->s_comp) (void)hipStreamSynchronize(r->s_comp);
+    if (r->s_d2h) (void)hipStreamSynchronize(r->s_d2h);
     free_ring(r);
     return HALO_OK;
 }
 
+// One poll, pipelined over 16 MiB pieces of the span: every piece's H2D copy is queued at once on
+// the copy stream; piece k is then walked from the record boundary where piece k-1's walk ended
+// (a record crossing a piece end is simply PARTIAL there and taken with the next piece), parsed
+// where it lies and its records copied back on a third stream — so the walk, the parse and the
+// record copies of piece k overlap the transfer of the pieces after it.
 extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, const halo_rx_netif_t* netif,
                                           halo_rx_result_t* out, uint32_t* status_hist, uint64_t* positions,
                                           halo_rx_ring_scan_t* info) {
@@ -493,18 +611,14 @@ extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, con
     }
     used = std::min(used, r->max_bytes) & ~3ull;
     if (used == 0) return HALO_OK;  // EMPTY
-    const Geom g = halo::geometry(used, r->cap);
-    const Scan s = halo::make_scan(g, r->d_span, r->size, r->cap, r->max_frames, r->d_ws, r->d_info, r->d_off,
-                                   r->d_len);
-    // DMA the span piece by piece; each piece's tile maps start as soon as it has landed
     const uint64_t mask = r->size - 1, pos = r->cursor & mask;
-    uint32_t tiles_done = 0;
-    size_t k = 0;
+    const uint32_t n_pieces = (uint32_t)((used + halo::kPieceBytes - 1) / halo::kPieceBytes);
     int rc = HALO_OK;
-    for (uint64_t b0 = 0; b0 < used && rc == HALO_OK; b0 += halo::kPieceBytes, ++k) {
-        const uint64_t b1 = std::min(used, b0 + halo::kPieceBytes);
+    // 1. every piece's copy, in order, on the copy stream
+    for (uint32_t k = 0; k < n_pieces && rc == HALO_OK; ++k) {
+        const uint64_t b0 = (uint64_t)k * halo::kPieceBytes, b1 = std::min(used, b0 + halo::kPieceBytes);
         uint64_t src = (pos + b0) & mask, len = b1 - b0, dst = b0;
-        while (len && rc == HALO_OK) {  // at most two pieces: up to the end of the data area, then from 0
+        while (len && rc == HALO_OK) {  // up to the end of the data area, then from its start
             const uint64_t c = std::min(len, r->size - src);
             if (hipMemcpyAsync(r->d_span + dst, r->data + src, c, hipMemcpyHostToDevice, r->s_copy) != hipSuccess)
                 rc = HALO_E_HIP;
@@ -512,50 +626,65 @@ extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, con
             len -= c;
             src = 0;
         }
-        if (rc) break;
-        if (hipEventRecord(r->ev[k], r->s_copy) != hipSuccess || hipStreamWaitEvent(r->s_comp, r->ev[k], 0) != hipSuccess)
-            rc = HALO_E_HIP;
-        const uint32_t t1 = b1 == used ? g.n_tiles : (uint32_t)(b1 / (4ull * halo::kTile));
-        if (!rc) rc = halo::launch_tile_maps(s, tiles_done, t1, r->s_comp);
-        tiles_done = t1;
+        if (!rc && hipEventRecord(r->ev[2 * k], r->s_copy) != hipSuccess) rc = HALO_E_HIP;
     }
-    if (!rc) rc = halo::launch_finish(s, r->s_comp);
-    if (!rc && hipMemcpyAsync(r->h_info, r->d_info, sizeof *info, hipMemcpyDeviceToHost, r->s_comp) != hipSuccess)
-        rc = HALO_E_HIP;
-    if (hipStreamSynchronize(r->s_comp) != hipSuccess && !rc) rc = HALO_E_HIP;
-    if (rc) {
-        (void)hipStreamSynchronize(r->s_copy);
-        return rc;
+    // 2. walk, parse and return piece by piece
+    uint64_t off = 0;         // span bytes consumed: the record boundary the next walk starts at
+    uint32_t done = 0;        // frames taken
+    std::vector<std::pair<uint32_t, uint64_t>> spans;  // (first frame, span offset) per piece (positions)
+    for (uint32_t k = 0; k < n_pieces && rc == HALO_OK; ++k) {
+        const uint64_t avail = std::min(used, (uint64_t)(k + 1) * halo::kPieceBytes) - off;
+        if (hipStreamWaitEvent(r->s_comp, r->ev[2 * k], 0) != hipSuccess) { rc = HALO_E_HIP; break; }
+        const Geom g = halo::geometry(avail, r->cap);
+        const Scan sc = halo::make_scan(g, r->d_span + off, r->size, r->cap, r->max_frames - done, r->d_ws, r->d_info,
+                                        r->d_off + done, r->d_len + done);
+        if ((rc = halo::launch_tile_maps(sc, 0, g.n_tiles, r->s_comp)) || (rc = halo::launch_finish(sc, r->s_comp))) break;
+        if (hipMemcpyAsync(r->h_info, r->d_info, sizeof *info, hipMemcpyDeviceToHost, r->s_comp) != hipSuccess ||
+            hipStreamSynchronize(r->s_comp) != hipSuccess) { rc = HALO_E_HIP; break; }
+        const halo_rx_ring_scan_t pi = *r->h_info;
+        if (pi.n_frames) {
+            spans.emplace_back(done, off);
+            rc = halo_rx_parse_batch_device(r->d_span + off, r->d_off + done, r->d_len + done, pi.n_frames, flags,
+                                            netif, pi.max_len, r->d_res + done, status_hist ? r->d_hist : nullptr,
+                                            r->s_comp);
+            if (rc) break;
+            if (hipEventRecord(r->ev[2 * k + 1], r->s_comp) != hipSuccess ||
+                hipStreamWaitEvent(r->s_d2h, r->ev[2 * k + 1], 0) != hipSuccess ||
+                hipMemcpyAsync(out + done, r->d_res + done, sizeof(halo_rx_result_t) * pi.n_frames,
+                               hipMemcpyDeviceToHost, r->s_d2h) != hipSuccess) { rc = HALO_E_HIP; break; }
+        }
+        done += pi.n_frames;
+        off += pi.end_bytes;
+        info->max_len = std::max(info->max_len, pi.max_len);
+        info->stop = pi.stop;
+        // a record cut by the piece's end (PARTIAL) or a piece ending on a record boundary
+        // (EMPTY) continues with the next piece; anything else ends the walk
+        if (pi.stop != HALO_RING_STOP_PARTIAL && pi.stop != HALO_RING_STOP_EMPTY) break;
     }
-    *info = *r->h_info;
-    const uint32_t n = info->n_frames;
-    // parse the frames where they lie; the records of chunk c copy back while chunk c+1 parses
-    for (uint32_t f0 = 0; f0 < n && rc == HALO_OK; f0 += halo::kParseChunk, ++k) {
-        const uint32_t cnt = std::min(halo::kParseChunk, n - f0);
-        rc = halo_rx_parse_batch_device(r->d_span, r->d_off + f0, r->d_len + f0, cnt, flags, netif, info->max_len,
-                                        r->d_res + f0, status_hist ? r->d_hist : nullptr, r->s_comp);
-        if (rc) break;
-        if (hipEventRecord(r->ev[k], r->s_comp) != hipSuccess || hipStreamWaitEvent(r->s_copy, r->ev[k], 0) != hipSuccess ||
-            hipMemcpyAsync(out + f0, r->d_res + f0, sizeof(halo_rx_result_t) * cnt, hipMemcpyDeviceToHost,
-                           r->s_copy) != hipSuccess)
-            rc = HALO_E_HIP;
-    }
-    if (!rc && positions && n &&
-        hipMemcpyAsync(r->h_off, r->d_off, 4ull * n, hipMemcpyDeviceToHost, r->s_copy) != hipSuccess)
+    if (!rc && positions && done &&
+        hipMemcpyAsync(r->h_off, r->d_off, 4ull * done, hipMemcpyDeviceToHost, r->s_d2h) != hipSuccess)
         rc = HALO_E_HIP;
     if (hipStreamSynchronize(r->s_copy) != hipSuccess && !rc) rc = HALO_E_HIP;
     if (hipStreamSynchronize(r->s_comp) != hipSuccess && !rc) rc = HALO_E_HIP;
+    if (hipStreamSynchronize(r->s_d2h) != hipSuccess && !rc) rc = HALO_E_HIP;
     if (rc) return rc;
-    if (positions)
-        for (uint32_t i = 0; i < n; ++i) positions[i] = r->cursor + 4ull * (r->h_off[i] - 1u);
-    if (status_hist && n) {
+    if (positions) {
+        for (size_t j = 0; j < spans.size(); ++j) {
+            const uint32_t f1 = j + 1 < spans.size() ? spans[j + 1].first : done;
+            for (uint32_t i = spans[j].first; i < f1; ++i)
+                positions[i] = r->cursor + spans[j].second + 4ull * (r->h_off[i] - 1u);
+        }
+    }
+    if (status_hist && done) {
         uint32_t h[HALO_RX_STATUS_COUNT];
         if (hipMemcpy(h, r->d_hist, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemset(r->d_hist, 0, sizeof h) != hipSuccess)
             return HALO_E_HIP;
         for (int j = 0; j < HALO_RX_STATUS_COUNT; ++j) status_hist[j] += h[j];
     }
-    r->cursor += info->end_bytes;
+    info->n_frames = done;
+    info->end_bytes = off;
+    r->cursor += off;
     return HALO_OK;
 }
 
