@@ -139,6 +139,8 @@ def bench_lib():
         L.halo_bench_xxh3_steps.restype = ctypes.c_int
         L.halo_bench_xxh3_steps.argtypes = [i32, vp, vp, vp, u32, vp] + tail
         u64 = ctypes.c_uint64
+        L.halo_bench_read_peak.restype = ctypes.c_int
+        L.halo_bench_read_peak.argtypes = [vp, u64, vp] + tail
         L.halo_bench_ring_scan_steps.restype = ctypes.c_int
         L.halo_bench_ring_scan_steps.argtypes = [i32, vp, u64, u64, u32, vp, vp, vp, vp, u64] + tail
         _BENCH_LIB = L
@@ -494,10 +496,35 @@ def ring_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = False):
     return res
 
 
+MEASURED_READ_GBS = None  # set by measure_read_peak() on this box
+
+
+def measure_read_peak(dev, d: Dist, gib: int = 2):
+    """A read-only streaming kernel over `gib` GiB (8x the Infinity Cache): this box's achievable
+    HBM read bandwidth, the second peak SURVEY.md §8d asks the roofline to be reported against."""
+    import torch
+
+    global MEASURED_READ_GBS
+    nbytes = gib << 30
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    buf.fill_(1)
+    sink = torch.zeros(256 * 16, dtype=torch.int32, device=dev)
+    w, k = time_native(bench_lib().halo_bench_read_peak, buf.data_ptr(), nbytes, sink.data_ptr(), steps=20,
+                       warmup=3, d=d)
+    MEASURED_READ_GBS = round(nbytes / (k * 1e-3) / 1e9, 1)
+    del buf
+    torch.cuda.empty_cache()
+    return MEASURED_READ_GBS
+
+
 def roofline(alg_bytes_per_launch, kernel_ms, traffic=None):
     achieved = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+    if MEASURED_READ_GBS:
+        r["peak_measured_read"] = MEASURED_READ_GBS
+        r["frac_of_measured"] = round(achieved / MEASURED_READ_GBS, 4)
+    return r
 
 
 def load_traffic(workload: str):
@@ -603,6 +630,7 @@ def main():
 
     _lib.check("halo_rx_init", _lib.lib.halo_rx_init(gpu))
     netif = NetIf.make()  # eth0 of example.UsePcapDev (example/example.go:768-773)
+    measure_read_peak(dev, d)
     n = args.frames
 
     log(f"[rank {d.rank}] generating {args.rotate} x {n} frames of 64 B")

@@ -142,3 +142,41 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_ring_scan_steps
     };
     return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
 }
+
+// Measured streaming-read ceiling (the roofline is reported against the HBM3E spec
+// peak AND a read-only streaming kernel on the same box): every 16-byte chunk of `bytes` read once
+// with fully coalesced loads, 8 in flight per lane, folded into one word per block so nothing is
+// optimised away. Not part of the product library.
+namespace {
+__global__ void __launch_bounds__(256) read_peak_kernel(const uint4* __restrict__ src, uint64_t n16,
+                                                        uint32_t* __restrict__ sink) {
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 7 * stride < n16; i += 8 * stride) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    for (; i < n16; i += stride) {
+        const uint4 v = src[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;  // practically never: keeps the loads live
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_read_peak(const void* buf, uint64_t bytes,
+                                                                            uint32_t* sink, int warmup, int steps,
+                                                                            void* stream, float* region_ms,
+                                                                            double* wall_s) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto launch = [&](int) {
+        hipLaunchKernelGGL(read_peak_kernel, dim3(256 * 16), dim3(256), 0, s, static_cast<const uint4*>(buf),
+                           bytes / 16, sink);
+        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+    };
+    return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
+}
