@@ -309,7 +309,10 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
                                              uint4* stage = nullptr) {
     constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
     constexpr int U0 = kRound0<G>;    // chunks already loaded
-    constexpr int U = 4;              // 16-byte chunks in flight per lane per later round
+#ifndef HALO_RX_LATER_CHUNKS
+#define HALO_RX_LATER_CHUNKS 8
+#endif
+    constexpr int U = HALO_RX_LATER_CHUNKS;  // 16-byte chunks in flight per lane per later round
     uint32_t h[12];
     frame_header<G>(st, grp_base, h);
     Verdict v = parse_header(h, st.L, present, p);
@@ -410,8 +413,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) rx_l
 }
 
 // G lanes per frame (G in {4, 8, 16}); VGPR-limited occupancy, so no SGPR cap.
+#ifndef HALO_RX_GROUP_WAVES
+#define HALO_RX_GROUP_WAVES 5
+#endif
 template <int G, int LAYOUT>
-__global__ void __launch_bounds__(256) rx_group_kernel(const RxParams p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_RX_GROUP_WAVES)))
+rx_group_kernel(const RxParams p) {
     static_assert(G == 4 || G == 8 || G == 16, "G must be 4, 8 or 16");
     group_kernel_body<G, LAYOUT>(p);
 }
@@ -422,7 +429,11 @@ __global__ void __launch_bounds__(256) rx_group_kernel(const RxParams p) {
 // the uniform sweep found best for that size: <= 128 B (and frames failing the length check)
 // lane per frame, <= 1024 B 4 lanes, <= 4096 B 8 lanes, longer 16 lanes. Every pass keeps all
 // groups busy with frames of one class, so no lane waits behind a longer neighbour.
-constexpr uint32_t kMixWindow = 256;
+#ifndef HALO_RX_MIX_WINDOW
+#define HALO_RX_MIX_WINDOW 256
+#endif
+constexpr uint32_t kMixWindow = HALO_RX_MIX_WINDOW;  // frames per wave window (a multiple of 64)
+constexpr int kMixPer = (int)(kMixWindow / 64);      // frames per lane in the classification
 
 template <int G>
 __device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, uint32_t e_end, uint32_t lane,
@@ -444,7 +455,10 @@ __device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, ui
 }
 
 template <int LAYOUT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) rx_mix_kernel(const RxParams p) {
+#ifndef HALO_RX_MIX_WAVES
+#define HALO_RX_MIX_WAVES 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_RX_MIX_WAVES))) rx_mix_kernel(const RxParams p) {
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     __shared__ uint64_t s_ptr[4][kMixWindow];
     __shared__ uint32_t s_idx[4][kMixWindow];
@@ -458,11 +472,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) r
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t base = wave * kMixWindow; base < p.n; base += nwaves * kMixWindow) {
-        // classify: frame base + 64k + lane, k = 0..3
-        const uint8_t* fp[4];
-        uint32_t fl[4], cls[4];
+        // classify: frame base + 64k + lane, k < kMixPer
+        const uint8_t* fp[kMixPer];
+        uint32_t fl[kMixPer], cls[kMixPer];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kMixPer; ++k) {
             const uint32_t i = base + 64 * k + lane;
             fp[k] = p.bytes;
             fl[k] = 0;
@@ -472,14 +486,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) r
                    : fl[k] <= 1024 ? 1u : fl[k] <= 4096 ? 2u : 3u;
         }
         // counting sort by class: one ballot live at a time
-        uint32_t pos[4] = {0, 0, 0, 0};
+        uint32_t pos[kMixPer];
         uint32_t start[5];
         uint32_t run = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             start[c] = run;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < kMixPer; ++k) {
                 const uint64_t b = __ballot(cls[k] == (uint32_t)c);
                 if (cls[k] == (uint32_t)c)
                     pos[k] = run + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
@@ -489,7 +503,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) r
         }
         start[4] = run;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kMixPer; ++k) {
             if (cls[k] < 4u) {
                 s_ptr[w][pos[k]] = reinterpret_cast<uint64_t>(fp[k]);
                 s_idx[w][pos[k]] = base + 64 * k + lane;
