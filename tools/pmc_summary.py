@@ -56,6 +56,8 @@ def alg_bytes():
 
 
 def main():
+    if len(sys.argv) < 2 or not os.path.isdir(sys.argv[1]):
+        sys.exit(__doc__)
     sess = sys.argv[1]
     out_path = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else os.path.join(
         ROOT, "profiles", "pmc_summary.json")
