@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 
 #include "halo_rx.h"
 
@@ -148,21 +149,24 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_ring_scan_steps
 // with fully coalesced loads, 8 in flight per lane, folded into one word per block so nothing is
 // optimised away. Not part of the product library.
 namespace {
+// Each block streams whole 64 KB tiles (tile = blockIdx.x + k * gridDim.x): 16 loads of 16 bytes per
+// thread per tile, issued 8 at a time, consecutive threads on consecutive chunks — DRAM pages are
+// swept in order, as a group of lanes sweeps a long frame.
 __global__ void __launch_bounds__(256) read_peak_kernel(const uint4* __restrict__ src, uint64_t n16,
                                                         uint32_t* __restrict__ sink) {
+    constexpr uint32_t kTile16 = 4096;  // 64 KB
     uint32_t acc = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 7 * stride < n16; i += 8 * stride) {
-        uint4 v[8];
+    const uint64_t tiles = n16 / kTile16;
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const uint4* p = src + t * kTile16 + threadIdx.x;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = src[i + u * stride];
+        for (int h = 0; h < 2; ++h) {
+            uint4 v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-    }
-    for (; i < n16; i += stride) {
-        const uint4 v = src[i];
-        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+            for (int u = 0; u < 8; ++u) v[u] = p[(h * 8 + u) * 256];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
     }
     if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;  // practically never: keeps the loads live
 }
@@ -173,8 +177,10 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_read_peak(const
                                                                             void* stream, float* region_ms,
                                                                             double* wall_s) {
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const char* gb = getenv("HALO_READ_PEAK_BLOCKS");  // measurement tooling knob
+    const uint32_t grid_blocks = gb ? (uint32_t)atoi(gb) : 256u * 32u;  // best of 1k..8k blocks (tools/exp/read_peak_sweep.sh)
     auto launch = [&](int) {
-        hipLaunchKernelGGL(read_peak_kernel, dim3(256 * 16), dim3(256), 0, s, static_cast<const uint4*>(buf),
+        hipLaunchKernelGGL(read_peak_kernel, dim3(grid_blocks), dim3(256), 0, s, static_cast<const uint4*>(buf),
                            bytes / 16, sink);
         return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
     };
