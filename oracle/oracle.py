@@ -110,6 +110,10 @@ def lib() -> ctypes.CDLL:
                                              vp]
         L.ora_ring_scan.restype = u32
         L.ora_ring_scan.argtypes = [vp, u64, u64, u32, u32, vp, vp, u32p, u64p, u32p]
+        L.ora_fuzz_layout.restype = u64
+        L.ora_fuzz_layout.argtypes = [u64, u32, vp, vp]
+        L.ora_fuzz_fill.restype = None
+        L.ora_fuzz_fill.argtypes = [u64, u32, vp, vp, ctypes.POINTER(NetIf), vp]
         _lib = L
     return _lib
 
@@ -358,3 +362,13 @@ def ring_scan(span: np.ndarray, used: int, ring_size: int, capacity: int = 1514,
     n = lib().ora_ring_scan(_p(span), used, ring_size, capacity, max_frames, _p(off), _p(lens), ctypes.byref(stop),
                             ctypes.byref(end), ctypes.byref(ml))
     return off[:n], lens[:n], int(stop.value), int(end.value), int(ml.value)
+
+
+def fuzz_batch(seed: int, n: int, netif: NetIf):
+    """(data, offsets_dw, lens) of n structured-fuzz frames (halo_fuzz.c), 4-byte aligned."""
+    lens = np.zeros(n, np.uint16)
+    offs = np.zeros(n, np.uint32)
+    total_dw = lib().ora_fuzz_layout(seed, n, _p(lens), _p(offs))
+    data = np.zeros(max(16, 4 * total_dw), np.uint8)
+    lib().ora_fuzz_fill(seed, n, _p(lens), _p(offs), netif, _p(data))
+    return data, offs, lens
