@@ -472,8 +472,10 @@ def ring_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = False):
             times.append(el)
     el = float(np.median(times))
     res["config1_wire_1k_64B"] = {"frames": m, "mpps": round(m / el / 1e6, 3), "us_per_batch": round(el * 1e6, 1),
-                                  "what": "engine.Wire ring (8 MiB), 1k x 64 B UDP, GPU poll + commit per batch "
-                                          "(latency-bound: ~6 dependent launches + 3 copies)"}
+                                  "what": "engine.Wire ring (8 MiB), 1k x 64 B UDP, GPU poll + commit per batch, median "
+                                          "(small path: the host reads the 1k length fields, one rx launch parses "
+                                          "the frames in place in the registered ring over PCIe and writes the "
+                                          "records into the registered result array)"}
     wcons.close()
     if with_cpu:
         from oracle import oracle as O

@@ -165,6 +165,7 @@ _PROTOS = {
     "halo_rx_ring_poll": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p, _u8p, _u8p]),
     "halo_rx_ring_commit": (ctypes.c_int, [ctypes.c_void_p]),
+    "halo_rx_ring_set_small_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "halo_rx_ring_scan_workspace": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32]),
     "halo_rx_ring_scan_device": (ctypes.c_int, [
         _u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, _u8p,

@@ -49,6 +49,8 @@ constexpr uint32_t kMaxCapacity = 4 * kTile - 8; // the longest record must fit 
 constexpr uint32_t kRbHeader = 128;              // sizeof(RingBuffer), mem/ring_buffer.go:18-26
 constexpr uint64_t kMaxSpan = (16ull << 30) - (64ull << 10);  // dword offsets stay below 2^32
 constexpr uint64_t kPieceBytes = 16ull << 20;    // DMA piece (1024 tiles) whose maps start on arrival
+constexpr uint64_t kSmallPoll = 4ull << 20;      // default: polls up to this size take the small path
+constexpr uint64_t kSmallPollMax = 16ull << 20;
 
 struct Scan {
     const uint32_t* span;   // the ring bytes [tail, tail + used) in stream order, as dwords
@@ -474,6 +476,20 @@ struct halo_rx_ring {
     halo_rx_ring_scan_t* d_info = nullptr;
     halo_rx_ring_scan_t* h_info = nullptr;  // pinned
     uint32_t* h_off = nullptr;              // pinned
+    // small path (registered rings): the ring's data area as the device sees it, and pinned
+    // (offset, length, record) arrays for up to small_frames frames
+    uint8_t* d_data = nullptr;
+    uint64_t small = 0;
+    uint32_t small_frames = 0;
+    uint32_t* h_soff = nullptr;
+    uint16_t* h_slen = nullptr;
+    halo_rx_result_t* h_sres = nullptr;
+    uint32_t* d_soff = nullptr;
+    uint16_t* d_slen = nullptr;
+    halo_rx_result_t* d_sres = nullptr;
+    const void* last_out = nullptr;  // the caller's record array seen last, if device-mapped
+    uint64_t last_out_bytes = 0;
+    halo_rx_result_t* last_out_dev = nullptr;
 };
 
 namespace {
@@ -492,8 +508,111 @@ void free_ring(halo_rx_ring* r) {
     if (r->d_info) (void)hipFree(r->d_info);
     if (r->h_info) (void)hipHostFree(r->h_info);
     if (r->h_off) (void)hipHostFree(r->h_off);
+    if (r->h_soff) (void)hipHostFree(r->h_soff);
+    if (r->h_slen) (void)hipHostFree(r->h_slen);
+    if (r->h_sres) (void)hipHostFree(r->h_sres);
     if (r->registered) (void)hipHostUnregister(r->mem);
     delete r;
+}
+
+// Device address of host memory [p, p + bytes) when it is pinned or registered in one piece,
+// else nullptr (the failed query's error is cleared so later launch checks do not see it).
+void* device_view(const void* p, uint64_t bytes) {
+    void *d0 = nullptr, *d1 = nullptr;
+    if (!p || !bytes) return nullptr;
+    if (hipHostGetDevicePointer(&d0, const_cast<void*>(p), 0) != hipSuccess ||
+        hipHostGetDevicePointer(&d1, const_cast<uint8_t*>(static_cast<const uint8_t*>(p)) + bytes - 1, 0) !=
+            hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t*>(d1) - static_cast<uint8_t*>(d0) == (ptrdiff_t)(bytes - 1) ? d0 : nullptr;
+}
+
+int alloc_small(halo_rx_ring* r, uint64_t bytes) {
+    const uint32_t frames = (uint32_t)std::min<uint64_t>(bytes / 8, r->max_frames);
+    if (frames > r->small_frames) {
+        if (r->h_soff) (void)hipHostFree(r->h_soff);
+        if (r->h_slen) (void)hipHostFree(r->h_slen);
+        if (r->h_sres) (void)hipHostFree(r->h_sres);
+        r->h_soff = nullptr;
+        r->h_slen = nullptr;
+        r->h_sres = nullptr;  // allocated on first use: only for callers whose array is not mapped
+        r->d_sres = nullptr;
+        r->small_frames = 0;
+        if (hipHostMalloc((void**)&r->h_soff, 4ull * frames, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&r->h_slen, 2ull * frames, hipHostMallocDefault) != hipSuccess)
+            return HALO_E_NOMEM;
+        r->d_soff = static_cast<uint32_t*>(device_view(r->h_soff, 4ull * frames));
+        r->d_slen = static_cast<uint16_t*>(device_view(r->h_slen, 2ull * frames));
+        if (!r->d_soff || !r->d_slen) return HALO_E_NOMEM;
+        r->small_frames = frames;
+    }
+    r->small = bytes;
+    return HALO_OK;
+}
+
+// The small path (BASELINE config 1: 1k-frame batches through engine.Wire). The host reads the
+// records' length fields exactly as ReadPacket does (mem/ring_buffer.go:309-335: 4 bytes per
+// record, never a frame byte); one rx launch then parses the frames where they lie in the
+// registered ring, over PCIe, and writes the records straight into the caller's array when that
+// is pinned or registered. One launch and one synchronisation replace the span DMA, the seven
+// walk launches, the info round trip and the record copies of the pipelined path, which are
+// latency, not bandwidth, at this size. Returns 1 (nothing done) when a frame wraps around the end
+// of the data area: that poll takes the pipelined path, which linearises the span.
+int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_netif_t* netif,
+               halo_rx_result_t* out, uint32_t* status_hist, uint64_t* positions, halo_rx_ring_scan_t* info) {
+    const uint64_t mask = r->size - 1, half = r->size >> 1;
+    uint64_t a = 0;
+    uint32_t n = 0, max_len = 0, stop;
+    for (;;) {
+        if (used - a < 4) { stop = HALO_RING_STOP_EMPTY; break; }
+        const uint64_t p = (r->cursor + a) & mask;
+        uint32_t len;
+        memcpy(&len, r->data + p, 4);
+        if (len == 0 || len > half) { stop = HALO_RING_STOP_BAD_LEN; break; }
+        const uint64_t bytes = (4ull + len + 3ull) & ~3ull;
+        if (used - a < bytes) { stop = HALO_RING_STOP_PARTIAL; break; }
+        if (len > r->cap) { stop = HALO_RING_STOP_CAPACITY; break; }
+        if (n == r->max_frames) { stop = HALO_RING_STOP_MAX; break; }
+        const uint64_t f = (p + 4) & mask;
+        if (f + len > r->size) return 1;
+        r->h_soff[n] = (uint32_t)(f >> 2);
+        r->h_slen[n] = (uint16_t)len;
+        if (positions) positions[n] = r->cursor + a;
+        max_len = std::max(max_len, len);
+        ++n;
+        a += bytes;
+    }
+    if (n) {
+        const uint64_t rb = sizeof(halo_rx_result_t) * (uint64_t)n;
+        halo_rx_result_t* dout = nullptr;
+        if (out == r->last_out && rb <= r->last_out_bytes) {
+            dout = r->last_out_dev;
+        } else if ((dout = static_cast<halo_rx_result_t*>(device_view(out, rb)))) {
+            r->last_out = out;
+            r->last_out_bytes = rb;
+            r->last_out_dev = dout;
+        }
+        if (!dout && !r->h_sres) {
+            const uint64_t sb = sizeof(halo_rx_result_t) * (uint64_t)r->small_frames;
+            if (hipHostMalloc((void**)&r->h_sres, sb, hipHostMallocDefault) != hipSuccess) return HALO_E_NOMEM;
+            if (!(r->d_sres = static_cast<halo_rx_result_t*>(device_view(r->h_sres, sb)))) return HALO_E_NOMEM;
+        }
+        int rc = halo_rx_parse_batch_device(r->d_data, r->d_soff, r->d_slen, n, flags, netif, max_len,
+                                            dout ? dout : r->d_sres, nullptr, r->s_comp);
+        if (rc) return rc;
+        if (hipStreamSynchronize(r->s_comp) != hipSuccess) return HALO_E_HIP;
+        if (!dout) memcpy(out, r->h_sres, rb);
+        if (status_hist)
+            for (uint32_t i = 0; i < n; ++i) ++status_hist[out[i].status];  // the statuses the kernel wrote
+    }
+    info->n_frames = n;
+    info->stop = stop;
+    info->end_bytes = a;
+    info->max_len = max_len;
+    r->cursor += a;
+    return HALO_OK;
 }
 }  // namespace
 
@@ -572,6 +691,10 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     if (ok && (attach_flags & HALO_RING_REGISTER)) {
         ok = hipHostRegister(mem, halo::kRbHeader + size, hipHostRegisterDefault) == hipSuccess;
         r->registered = ok;
+        if (ok && size <= halo::kMaxSpan + (64ull << 10)) {  // dword offsets into the data area fit u32
+            r->d_data = static_cast<uint8_t*>(device_view(r->data, size));
+            ok = !r->d_data || alloc_small(r, halo::kSmallPoll) == HALO_OK;
+        }
     }
     if (!ok) {
         free_ring(r);
@@ -611,6 +734,10 @@ extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, con
     }
     used = std::min(used, r->max_bytes) & ~3ull;
     if (used == 0) return HALO_OK;  // EMPTY
+    if (used <= r->small && r->d_data) {
+        const int rc = small_poll(r, used, flags, netif, out, status_hist, positions, info);
+        if (rc <= 0) return rc;  // 1: a frame wraps around the data area's end -> pipelined path
+    }
     const uint64_t mask = r->size - 1, pos = r->cursor & mask;
     const uint32_t n_pieces = (uint32_t)((used + halo::kPieceBytes - 1) / halo::kPieceBytes);
     int rc = HALO_OK;
@@ -686,6 +813,17 @@ extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, con
     info->end_bytes = off;
     r->cursor += off;
     return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_ring_set_small_poll(halo_rx_ring_t* r, uint64_t bytes) {
+    if (!r || bytes > halo::kSmallPollMax) return HALO_E_INVAL;
+    if (bytes && !r->d_data) return HALO_E_INVAL;  // needs a ring attached with HALO_RING_REGISTER
+    if (hipSetDevice(r->device) != hipSuccess) return HALO_E_NODEV;
+    if (!bytes) {
+        r->small = 0;
+        return HALO_OK;
+    }
+    return alloc_small(r, bytes);
 }
 
 extern "C" HALO_API int halo_rx_ring_commit(halo_rx_ring_t* r) {

@@ -90,16 +90,20 @@ class RingBuffer:
 
 class RingConsumer:
     """The GPU consumer of one ring (halo_rx_ring_attach). ``capacity`` is ReadPacket's
-    ``len(data)`` (1514 in the DPDK driver and Wire)."""
+    ``len(data)`` (1514 in the DPDK driver and Wire). ``small_poll``: spans up to this many bytes
+    take the one-launch small path (None: the library default; 0: always the pipelined path)."""
 
     def __init__(self, ring: RingBuffer, device: int = 0, capacity: int = MAX_PACKET_SIZE, max_bytes: int = 0,
-                 max_frames: int = 0, register: bool = True):
+                 max_frames: int = 0, register: bool = True, small_poll: int | None = None):
         self.ring = ring
+        self._out_registered = False
         h = ctypes.c_void_p()
         rc = _lib.lib.halo_rx_ring_attach(device, ring.mem.ctypes.data, 0, capacity, max_bytes, max_frames,
                                           RING_REGISTER if register else 0, ctypes.byref(h))
         _lib.check("halo_rx_ring_attach", rc)
         self._h = h
+        if small_poll is not None:
+            _lib.check("halo_rx_ring_set_small_poll", _lib.lib.halo_rx_ring_set_small_poll(h, small_poll))
         cap = max_bytes or min(ring.size, 256 << 20)
         self.max_frames = min(max_frames or (1 << 32) - 1, min(cap, ring.size) // 8)
         self._out = np.zeros(self.max_frames, dtype=RESULT_DTYPE)

@@ -269,6 +269,13 @@ HALO_API int halo_rx_ring_detach(halo_rx_ring_t* ring);
 HALO_API int halo_rx_ring_poll(halo_rx_ring_t* ring, uint32_t flags, const halo_rx_netif_t* netif,
                                halo_rx_result_t* out, uint32_t* status_hist, uint64_t* positions,
                                halo_rx_ring_scan_t* info);
+/* Small polls (rings attached with HALO_RING_REGISTER; default: spans up to 4 MiB): the host
+ * reads the records' length fields as ReadPacket does and ONE rx launch parses the frames in
+ * place in the registered ring, writing the records straight into `out` when it is pinned or
+ * registered. Same results, stop and cursor as the pipelined path (a poll whose span has a frame
+ * wrapping around the data area's end takes the pipelined path). `bytes` = 0 turns the small
+ * path off; at most 16 MiB; HALO_E_INVAL for an unregistered ring.                         */
+HALO_API int halo_rx_ring_set_small_poll(halo_rx_ring_t* ring, uint64_t bytes);
 /* Release everything polled so far to the producer: tail = cursor (store-release). */
 HALO_API int halo_rx_ring_commit(halo_rx_ring_t* ring);
 

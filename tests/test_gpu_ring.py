@@ -47,8 +47,13 @@ def _span(ring, start, used):
     return ring.mem[128:][idx]
 
 
+SMALL = [0, None, 16 << 20]  # pipelined path only / library default / small path for every poll
+SMALL_IDS = ["pipelined", "default", "small16M"]
+
+
+@pytest.mark.parametrize("small_poll", SMALL, ids=SMALL_IDS)
 @pytest.mark.parametrize("flags", [0, 1, 3])
-def test_poll_golden_frames_across_the_wrap(dev, golden, oracle_lib, flags):
+def test_poll_golden_frames_across_the_wrap(dev, golden, oracle_lib, flags, small_poll):
     from halo_amd._lib import NetIf
     from halo_amd.engine import dispatch
     from halo_amd.ring import RingBuffer, RingConsumer
@@ -63,7 +68,7 @@ def test_poll_golden_frames_across_the_wrap(dev, golden, oracle_lib, flags):
     assert n_w == int(small.sum())
     want, acts, pos, tail = _oracle_drain(O, ring.mem, O.NetIf.make(), flags, 1514)
     assert len(want) == n_w
-    cons = RingConsumer(ring, capacity=1514)
+    cons = RingConsumer(ring, capacity=1514, small_poll=small_poll)
     got, info, gpos = cons.poll(NetIf.make(), check_sum_enable=bool(flags & 1), jumbo=bool(flags & 2),
                                 positions=True)
     assert_records_equal(got.copy(), want, [n for n, s in zip(names, small) if s], f"ring flags={flags}")
@@ -78,7 +83,8 @@ def test_poll_golden_frames_across_the_wrap(dev, golden, oracle_lib, flags):
     cons.close()
 
 
-def test_poll_stops_like_readpacket(dev, golden, oracle_lib):
+@pytest.mark.parametrize("small_poll", SMALL, ids=SMALL_IDS)
+def test_poll_stops_like_readpacket(dev, golden, oracle_lib, small_poll):
     """An oversize record (> capacity) stops the drain and stays; a corrupt length stops it for
     good; max_frames and max_bytes cut it. Every poll is compared with the oracle loop."""
     from halo_amd._lib import NetIf
@@ -103,7 +109,7 @@ def test_poll_stops_like_readpacket(dev, golden, oracle_lib):
             ring.mem[0:8].view(np.uint64)[0] = ring.head + 8
         ring.write_batch(data, offs[sel].astype(np.uint64) * 4, lens[sel])
         kw = dict(max_frames=50) if case == "max_frames" else dict(max_bytes=6000) if case == "max_bytes" else {}
-        cons = RingConsumer(ring, capacity=1514, **kw)
+        cons = RingConsumer(ring, capacity=1514, small_poll=small_poll, **kw)
         mem_before = ring.mem.copy()
         got_all = []
         for _ in range(200):
@@ -187,6 +193,75 @@ def test_scan_device_matches_walk(dev, oracle_lib, name, gen, cap, max_frames, c
         assert (int(inf["stop"]), int(inf["end_bytes"]), int(inf["max_len"])) == (w_stop, w_end, w_ml), (name, trim)
         assert np.array_equal(d_off[:n].cpu().numpy().view(np.uint32), w_off), name
         assert np.array_equal(d_len[:n].cpu().numpy().view(np.uint16), w_len), name
+
+
+def test_small_poll_laps_the_ring(dev, oracle_lib):
+    """The small path reads frames in place in the registered ring: 300 produce/poll/commit rounds
+    over a 64 KiB ring (the data area is rewritten ~70 times) with fresh frames each round, a
+    record wrapping the end now and then (that poll takes the pipelined path), each poll's records
+    == the oracle on exactly the frames written; positions and tail follow ReadPacket."""
+    from halo_amd._lib import NetIf
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    O = oracle_lib
+    ring = RingBuffer(1 << 16)
+    _seek(ring, (1 << 33) - 100)
+    cons = RingConsumer(ring, capacity=1514)
+    rng = np.random.default_rng(17)
+    onetif = O.NetIf.make()
+    for it in range(300):
+        k = int(rng.integers(1, 24))
+        lens = rng.integers(42, 1515, size=k).astype(np.uint16)
+        kinds = rng.integers(0, 3, size=k).astype(np.uint8)
+        offs = np.concatenate([[0], np.cumsum((lens.astype(np.int64) + 3) & ~3)[:-1]]).astype(np.uint32) // 4
+        data = O.synth_batch(it, 0, lens, kinds, onetif, offsets_dw=offs)
+        if it % 3 == 1:  # a bit flip somewhere in one frame
+            j = int(rng.integers(0, k))
+            data[int(offs[j]) * 4 + int(rng.integers(14, int(lens[j])))] ^= 1 << int(rng.integers(0, 8))
+        start = ring.head
+        assert ring.write_batch(data, offs.astype(np.uint64) * 4, lens) == k
+        got, info, pos = cons.poll(NetIf.make(), positions=True)
+        want, _ = O.rx_batch(data, lens, onetif, 1, offsets_dw=offs)
+        assert info["n_frames"] == k and info["stop"] == "EMPTY", (it, info)
+        assert_records_equal(got.copy(), want, None, f"lap round {it}")
+        rec = np.concatenate([[0], np.cumsum(4 + ((lens.astype(np.int64) + 3) & ~3))[:-1]])
+        assert np.array_equal(pos, start + rec)
+        cons.commit()
+        assert ring.tail == ring.head
+    cons.close()
+
+
+def test_small_poll_unpinned_out_and_unregistered_ring(dev, golden, oracle_lib):
+    """Records into a caller array that is neither pinned nor registered (the small path stages
+    them); an unregistered ring has no small path (set_small_poll refuses) and polls pipelined."""
+    from halo_amd import _lib
+    from halo_amd._lib import RING_SCAN_DTYPE, NetIf
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    O = oracle_lib
+    meta, blob = golden
+    data, offs, lens, _ = golden_arrays(meta, blob)
+    sel = np.nonzero((lens > 0) & (lens <= 1514))[0][:100]
+    for register in (True, False):
+        ring = RingBuffer(1 << 18)
+        ring.write_batch(data, offs[sel].astype(np.uint64) * 4, lens[sel])
+        want, _, _, tail = _oracle_drain(O, ring.mem, O.NetIf.make(), 1, 1514)
+        cons = RingConsumer(ring, capacity=1514, register=register)
+        if not register:
+            assert _lib.lib.halo_rx_ring_set_small_poll(cons._h, 1 << 16) == _lib.HALO_E_INVAL
+        out = np.full(len(sel) + 5, 0xEE, np.uint8).repeat(32).view(_lib.RESULT_DTYPE)
+        info = np.zeros(1, RING_SCAN_DTYPE)
+        hist = np.zeros(14, np.uint32)
+        _lib.check("poll", _lib.lib.halo_rx_ring_poll(cons._h, 1, NetIf.make(), out.ctypes.data, hist.ctypes.data,
+                                                      None, info.ctypes.data))
+        n = int(info["n_frames"][0])
+        assert n == len(sel)
+        assert_records_equal(out[:n], want, None, f"unpinned out, registered ring={register}")
+        assert np.all(out[n:].view(np.uint8) == 0xEE)
+        assert np.array_equal(hist, np.bincount(want["status"], minlength=14))
+        cons.commit()
+        assert ring.tail == tail
+        cons.close()
 
 
 def test_poll_large_imix_ring(dev, oracle_lib):
