@@ -141,6 +141,8 @@ def bench_lib():
         u64 = ctypes.c_uint64
         L.halo_bench_read_peak.restype = ctypes.c_int
         L.halo_bench_read_peak.argtypes = [vp, u64, vp] + tail
+        L.halo_bench_stream_rw.restype = ctypes.c_int
+        L.halo_bench_stream_rw.argtypes = [vp, vp, i32, u64, u64, vp] + tail
         L.halo_bench_ring_scan_steps.restype = ctypes.c_int
         L.halo_bench_ring_scan_steps.argtypes = [i32, vp, u64, u64, u32, vp, vp, vp, vp, u64] + tail
         _BENCH_LIB = L
@@ -519,6 +521,33 @@ def measure_read_peak(dev, d: Dist, gib: int = 2):
     return MEASURED_READ_GBS
 
 
+def size_matched_probe(dev, read_bytes: int, write_bytes: int, d: Dist, nbuf: int = 8, steps: int = 50):
+    """Speed-of-light for a kernel's byte shape on this box: one kernel that streams `read_bytes`
+    in (16 KB tiles, 16-byte loads) and writes `write_bytes` out (coalesced 16-byte stores) over
+    `nbuf` rotating buffers, doing no other work (tools/bench_loop.hip stream_rw_kernel). Returns
+    the average launch duration in ms."""
+    import ctypes
+
+    import torch
+
+    r16, w16 = (read_bytes + 15) // 16 * 16, (write_bytes + 15) // 16 * 16
+    srcs = [torch.ones(r16, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    dsts = [torch.empty(w16, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    sink = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
+    arr = lambda xs: (ctypes.c_void_p * len(xs))(*[x.data_ptr() for x in xs])  # noqa: E731
+    _, k = time_native(bench_lib().halo_bench_stream_rw, arr(srcs), arr(dsts), nbuf, r16, w16, sink.data_ptr(),
+                       steps=steps, warmup=5, d=d)
+    del srcs, dsts, sink
+    torch.cuda.empty_cache()
+    return k
+
+
+def with_probe(r: dict, probe_ms: float, kernel_ms: float) -> dict:
+    r["size_matched_probe_ms"] = round(probe_ms, 5)
+    r["frac_of_size_matched"] = round(probe_ms / kernel_ms, 4)
+    return r
+
+
 def roofline(alg_bytes_per_launch, kernel_ms, traffic=None):
     achieved = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -663,7 +692,12 @@ def main():
     line["roofline"]["note"] = ("achieved = (frame bytes + 6 B metadata + 32 B record) per launch / average "
                                 "launch duration (one HIP event pair over the timed region / steps); "
                                 "peak = HBM3E spec; traffic = 2 x FETCH_SIZE + WRITE_SIZE per launch from "
-                                "profiles/pmc_summary.json")
+                                "profiles/pmc_summary.json; size_matched_probe_ms = a no-work kernel streaming "
+                                "the same bytes in and out with perfect access patterns over the same number of "
+                                "rotating buffers (frac_of_size_matched = probe / kernel time)")
+    if d.world == 1 and not args.no_secondary:
+        with_probe(line["roofline"], size_matched_probe(dev, fbytes + 6 * n, RESULT_BYTES * n, d, nbuf=args.rotate),
+                   kern_ms)
 
     if d.world == 1 and not args.no_secondary:
         sec = {}
@@ -731,6 +765,9 @@ def main():
                          "roofline": roofline(a2, k2, load_traffic(name))}
             del bs, o2
             torch.cuda.empty_cache()
+            if not strided_len:
+                with_probe(sec[name]["roofline"], size_matched_probe(dev, fb + nn * meta, nn * RESULT_BYTES, d,
+                                                                     nbuf=rot, steps=steps), k2)
         # end to end from host memory: pinned H2D -> kernel -> D2H, double
         # buffered in 64 MB chunks by halo_rx_parse_batch_host; the frame buffer is registered
         # (pinned in place) so each chunk is one DMA straight from it

@@ -170,6 +170,28 @@ __global__ void __launch_bounds__(256) read_peak_kernel(const uint4* __restrict_
     }
     if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;  // practically never: keeps the loads live
 }
+
+// Size-matched speed-of-light probe: block t reads 16 KB tile t of `src` (four 16-byte loads per
+// thread in flight) and writes its share of `dst` with coalesced 16-byte stores — the rx kernel's
+// bytes (frames + metadata in, records out) with perfect access patterns and no work.
+__global__ void __launch_bounds__(256) stream_rw_kernel(const uint4* __restrict__ src, uint64_t r16,
+                                                        uint4* __restrict__ dst, uint64_t w16, uint64_t wt16,
+                                                        uint32_t* __restrict__ sink) {
+    constexpr uint32_t kTile16 = 1024;  // 16 KB
+    const uint64_t t = blockIdx.x;
+    uint32_t acc = 0;
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint64_t k = t * kTile16 + u * 256 + threadIdx.x;
+        v[u] = k < r16 ? src[k] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    const uint64_t w0 = t * wt16, w1 = w0 + wt16 < w16 ? w0 + wt16 : w16;
+    for (uint64_t k = w0 + threadIdx.x; k < w1; k += 256) dst[k] = make_uint4((uint32_t)k, (uint32_t)t, 0, 0);
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;  // practically never: keeps the loads live
+}
 }  // namespace
 
 extern "C" __attribute__((visibility("default"))) int halo_bench_read_peak(const void* buf, uint64_t bytes,
@@ -182,6 +204,27 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_read_peak(const
     auto launch = [&](int) {
         hipLaunchKernelGGL(read_peak_kernel, dim3(grid_blocks), dim3(256), 0, s, static_cast<const uint4*>(buf),
                            bytes / 16, sink);
+        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+    };
+    return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
+}
+
+// The size-matched probe over `nbuf` rotating (src, dst) pairs, like the rx steps rotate batches.
+extern "C" __attribute__((visibility("default"))) int halo_bench_stream_rw(const void* const* srcs,
+                                                                            void* const* dsts, int nbuf,
+                                                                            uint64_t read_bytes, uint64_t write_bytes,
+                                                                            uint32_t* sink, int warmup, int steps,
+                                                                            void* stream, float* region_ms,
+                                                                            double* wall_s) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint64_t r16 = read_bytes / 16, w16 = write_bytes / 16;
+    const uint64_t tiles = (r16 + 1023) / 1024;
+    if (!tiles || nbuf <= 0) return HALO_E_INVAL;
+    const uint64_t wt16 = (w16 + tiles - 1) / tiles;
+    auto launch = [&](int step) {
+        const int b = step % nbuf;
+        hipLaunchKernelGGL(stream_rw_kernel, dim3((uint32_t)tiles), dim3(256), 0, s, static_cast<const uint4*>(srcs[b]),
+                           r16, static_cast<uint4*>(dsts[b]), w16, wt16, sink);
         return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
     };
     return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
