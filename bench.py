@@ -744,11 +744,12 @@ def main():
         sec["route_lpm_500k_prefixes"] = route_secondary(dev, max(10, args.steps // 4), 3, d, with_cpu=not args.no_cpu)
         torch.cuda.empty_cache()
         for name, kw, hint, strided_len, flags in [
+            ("config4_shard_16M_64B", dict(length=64), 64, 0, 1),
             ("1500B_udp_1M", dict(length=1500), 1500, 0, 1),
             ("config3_imix_16M", dict(size_mode=1, proto_mode=3), 1500, 0, 1),
             ("config5_jumbo_9000B_tcp_4M_ext", dict(length=9000, proto_mode=1, strided=True), 0, 9000, 3),
         ]:
-            nn = (16 << 20) if "imix" in name else ((4 << 20) if "jumbo" in name else n)
+            nn = (16 << 20) if ("imix" in name or "config4" in name) else ((4 << 20) if "jumbo" in name else n)
             rot = 2 if nn * (kw.get("length", 352)) < (1 << 31) else 1
             log(f"[secondary] {name}: {rot} x {nn} frames")
             bs = make_batches(dev, netif, n=nn, rotate=rot, rank=0, **kw)
@@ -763,6 +764,9 @@ def main():
             sec[name] = {"frames": nn, "mpps": round(nn * steps / w2 / 1e6, 1),
                          "gbit_s": round(fb * steps * 8 / w2 / 1e9, 1), "kernel_ms": round(k2, 4),
                          "roofline": roofline(a2, k2, load_traffic(name))}
+            if "config4" in name:
+                sec[name]["what"] = ("one GPU's shard of BASELINE config 4 (128M x 64 B over 8 GPUs = 16M per GPU, "
+                                     "index-sharded, no collective); the scaling run itself is bench.py --gpus N")
             del bs, o2
             torch.cuda.empty_cache()
             if not strided_len:

@@ -375,13 +375,21 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     flush_hist(p, hist);
 }
 
-// Lane per frame. SGPRs <= 80 lets 8 blocks of 256 threads share a CU (MI355X_MICROARCH.md
-// "Residency"); at ~56 VGPRs that is the full 8 waves per SIMD. A wave's 64 records are
+// Lane per frame. The build lands at 76 VGPRs = 6 waves per SIMD; forcing 7 (72 VGPRs) or 8
+// (64, with scratch spills) was not faster (profiles/r01/ab_r2o_lane_waves.log: 22.2 / 27.8 µs vs
+// 21.9 µs on config 2), so the knob HALO_RX_LANE_WAVES stays off. A wave's 64 records are
 // consecutive: they are staged in LDS and written with fully coalesced 16-byte stores (a lane
 // writing its own 32 B record at a 32 B stride stored the same bytes 25 % slower:
 // profiles/r01/probe_store_patterns.log).
 template <int LAYOUT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) rx_lane_kernel(const RxParams p) {
+#ifndef HALO_RX_LANE_WAVES
+#define HALO_RX_LANE_WAVES 0
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80)))
+#if HALO_RX_LANE_WAVES
+__attribute__((amdgpu_waves_per_eu(HALO_RX_LANE_WAVES)))
+#endif
+rx_lane_kernel(const RxParams p) {
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     __shared__ uint4 s_rec[4][128];  // per wave: 64 records of 32 B
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
