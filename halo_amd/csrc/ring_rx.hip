@@ -487,9 +487,6 @@ struct halo_rx_ring {
     uint32_t* d_soff = nullptr;
     uint16_t* d_slen = nullptr;
     halo_rx_result_t* d_sres = nullptr;
-    const void* last_out = nullptr;  // the caller's record array seen last, if device-mapped
-    uint64_t last_out_bytes = 0;
-    halo_rx_result_t* last_out_dev = nullptr;
 };
 
 namespace {
@@ -586,14 +583,8 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
     }
     if (n) {
         const uint64_t rb = sizeof(halo_rx_result_t) * (uint64_t)n;
-        halo_rx_result_t* dout = nullptr;
-        if (out == r->last_out && rb <= r->last_out_bytes) {
-            dout = r->last_out_dev;
-        } else if ((dout = static_cast<halo_rx_result_t*>(device_view(out, rb)))) {
-            r->last_out = out;
-            r->last_out_bytes = rb;
-            r->last_out_dev = dout;
-        }
+        // looked up per poll (not cached): the caller may unregister or reuse the array between polls
+        halo_rx_result_t* dout = static_cast<halo_rx_result_t*>(device_view(out, rb));
         if (!dout && !r->h_sres) {
             const uint64_t sb = sizeof(halo_rx_result_t) * (uint64_t)r->small_frames;
             if (hipHostMalloc((void**)&r->h_sres, sb, hipHostMallocDefault) != hipSuccess) return HALO_E_NOMEM;

@@ -261,6 +261,19 @@ def test_small_poll_unpinned_out_and_unregistered_ring(dev, golden, oracle_lib):
         assert np.array_equal(hist, np.bincount(want["status"], minlength=14))
         cons.commit()
         assert ring.tail == tail
+        if register:  # the same array registered for one poll, unregistered for the next
+            ring.write_batch(data, offs[sel].astype(np.uint64) * 4, lens[sel])
+            _lib.check("register", _lib.lib.halo_rx_host_register(out.ctypes.data, out.nbytes))
+            for k in range(2):
+                if k:
+                    _lib.check("unregister", _lib.lib.halo_rx_host_unregister(out.ctypes.data))
+                    ring.write_batch(data, offs[sel].astype(np.uint64) * 4, lens[sel])
+                out.view(np.uint8)[:] = 0xEE
+                _lib.check("poll", _lib.lib.halo_rx_ring_poll(cons._h, 1, NetIf.make(), out.ctypes.data, None,
+                                                              None, info.ctypes.data))
+                assert int(info["n_frames"][0]) == len(sel)
+                assert_records_equal(out[:len(sel)], want, None, f"out registered={not k}")
+                cons.commit()
         cons.close()
 
 
