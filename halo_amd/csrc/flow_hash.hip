@@ -239,12 +239,49 @@ struct XxhParams {
     uint64_t* out;
 };
 
-// strings <= 240 B, one lane each (the long ones are left to xxh3_long_kernel)
+// strings <= 240 B, one lane each (the long ones are left to xxh3_long_kernel). A wave scans
+// kShortScan strings and compacts the short ones into LDS — the 129..240 B ones first, then the
+// rest, so a wave-instruction's lanes mostly take the same hashLarge / hashMedium / hashSmall
+// branch — and hashes them 64 at a time: a ragged batch whose short strings are a minority no
+// longer runs the whole short path for a handful of lanes in every wave.
+#ifndef HALO_XXH3_SHORT_SCAN
+#define HALO_XXH3_SHORT_SCAN 256
+#endif
+constexpr uint32_t kShortScan = HALO_XXH3_SHORT_SCAN;  // strings per wave window (a multiple of 64)
 __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += stride) {
-        const uint32_t len = p.lens[i];
-        if (len <= 240) p.out[i] = hash_short(p.bytes + p.offsets[i], len);
+    __shared__ uint32_t s_idx[4][kShortScan];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t base = wave * kShortScan; base < p.n; base += nwaves * kShortScan) {
+        uint32_t len[kShortScan / 64];
+#pragma unroll
+        for (uint32_t k = 0; k < kShortScan / 64; ++k) {
+            const uint32_t i = base + 64 * k + lane;
+            len[k] = i < p.n ? p.lens[i] : 0xFFFFFFFFu;
+        }
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+            for (uint32_t k = 0; k < kShortScan / 64; ++k) {
+                const bool take = pass == 0 ? (len[k] > 128 && len[k] <= 240) : len[k] <= 128;
+                const uint64_t b = __ballot(take);
+                if (take)
+                    s_idx[w][cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
+                        base + 64 * k + lane;
+                cnt += (uint32_t)__popcll(b);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t e = lane; e < ((cnt + 63) & ~63u); e += 64) {
+            if (e < cnt) {
+                const uint32_t i = s_idx[w][e];
+                p.out[i] = hash_short(p.bytes + p.offsets[i], p.lens[i]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -340,7 +377,9 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
     if (rc) return rc;
     halo::XxhParams p{d_bytes, d_offsets, d_lens, n, d_hash};
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(halo::xxh3_short_kernel, dim3(halo::blocks_for(n)), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(halo::xxh3_short_kernel, dim3(halo::blocks_for((n + halo::kShortScan / 64 - 1) /
+                                                                       (halo::kShortScan / 64))),
+                       dim3(256), 0, s, p);
     hipLaunchKernelGGL(halo::xxh3_long_kernel, dim3(halo::blocks_for(n)), dim3(256), 0, s, p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
