@@ -126,8 +126,10 @@ def test_poll_stops_like_readpacket(dev, golden, oracle_lib, small_poll):
         cons.close()
 
 
-def _records_span(rng, lens, corrupt_at=None, corrupt_val=0):
-    """A ring span in stream order holding records of `lens` (+ random bytes)."""
+def _records_span(rng, lens, corrupt_at=None, corrupt_val=0, garbage=0.0):
+    """A ring span in stream order holding records of `lens` (+ random bytes). `garbage`: the
+    fraction of payload dwords replaced by values that pass ReadPacket's length checks (1..1514),
+    so walks started off the record chain look valid for a while (record decoys)."""
     lens = np.asarray(lens, np.int64)
     sizes = (4 + lens + 3) & ~3
     starts = np.zeros(len(lens), np.int64)
@@ -135,6 +137,9 @@ def _records_span(rng, lens, corrupt_at=None, corrupt_val=0):
     used = int(sizes.sum())
     span = rng.integers(0, 256, used + 16, dtype=np.uint8)
     words = span[:used].view(np.uint32)
+    if garbage:
+        decoy = rng.random(words.size) < garbage
+        words[decoy] = rng.integers(1, 1515, int(decoy.sum()), dtype=np.uint32)
     words[starts // 4] = lens.astype(np.uint32)
     if corrupt_at is not None:
         words[starts[corrupt_at] // 4] = corrupt_val
@@ -157,7 +162,15 @@ SCAN_CASES = [
     ("max_frames_cut", lambda r: r.integers(1, 1515, 50_000), 1514, 12_345, None),
     ("max_frames_exact", lambda r: [64] * 5000, 1514, 5000, None),
     ("max_frames_one", lambda r: [64] * 5000, 1514, 1, None),
+    # record decoys in the payloads (every / 1 in 100 payload dwords a plausible length)
+    ("decoys_all_imix", lambda r: r.choice([64, 570, 1500], 60_000, p=[7 / 12, 4 / 12, 1 / 12]), 1514, 0, None),
+    ("decoys_1pct", lambda r: r.integers(1, 1515, 60_000), 1514, 0, None),
+    ("decoys_all_dense", lambda r: r.integers(1, 9, 200_000), 1514, 0, None),
+    ("decoys_all_bad_len", lambda r: r.integers(1, 1515, 50_000), 1514, 0, (40_000, 0)),
+    ("decoys_all_max_frames", lambda r: r.integers(60, 200, 50_000), 1514, 33_333, None),
 ]
+DECOYS = {"decoys_all_imix": 1.0, "decoys_1pct": 0.01, "decoys_all_dense": 1.0, "decoys_all_bad_len": 1.0,
+          "decoys_all_max_frames": 1.0}
 
 
 @pytest.mark.parametrize("name,gen,cap,max_frames,corrupt", SCAN_CASES, ids=[c[0] for c in SCAN_CASES])
@@ -169,7 +182,7 @@ def test_scan_device_matches_walk(dev, oracle_lib, name, gen, cap, max_frames, c
     O = oracle_lib
     rng = np.random.default_rng(zlib.crc32(name.encode()))
     lens = gen(rng)
-    span, used = _records_span(rng, lens, *(corrupt or (None, 0)))
+    span, used = _records_span(rng, lens, *(corrupt or (None, 0)), garbage=DECOYS.get(name, 0.0))
     ring_size = 1 << max(12, int(np.ceil(np.log2(max(used, 8)))) + 1)
     for trim in (0, 4, 12) if used > 64 else (0,):  # also spans that end inside a record
         u = max(0, used - trim)
