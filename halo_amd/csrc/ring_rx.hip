@@ -22,7 +22,9 @@
 //   3. chain       — one workgroup runs the superblock maps from the span's start: the entry and
 //                    the number of records before every superblock.
 //   4. emit        — every tile follows at most S-1 tile maps from its superblock's entry to its
-//                    own, then walks its own records in LDS and writes (dword offset, length).
+//                    own, finds its records from that entry by one parallel pass over the links
+//                    of its record positions (a serial walk in LDS only behind a record decoy) and
+//                    writes (dword offset, length).
 // Every step applies ReadPacket's checks in ReadPacket's order, so the frames taken, the stop and
 // the new tail are those of repeated ReadPacket calls (tests/test_gpu_ring.py, against the oracle,
 // which tests/test_ring_oracle.py checks against the reference's own cgo/ring_buffer.h).
@@ -271,8 +273,10 @@ __global__ void __launch_bounds__(kThreads) ring_expand_kernel(const uint2* pare
 }
 
 // 5. Emit: one wave per tile. The lanes tabulate every position's next record position (or its
-// stop reason) in LDS; lane 0 follows the chain from the tile's entry (one dependent LDS read per
-// record); the lanes then write the records' (offset, length) pairs.
+// stop reason) in LDS and list, in order, the positions from the tile's entry on that pass
+// ReadPacket's checks; one pass over those candidates' links finds the chain (a serial walk, one
+// dependent LDS read per record, only behind a record decoy); the lanes then write the records'
+// (offset, length) pairs.
 constexpr uint32_t kEmitWaves = kThreads / 64;
 __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
     __shared__ uint16_t nxt[kEmitWaves][kTile];
@@ -285,6 +289,7 @@ __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
     const uint32_t entry = te.x, base = te.y;
     if (entry == kMapStop || base > n) return;  // wave-uniform
     const uint32_t tbase = t * kTile;
+    uint32_t n_act = 0;  // positions at or past the entry that pass ReadPacket's checks
     // the wave's 16 KB in two rounds of eight 16-byte loads in flight per lane
     const bool whole = tbase + kTile <= s.n_dw;  // wave-uniform
     for (uint32_t r0 = 0; r0 < kTile; r0 += 8 * 4 * 64) {
@@ -303,34 +308,81 @@ __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
         for (int u = 0; u < 8; ++u) {
             const uint32_t q = r0 + 4 * (lane + 64 * u);
             const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            uint32_t mine = 0;  // bit j: position q + j holds a record and is at or past the entry
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 uint32_t why;
                 const uint32_t step = record_dwords(s, tbase + q + j, d[j], why);
                 nxt[w][q + j] = (uint16_t)(step ? q + j + step : (kLdsStop | why));
+                mine |= (step && q + j >= entry) ? 1u << j : 0u;
             }
+            // ordered compaction of those positions (block order, then lane, then j)
+            uint32_t before = 0, total = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t b = __ballot((mine >> j) & 1u);
+                before += lane_rank(b);
+                total += (uint32_t)__popcll(b);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = n_act + before + (uint32_t)__builtin_popcount(mine & ((1u << j) - 1u));
+                if (((mine >> j) & 1u) && k < kTile / 2) list[w][k] = (uint16_t)(q + j);
+            }
+            n_act += total;
         }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // the walk: every lane follows the same chain (values made scalar), so the loop is uniform
-    // control flow around one dependent LDS read per record
     const uint32_t limit = min(n - base, kTile / 2);  // records this tile may still take
-    uint32_t c = 0, q = entry, v = 0;
-    while (c < limit && q < kTile) {
-        v = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt[w][q]);
-        if (v & kLdsStop) break;
-        list[w][c++] = (uint16_t)q;
-        q = v;
+    uint32_t c = 0, q = entry;
+    // Fast path: in ring data the positions that pass ReadPacket's checks are, almost always,
+    // exactly the record starts. If the k-th such position from the entry on links to the
+    // (k+1)-th for k < F and the F-th does not, the walk is those F + 1 records — found by one
+    // parallel pass over the links instead of one dependent LDS read per record. A position that
+    // passes the checks but is not on the chain (a record decoy in a payload) shows up as a link
+    // that skips over it; the serial walk then takes over from where the links end.
+    bool serial = n_act > kTile / 2;  // too many candidates to list: walk serially from the entry
+    if (!serial && n_act && list[w][0] == entry) {
+        uint32_t F = n_act - 1;  // the last candidate's link always "fails" (no successor listed)
+        for (uint32_t i0 = 0; i0 < n_act; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            bool brk = false;
+            if (i < n_act) brk = nxt[w][list[w][i]] != (i + 1 < n_act ? list[w][i + 1] : 0xFFFFu);
+            const uint64_t b = __ballot(brk);
+            if (b) {
+                F = i0 + (uint32_t)__builtin_ctzll(b);
+                break;
+            }
+        }
+        const uint32_t M = F + 1;
+        c = min(M, limit);
+        q = c < M ? list[w][c] : nxt[w][list[w][F]];
+        // the chain goes on at a position past a decoy: continue serially from there
+        serial = c == M && c < limit && q < kTile && !(nxt[w][q] & kLdsStop);
+    } else if (!serial) {
+        c = 0;
+        q = entry;  // the entry itself fails ReadPacket's checks (or the tile has no record)
+    } else {
+        c = 0;
+        q = entry;
     }
+    if (serial) {
+        // every lane follows the same chain (values made scalar): uniform control flow around
+        // one dependent LDS read per record
+        while (c < limit && q < kTile) {
+            const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt[w][q]);
+            if (v & kLdsStop) break;
+            list[w][c++] = (uint16_t)q;
+            q = v;
+        }
+    }
+    uint32_t v = q < kTile ? nxt[w][q] : 0u;
     if (lane == 0) {
         if (base + c == n && c) s.info->end_bytes = 4ull * (tbase + q);
         // where the walk ends inside this tile: say why, unless max_frames cut it (MAX, set)
-        if (q < kTile && n == *s.total) {
-            if (c == limit) v = nxt[w][q];
-            if (v & kLdsStop) s.info->stop = v & 0xFFu;
-        }
+        if (q < kTile && n == *s.total && (v & kLdsStop)) s.info->stop = v & 0xFFu;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
