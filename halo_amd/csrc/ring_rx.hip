@@ -65,6 +65,7 @@ struct Scan {
     uint32_t n_ss;          // super-superblocks: S superblocks each
     uint32_t max_frames;
     uint64_t half;          // RingBuffer.size / 2
+    uint32_t half32;        // min(half, 2^32 - 1)
     uint2* tile_map;        // [n_tiles][W]: (entry into the next tile | kMapStop, records taken)
     uint2* sb_map;          // [n_sb][W]
     uint2* ss_map;          // [n_ss][W]
@@ -79,13 +80,16 @@ struct Scan {
 
 // Dwords of the record whose length field is span dword a (value `len`), or 0 where ReadPacket
 // returns false, with the reason: the checks of mem/ring_buffer.go:309-335, in that order.
+// 32-bit arithmetic throughout (the walk is VALU-bound): the record's dwords are
+// ceil((4 + len) / 4) = (len >> 2) + 1 + (len & 3 != 0) without overflow, and size/2 is clamped
+// to 2^32 - 1 (a u32 length can only exceed it when it is smaller).
 __device__ __forceinline__ uint32_t record_dwords(const Scan& s, uint32_t a, uint32_t len, uint32_t& why) {
     if (a >= s.n_dw) { why = HALO_RING_STOP_EMPTY; return 0; }                                  // usedSpace < 4
-    if (len == 0 || (uint64_t)len > s.half) { why = HALO_RING_STOP_BAD_LEN; return 0; }
-    const uint64_t bytes = (4ull + len + 3ull) & ~3ull;                                         // ringBufferRecordSize
-    if ((uint64_t)(s.n_dw - a) * 4ull < bytes) { why = HALO_RING_STOP_PARTIAL; return 0; }      // usedSpace < totalSize
+    if (len == 0 || len > s.half32) { why = HALO_RING_STOP_BAD_LEN; return 0; }
+    const uint32_t dw = (len >> 2) + 1u + ((len & 3u) != 0u);                                   // ringBufferRecordSize / 4
+    if (s.n_dw - a < dw) { why = HALO_RING_STOP_PARTIAL; return 0; }                            // usedSpace < totalSize
     if (len > s.cap) { why = HALO_RING_STOP_CAPACITY; return 0; }                              // len(data) < packetLen
-    return (uint32_t)(bytes >> 2);
+    return dw;
 }
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -279,7 +283,7 @@ __global__ void __launch_bounds__(kThreads) ring_expand_kernel(const uint2* pare
 // (offset, length) pairs.
 constexpr uint32_t kEmitWaves = kThreads / 64;
 __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
-    __shared__ uint16_t nxt[kEmitWaves][kTile];
+    __shared__ __align__(8) uint16_t nxt[kEmitWaves][kTile];
     __shared__ uint16_t list[kEmitWaves][kTile / 2];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t t = blockIdx.x * kEmitWaves + w;
@@ -309,13 +313,15 @@ __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
             const uint32_t q = r0 + 4 * (lane + 64 * u);
             const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
             uint32_t mine = 0;  // bit j: position q + j holds a record and is at or past the entry
+            uint32_t nx[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 uint32_t why;
                 const uint32_t step = record_dwords(s, tbase + q + j, d[j], why);
-                nxt[w][q + j] = (uint16_t)(step ? q + j + step : (kLdsStop | why));
+                nx[j] = step ? q + j + step : (kLdsStop | why);
                 mine |= (step && q + j >= entry) ? 1u << j : 0u;
             }
+            *reinterpret_cast<uint2*>(&nxt[w][q]) = make_uint2(nx[0] | (nx[1] << 16), nx[2] | (nx[3] << 16));
             // ordered compaction of those positions (block order, then lane, then j)
             uint32_t before = 0, total = 0;
 #pragma unroll
@@ -444,6 +450,7 @@ Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_
     s.n_ss = g.n_ss;
     s.max_frames = max_frames;  // 0: no frame may be taken
     s.half = ring_size / 2;
+    s.half32 = (uint32_t)std::min<uint64_t>(s.half, 0xFFFFFFFFull);
     s.tile_map = reinterpret_cast<uint2*>(ws + g.tile_map_off);
     s.sb_map = reinterpret_cast<uint2*>(ws + g.sb_map_off);
     s.ss_map = reinterpret_cast<uint2*>(ws + g.ss_map_off);
