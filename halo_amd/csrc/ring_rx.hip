@@ -695,6 +695,15 @@ extern "C" HALO_API int halo_rx_ring_scan_device(const uint8_t* d_span, uint64_t
     return halo::launch_finish(s, st);
 }
 
+// The walk + parse stream, at the device's highest priority: its workgroups are placed ahead of
+// the record copies' blit waves as CUs free up (profiles/r01/ab_r3x_ring_e2e.log).
+static bool comp_stream(hipStream_t* st) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+        return hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi) == hipSuccess;
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking) == hipSuccess;
+}
+
 extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t offset, uint32_t capacity,
                                             uint64_t max_bytes, uint32_t max_frames, uint32_t attach_flags,
                                             halo_rx_ring_t** out) {
@@ -725,7 +734,7 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     r->g = halo::geometry(std::min<uint64_t>(max_bytes, halo::kPieceBytes + 4ull * halo::kTile), capacity);  // a piece + a cut record
     r->ev.assign(2 * (size_t)((max_bytes + halo::kPieceBytes - 1) / halo::kPieceBytes), nullptr);
     bool ok = hipStreamCreateWithFlags(&r->s_copy, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&r->s_comp, hipStreamNonBlocking) == hipSuccess &&
+              comp_stream(&r->s_comp) &&
               hipStreamCreateWithFlags(&r->s_d2h, hipStreamNonBlocking) == hipSuccess;
     for (auto& e : r->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipMalloc((void**)&r->d_span, max_bytes + 16) == hipSuccess;
