@@ -141,6 +141,8 @@ def bench_lib():
         u64 = ctypes.c_uint64
         L.halo_bench_read_peak.restype = ctypes.c_int
         L.halo_bench_read_peak.argtypes = [vp, u64, vp] + tail
+        L.halo_bench_rx_flow_steps.restype = ctypes.c_int
+        L.halo_bench_rx_flow_steps.argtypes = [i32, vp, vp, vp, u32, u32, vp, u32, vp, u32, u32, vp, u32, vp] + tail
         L.halo_bench_stream_rw.restype = ctypes.c_int
         L.halo_bench_stream_rw.argtypes = [vp, vp, i32, u64, u64, vp] + tail
         L.halo_bench_ring_scan_steps.restype = ctypes.c_int
@@ -289,6 +291,30 @@ def flow_hash_secondary(batches, out_records, netif, steps, warmup, d: Dist, wit
                                        f"{n} records of batch 0 (oracle/halo_xxh3_oracle.c)")
     del recs
     return res
+
+
+def rx_flow_fused_secondary(batches, out, netif, steps, warmup, d: Dist, rx_ms: float, flow_ms: float):
+    """The headline parse with every record's NAT flow key hashed in the same pass
+    (halo_rx_parse_flow_batch_device), against the two separate launches it replaces."""
+    import ctypes
+
+    import torch
+
+    n = batches[0]["layout"]["n"]
+    nb = len(batches)
+    arr = lambda xs: (ctypes.c_void_p * nb)(*xs)  # noqa: E731
+    h = torch.empty(n, dtype=torch.int64, device=out.device)
+    bk = torch.empty(n, dtype=torch.int32, device=out.device)
+    w, k = time_native(bench_lib().halo_bench_rx_flow_steps, nb, arr([b["bytes"].data_ptr() for b in batches]),
+                       arr([b["offsets_dw"].data_ptr() for b in batches]),
+                       arr([b["lens"].data_ptr() for b in batches]), n, 1, ctypes.addressof(netif), 64,
+                       out.data_ptr(), 1, 0, h.data_ptr(), 1 << 20, bk.data_ptr(), steps=steps, warmup=warmup, d=d)
+    alg = frame_bytes(batches[0]) + n * (4 + 2 + RESULT_BYTES + 8 + 4)
+    return {"mpps": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 5),
+            "separate_ms": round(rx_ms + flow_ms, 5), "speedup_vs_separate": round((rx_ms + flow_ms) / k, 3),
+            "roofline": roofline(alg, k), "alg_bytes_per_launch": alg,
+            "what": "config-2 parse + NatWanFlowHash XXH3-64 + 2^20-bucket index of every record in one pass "
+                    "(records, hashes and buckets identical to the two separate launches)"}
 
 
 def xxh3_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
@@ -739,6 +765,8 @@ def main():
         del ops_d, res_d
         sec["flow_hash_config2_nat_wan"] = flow_hash_secondary(batches, out, netif, args.steps, args.warmup, d,
                                                                with_cpu=not args.no_cpu)
+        sec["rx_flow_fused_config2_nat_wan"] = rx_flow_fused_secondary(
+            batches, out, netif, args.steps, args.warmup, d, kern_ms, sec["flow_hash_config2_nat_wan"]["kernel_ms"])
         del batches
         torch.cuda.empty_cache()
         sec["xxh3_kcp_segments_1M"] = xxh3_secondary(dev, max(5, args.steps // 10), 2, d, with_cpu=not args.no_cpu)

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device_util.h"
+#include "flow_key.h"
 #include "halo_common.h"
 
 namespace halo {
@@ -341,18 +342,7 @@ __global__ void __launch_bounds__(256) flow_hash_kernel(const FlowParams p) {
         const uint4 a = reinterpret_cast<const uint4*>(p.recs)[2ull * i];
         const uint32_t ports = reinterpret_cast<const uint32_t*>(p.recs)[8ull * i + 4];
         const uint32_t proto = a.y & 0xFFu, src = a.z, dst = a.w;
-        const uint32_t sport = ports & 0xFFFFu, dport = ports >> 16;
-        const bool wan = p.kind == HALO_FLOW_NAT_WAN;
-        // NatGetFlowByWan(src, sport, dst, dport) / NatGetFlowByHash(dst, dport, src, sport)
-        uint32_t rip = wan ? src : dst, rport = wan ? sport : dport;
-        const uint32_t lip = wan ? dst : src, lport = wan ? dport : sport;
-        if (p.nat_type != HALO_NAT_SYMMETRIC) { rip = 0; rport = 0; }  // :528-534
-        if (proto == kIpIcmp) rport = 0;                                  // :535-537
-        // 13-byte key (engine/ipv4_engine.go:452-458): rip | rport | lip | lport | proto, LE
-        const uint64_t w_lo = (uint64_t)rip | (uint64_t)rport << 32 | (uint64_t)(lip & 0xFFFFu) << 48;
-        const uint64_t w_hi = (uint64_t)(rport >> 8) | (uint64_t)lip << 8 | (uint64_t)lport << 40 |
-                              (uint64_t)proto << 56;  // key bytes 5..12
-        const uint64_t h = hash_9to16(w_lo, w_hi, 13);
+        const uint64_t h = flowkey::nat_hash(proto, src, dst, ports & 0xFFFFu, ports >> 16, p.kind, p.nat_type);
         p.hash[i] = h;
         if (p.bucket) p.bucket[i] = (uint32_t)(h % p.buckets);  // hashmap/hashmap.go:64
     }

@@ -34,6 +34,10 @@ struct RxParams {
     uint32_t own_ip;  // IpAddrToU(NetIf.IpAddr)
     halo_rx_result_t* out;
     uint32_t* hist;
+    // fused NAT flow-key hash of every record (halo_rx_parse_flow_batch_device), or null
+    uint64_t* flow_hash;
+    uint32_t* flow_bucket;
+    uint32_t flow_buckets, flow_kind, flow_nat;
 };
 
 // splitmix64 finaliser — the synthetic-traffic generator's only randomness source.

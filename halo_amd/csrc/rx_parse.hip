@@ -33,6 +33,7 @@
 #include <atomic>
 
 #include "device_util.h"
+#include "flow_key.h"
 #include "halo_common.h"
 
 namespace halo {
@@ -296,6 +297,15 @@ __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool 
             }
         }
         if (gl == 0 && p.hist) hist.add(v.status);
+#ifndef HALO_RX_FLOW_FUSE
+#define HALO_RX_FLOW_FUSE 1
+#endif
+        if (HALO_RX_FLOW_FUSE && gl == 0 && p.flow_hash) {  // the flow key from the record's fields (flow_key.h)
+            const uint64_t fh = flowkey::nat_hash(lo.y & 0xFFu, lo.z, lo.w, hi.x & 0xFFFFu, hi.x >> 16,
+                                                  p.flow_kind, p.flow_nat);
+            p.flow_hash[i] = fh;
+            if (p.flow_bucket) p.flow_bucket[i] = (uint32_t)(fh % p.flow_buckets);  // hashmap/hashmap.go:64
+        }
     }
 }
 
@@ -610,6 +620,32 @@ extern "C" HALO_API int halo_rx_parse_batch_device(const uint8_t* d_bytes, const
     p.bytes = d_bytes;
     p.offsets_dw = d_offsets_dw;
     p.lens = d_lens;
+    return halo::launch_parse(p, 0, max_len_hint, false, static_cast<hipStream_t>(stream));
+}
+
+extern "C" HALO_API int halo_rx_parse_flow_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                                        const uint16_t* d_lens, uint32_t n, uint32_t flags,
+                                                        const halo_rx_netif_t* netif, uint32_t max_len_hint,
+                                                        halo_rx_result_t* d_out, uint32_t* d_status_hist,
+                                                        uint32_t flow_kind, uint32_t nat_type, uint64_t* d_hash,
+                                                        uint32_t bucket_count, uint32_t* d_bucket,
+                                                        halo_stream_t stream) {
+    if (flow_kind > HALO_FLOW_NAT_WAN || !d_hash || (reinterpret_cast<uintptr_t>(d_hash) & 7u)) return HALO_E_INVAL;
+    if (d_bucket && bucket_count == 0) return HALO_E_INVAL;
+    halo::RxParams p{};
+    int rc = halo::fill_common(p, n, flags, netif, d_out, d_status_hist);
+    if (rc) return rc;
+    if (n == 0) return HALO_OK;
+    if (!d_bytes || !d_offsets_dw || !d_lens) return HALO_E_INVAL;
+    if ((rc = halo::check_device())) return rc;
+    p.bytes = d_bytes;
+    p.offsets_dw = d_offsets_dw;
+    p.lens = d_lens;
+    p.flow_hash = d_hash;
+    p.flow_bucket = d_bucket;
+    p.flow_buckets = bucket_count;
+    p.flow_kind = flow_kind;
+    p.flow_nat = nat_type;
     return halo::launch_parse(p, 0, max_len_hint, false, static_cast<hipStream_t>(stream));
 }
 

@@ -367,6 +367,17 @@ HALO_API int halo_flow_hash_device(const halo_rx_result_t* d_records, uint32_t n
                                    uint64_t* d_hash, uint32_t bucket_count, uint32_t* d_bucket,
                                    halo_stream_t stream);
 
+/* The rx parse (halo_rx_parse_batch_device, same arguments and records) with the NAT flow key
+ * of every record hashed in the same pass, exactly as halo_flow_hash_device would hash the
+ * records it writes: the engine's receive -> forward -> NAT lookup chain without re-reading the
+ * records. Full or compact records (flags); d_hash (8-byte aligned) and d_bucket as above.     */
+HALO_API int halo_rx_parse_flow_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                             const uint16_t* d_lens, uint32_t n, uint32_t flags,
+                                             const halo_rx_netif_t* netif, uint32_t max_len_hint,
+                                             halo_rx_result_t* d_out, uint32_t* d_status_hist,
+                                             uint32_t flow_kind, uint32_t nat_type, uint64_t* d_hash,
+                                             uint32_t bucket_count, uint32_t* d_bucket, halo_stream_t stream);
+
 /* ---- route lookup ---------------------------------------------------
  * RouteTable (engine/ipv4_engine.go:270-390): a binary trie of route lists, longest-prefix
  * FindRoute with an ECMP pick lastMatch[fnv32a(ip) % len] (engine/engine.go:159). The trie is

@@ -113,3 +113,53 @@ def test_flow_hash_validation(dev):
     r = torch.zeros(64, dtype=torch.uint8, device=dev)
     h = torch.zeros(2, dtype=torch.int64, device=dev)
     assert L.halo_flow_hash_device(r.data_ptr(), 2, 0, 0, h.data_ptr(), 0, h.data_ptr(), None) == _lib.HALO_E_INVAL
+
+
+@pytest.mark.parametrize("variant", [0, 1, 4, 8, 16, -1])
+def test_fused_parse_flow_hash(dev, oracle_lib, golden, variant):
+    """halo_rx_parse_flow_batch_device: the same records as the plain parse (full and compact),
+    and the flow hashes / buckets the oracle computes from those records — golden frames, a
+    structured-fuzz corpus and IMIX, every kernel variant."""
+    import torch
+
+    from halo_amd import _lib, protocol, synth
+    from halo_amd._lib import NetIf
+    from tests.helpers import golden_arrays
+
+    meta, blob = golden
+    data, offs, lens, _ = golden_arrays(meta, blob)
+    fdata, foffs, flens = oracle_lib.fuzz_batch(0xF10, 50_000, oracle_lib.NetIf.make())
+    lay = synth.layout(100_000, size_mode=1, proto_mode=3, mutate_shift=5, first_index=4242)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    batches = [(torch.from_numpy(d).to(dev), torch.from_numpy(o.view(np.int32)).to(dev),
+                torch.from_numpy(ln.view(np.int16)).to(dev), hint)
+               for d, o, ln, hint in ((data, offs, lens, 0), (fdata, foffs, flens, 0))]
+    batches.append((fr["bytes"], fr["offsets_dw"], fr["lens"], 1500))
+    stream = torch.cuda.current_stream().cuda_stream
+    _lib.check("variant", _lib.lib.halo_rx_tune_variant(variant))
+    try:
+        for d, o, ln, hint in batches:
+            n = int(ln.numel())
+            for compact in (False, True):
+                flags = 1 | (_lib.HALO_RX_RECORD_COMPACT if compact else 0)
+                width = 16 if compact else 32
+                ref = torch.empty((n, width), dtype=torch.uint8, device=dev)
+                _lib.check("parse", _lib.lib.halo_rx_parse_batch_device(
+                    d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, ref.data_ptr(), None,
+                    stream))
+                full = protocol.parse_frames_batch(d, o, ln, netif=NetIf.make(), max_len_hint=hint)
+                for kind, nat, buckets in ((1, 0, 1 << 20), (0, 1, 0), (0, 0, 1000003)):
+                    got = torch.full((n, width), 0xEE, dtype=torch.uint8, device=dev)
+                    h = torch.zeros(n, dtype=torch.int64, device=dev)
+                    b = torch.zeros(n, dtype=torch.int32, device=dev)
+                    _lib.check("fused", _lib.lib.halo_rx_parse_flow_batch_device(
+                        d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, got.data_ptr(),
+                        None, kind, nat, h.data_ptr(), buckets, b.data_ptr() if buckets else None, stream))
+                    torch.cuda.synchronize()
+                    assert torch.equal(got, ref), (variant, compact, kind)
+                    wh, wb = oracle_lib.flow_hash_batch(protocol.records(full), kind, nat, buckets)
+                    assert np.array_equal(h.cpu().numpy().view(np.uint64), wh), (variant, compact, kind, nat)
+                    if buckets:
+                        assert np.array_equal(b.cpu().numpy().view(np.uint32), wb)
+    finally:
+        _lib.lib.halo_rx_tune_variant(0)

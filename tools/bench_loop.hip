@@ -229,3 +229,18 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_stream_rw(const
     };
     return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
 }
+
+// The fused receive + NAT flow-key pass (halo_rx_parse_flow_batch_device), rotating batches.
+extern "C" __attribute__((visibility("default"))) int halo_bench_rx_flow_steps(
+    int nbatch, const uint8_t* const* bytes, const uint32_t* const* offsets_dw, const uint16_t* const* lens,
+    uint32_t n, uint32_t flags, const halo_rx_netif_t* netif, uint32_t hint, halo_rx_result_t* out, uint32_t kind,
+    uint32_t nat_type, uint64_t* hash, uint32_t buckets, uint32_t* bucket, int warmup, int steps, void* stream,
+    float* region_ms, double* wall_s) {
+    if (nbatch <= 0) return HALO_E_INVAL;
+    auto launch = [&](int k) {
+        const int b = k % nbatch;
+        return halo_rx_parse_flow_batch_device(bytes[b], offsets_dw[b], lens[b], n, flags, netif, hint, out, nullptr,
+                                               kind, nat_type, hash, buckets, bucket, stream);
+    };
+    return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
+}
