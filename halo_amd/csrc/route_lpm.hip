@@ -11,7 +11,8 @@
 // list inherited from above (16M first-level entries, 64 MB of HBM: a dependent pair of 4-byte
 // reads per lookup, served mostly from the 256 MB Infinity Cache).
 //
-// Data plane (device): per address, one or two table reads, then the ECMP pick of FindRoute:
+// Data plane (device): per address, one or two table reads; a one-route list is stored in the
+// table as the route id itself, otherwise the ECMP pick of FindRoute follows:
 // ids[start + fnv32a(ip) % count] (Go hash/fnv New32a over the 4 address bytes, the
 // RouteTable.IpHash of engine/engine.go:159); count 0 is the reference's divide-by-zero panic,
 // reported as HALO_ROUTE_PANIC.
@@ -47,7 +48,8 @@ struct halo_route_table {
 namespace halo {
 namespace {
 
-constexpr uint32_t kExt = 0x80000000u;  // tbl24 entry: index of a tbl8 block
+constexpr uint32_t kExt = 0x80000000u;     // tbl24 entry: index of a tbl8 block
+constexpr uint32_t kDirect = 0x40000000u;  // entry: the route id itself (a one-route list)
 
 struct Compiler {
     const halo_route_table& t;
@@ -56,8 +58,10 @@ struct Compiler {
     std::vector<uint2>& lists;
     std::vector<uint32_t>& ids;
 
-    // list reference (index + 1) of a node with a non-nil list
+    // table value of a node with a non-nil list: kDirect | id for a one-route list (no ECMP pick:
+    // the lookup is then a single table read), else the list reference (index + 1)
     uint32_t list_of(const halo_route_table::Node& n) {
+        if (n.ids.size() == 1 && n.ids[0] < kDirect) return kDirect | n.ids[0];
         const uint32_t start = (uint32_t)ids.size();
         ids.insert(ids.end(), n.ids.begin(), n.ids.end());
         lists.push_back(make_uint2(start, (uint32_t)n.ids.size()));
@@ -129,6 +133,7 @@ __device__ __forceinline__ uint32_t find_route(const LpmView& v, uint32_t ip) {
     uint32_t e = v.tbl24[ip >> 8];
     if (e & kExt) e = v.tbl8[(size_t)(e & ~kExt) * 256 + (ip & 0xFFu)];
     if (e == 0) return HALO_ROUTE_NONE;
+    if (e & kDirect) return e & ~kDirect;
     const uint2 l = v.lists[e - 1];
     if (l.y == 0) return HALO_ROUTE_PANIC;
     return v.ids[l.x + fnv1a32(ip) % l.y];
