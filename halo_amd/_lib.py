@@ -148,6 +148,9 @@ _PROTOS = {
     "halo_rx_parse_flow_batch_device": (ctypes.c_int, [
         _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf), ctypes.c_uint32, _u8p, _u8p,
         ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
+    "halo_rx_parse_route_batch_device": (ctypes.c_int, [
+        _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf), ctypes.c_uint32, _u8p, _u8p,
+        ctypes.c_void_p, _u8p, ctypes.c_void_p]),
     "halo_flow_hash_device": (ctypes.c_int, [
         _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_route_table_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),

@@ -38,6 +38,12 @@ struct RxParams {
     uint64_t* flow_hash;
     uint32_t* flow_bucket;
     uint32_t flow_buckets, flow_kind, flow_nat;
+    // fused FindRoute of every record's dst (halo_rx_parse_route_batch_device), or null
+    const uint32_t* rt_tbl24;
+    const uint32_t* rt_tbl8;
+    const uint2* rt_lists;
+    const uint32_t* rt_ids;
+    uint32_t* route_out;
 };
 
 // splitmix64 finaliser — the synthetic-traffic generator's only randomness source.

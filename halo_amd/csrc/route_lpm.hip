@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "halo_common.h"
+#include "route_view.h"
 
 struct halo_route_table {
     struct Node {
@@ -48,8 +49,6 @@ struct halo_route_table {
 namespace halo {
 namespace {
 
-constexpr uint32_t kExt = 0x80000000u;     // tbl24 entry: index of a tbl8 block
-constexpr uint32_t kDirect = 0x40000000u;  // entry: the route id itself (a one-route list)
 
 struct Compiler {
     const halo_route_table& t;
@@ -111,33 +110,6 @@ struct Compiler {
         }
     }
 };
-
-__device__ __forceinline__ uint32_t fnv1a32(uint32_t ip) {
-    uint32_t h = 2166136261u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        h ^= (ip >> (24 - 8 * k)) & 0xFFu;
-        h *= 16777619u;
-    }
-    return h;
-}
-
-struct LpmView {
-    const uint32_t* tbl24;
-    const uint32_t* tbl8;
-    const uint2* lists;
-    const uint32_t* ids;
-};
-
-__device__ __forceinline__ uint32_t find_route(const LpmView& v, uint32_t ip) {
-    uint32_t e = v.tbl24[ip >> 8];
-    if (e & kExt) e = v.tbl8[(size_t)(e & ~kExt) * 256 + (ip & 0xFFu)];
-    if (e == 0) return HALO_ROUTE_NONE;
-    if (e & kDirect) return e & ~kDirect;
-    const uint2 l = v.lists[e - 1];
-    if (l.y == 0) return HALO_ROUTE_PANIC;
-    return v.ids[l.x + fnv1a32(ip) % l.y];
-}
 
 // four addresses per lane (one 16-byte load), grid-stride
 __global__ void __launch_bounds__(256) lpm_kernel(const LpmView v, const uint32_t* ips, uint32_t n, uint32_t* out) {
@@ -299,6 +271,14 @@ extern "C" HALO_API int halo_route_sync_device(halo_route_table_t* t, int device
     t->synced = true;
     return HALO_OK;
 }
+
+namespace halo {
+int route_view(const halo_route_table_t* t, LpmView* out) {
+    if (!t || !t->synced || !out) return HALO_E_INVAL;
+    *out = LpmView{t->d_tbl24, t->d_tbl8, t->d_lists, t->d_ids};
+    return HALO_OK;
+}
+}  // namespace halo
 
 extern "C" HALO_API int halo_route_lookup_device(const halo_route_table_t* t, const uint32_t* d_ips, uint32_t n,
                                                  uint32_t* d_route_ids, halo_stream_t stream) {

@@ -35,6 +35,7 @@
 #include "device_util.h"
 #include "flow_key.h"
 #include "halo_common.h"
+#include "route_view.h"
 
 namespace halo {
 namespace {
@@ -306,6 +307,11 @@ __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool 
             p.flow_hash[i] = fh;
             if (p.flow_bucket) p.flow_bucket[i] = (uint32_t)(fh % p.flow_buckets);  // hashmap/hashmap.go:64
         }
+#ifndef HALO_RX_ROUTE_FUSE
+#define HALO_RX_ROUTE_FUSE 1
+#endif
+        if (HALO_RX_ROUTE_FUSE && gl == 0 && p.route_out)  // FindRoute(dst) (route_view.h)
+            p.route_out[i] = find_route(LpmView{p.rt_tbl24, p.rt_tbl8, p.rt_lists, p.rt_ids}, lo.w);
     }
 }
 
@@ -646,6 +652,31 @@ extern "C" HALO_API int halo_rx_parse_flow_batch_device(const uint8_t* d_bytes, 
     p.flow_buckets = bucket_count;
     p.flow_kind = flow_kind;
     p.flow_nat = nat_type;
+    return halo::launch_parse(p, 0, max_len_hint, false, static_cast<hipStream_t>(stream));
+}
+
+extern "C" HALO_API int halo_rx_parse_route_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                                         const uint16_t* d_lens, uint32_t n, uint32_t flags,
+                                                         const halo_rx_netif_t* netif, uint32_t max_len_hint,
+                                                         halo_rx_result_t* d_out, uint32_t* d_status_hist,
+                                                         const halo_route_table_t* table, uint32_t* d_route_ids,
+                                                         halo_stream_t stream) {
+    halo::LpmView v{};
+    if (halo::route_view(table, &v) || !d_route_ids) return HALO_E_INVAL;
+    halo::RxParams p{};
+    int rc = halo::fill_common(p, n, flags, netif, d_out, d_status_hist);
+    if (rc) return rc;
+    if (n == 0) return HALO_OK;
+    if (!d_bytes || !d_offsets_dw || !d_lens) return HALO_E_INVAL;
+    if ((rc = halo::check_device())) return rc;
+    p.bytes = d_bytes;
+    p.offsets_dw = d_offsets_dw;
+    p.lens = d_lens;
+    p.rt_tbl24 = v.tbl24;
+    p.rt_tbl8 = v.tbl8;
+    p.rt_lists = v.lists;
+    p.rt_ids = v.ids;
+    p.route_out = d_route_ids;
     return halo::launch_parse(p, 0, max_len_hint, false, static_cast<hipStream_t>(stream));
 }
 

@@ -413,6 +413,16 @@ HALO_API int halo_route_lookup_device(const halo_route_table_t* t, const uint32_
                                       uint32_t* d_route_ids, halo_stream_t stream);
 HALO_API int halo_route_lookup_records_device(const halo_route_table_t* t, const halo_rx_result_t* d_records,
                                               uint32_t n, uint32_t* d_route_ids, halo_stream_t stream);
+/* The rx parse (halo_rx_parse_batch_device, same arguments and records) with FindRoute of every
+ * record's dst_ip in the same pass — the RxIpv4 -> Ipv4RouteForward -> FindRoute chain
+ * (engine/ipv4_engine.go:18-47, :108-269, :351-390) without re-reading the records: d_route_ids
+ * equals halo_route_lookup_records_device over the records written.                         */
+HALO_API int halo_rx_parse_route_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                              const uint16_t* d_lens, uint32_t n, uint32_t flags,
+                                              const halo_rx_netif_t* netif, uint32_t max_len_hint,
+                                              halo_rx_result_t* d_out, uint32_t* d_status_hist,
+                                              const halo_route_table_t* table, uint32_t* d_route_ids,
+                                              halo_stream_t stream);
 
 /* ---- the reference engine's per-frame decision (engine/ethernet_engine.go:13-31,
  *      engine/ipv4_engine.go:18-47, engine/{udp,tcp,icmp}_engine.go) ------------------ */

@@ -108,6 +108,56 @@ def test_route_lookup_from_records(dev, oracle_lib):
     assert np.array_equal(rid.cpu().numpy().view(np.uint32), o.find_batch(recs["dst_ip"]))
 
 
+@pytest.mark.parametrize("variant", [0, 1, 4, 8, 16, -1])
+def test_fused_parse_route(dev, oracle_lib, golden, variant):
+    """halo_rx_parse_route_batch_device: records identical to the plain parse (full and compact)
+    and route ids identical to the oracle's FindRoute of each record's dst — golden frames and
+    IMIX, a table with a /32 to the NetIf, a /24, an ECMP group, an emptied list and a default."""
+    import torch
+
+    from halo_amd import _lib, protocol, synth
+    from halo_amd._lib import NetIf
+    from tests.helpers import golden_arrays
+
+    ops = [("add", [0, 0, 1, 0]), ("add", [0xC0A86400, 0xFFFFFF00, 0, 1]), ("add", [0xC0A86464, 0xFFFFFFFF, 0, 2]),
+           ("add", [0x0A000000, 0xFF000000, 5, 3]), ("add", [0x0A000000, 0xFF000000, 6, 3]),
+           ("add", [0x0A800000, 0xFF800000, 9, 1]), ("del", [0x0A800000, 0xFF800000, 9, 1])]
+    g, o = _replay_both(ops, oracle_lib)
+    g.sync()
+    meta, blob = golden
+    data, offs, lens, _ = golden_arrays(meta, blob)
+    lay = synth.layout(60_000, size_mode=1, proto_mode=3, mutate_shift=4, first_index=777)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    batches = [(torch.from_numpy(data).to(dev), torch.from_numpy(offs.view(np.int32)).to(dev),
+                torch.from_numpy(lens.view(np.int16)).to(dev), 0), (fr["bytes"], fr["offsets_dw"], fr["lens"], 1500)]
+    stream = torch.cuda.current_stream().cuda_stream
+    _lib.check("variant", _lib.lib.halo_rx_tune_variant(variant))
+    try:
+        for d, o_, ln, hint in batches:
+            n = int(ln.numel())
+            full = protocol.parse_frames_batch(d, o_, ln, netif=NetIf.make(), max_len_hint=hint)
+            want_ids = o.find_batch(protocol.records(full)["dst_ip"])
+            for compact in (False, True):
+                flags = 1 | (_lib.HALO_RX_RECORD_COMPACT if compact else 0)
+                width = 16 if compact else 32
+                ref = torch.empty((n, width), dtype=torch.uint8, device=dev)
+                _lib.check("parse", _lib.lib.halo_rx_parse_batch_device(
+                    d.data_ptr(), o_.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, ref.data_ptr(), None,
+                    stream))
+                got = torch.full((n, width), 0xEE, dtype=torch.uint8, device=dev)
+                rid = torch.zeros(n, dtype=torch.int32, device=dev)
+                _lib.check("fused", _lib.lib.halo_rx_parse_route_batch_device(
+                    d.data_ptr(), o_.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, got.data_ptr(), None,
+                    g._t, rid.data_ptr(), stream))
+                torch.cuda.synchronize()
+                assert torch.equal(got, ref), (variant, compact)
+                assert np.array_equal(rid.cpu().numpy().view(np.uint32), want_ids), (variant, compact)
+    finally:
+        _lib.lib.halo_rx_tune_variant(0)
+    assert _lib.lib.halo_rx_parse_route_batch_device(None, None, None, 0, 1, NetIf.make(), 0, None, None, None,
+                                                     None, None) == _lib.HALO_E_INVAL  # no table
+
+
 def test_route_validation(dev):
     import ctypes
 
