@@ -712,7 +712,7 @@ def main():
                    "parallelism": f"index-sharded x{d.world}, no collective"},
         "gbit_s": round(gbit, 2),
         "kernel_ms": round(kern_ms, 5),
-        "kernel": "rx_lane_kernel<0> (lane per frame, ragged)",
+        "kernel": "rx_lane_kernel<0, 0> (lane per frame, ragged, no fused pass)",
         "roofline": roofline(alg, kern_ms, load_traffic("config2")),
         "alg_bytes_per_launch": alg,
         "cpu_baseline": None,

@@ -251,7 +251,10 @@ __device__ __forceinline__ void frame_header(const FrameState<G>& st, uint32_t g
 // Verdict after the L4 segment sum (this lane's or group's partial `c`), record store and count.
 // `stage` (lane-per-frame only): write the record to this wave's LDS staging slot instead of
 // global memory; the wave then stores its 64 consecutive records fully coalesced.
-template <int G>
+// FUSE (compile time, so the plain parse carries none of it): 1 = hash every record's NAT flow
+// key (halo_rx_parse_flow_batch_device), 2 = FindRoute of every record's dst
+// (halo_rx_parse_route_batch_device).
+template <int G, int FUSE = 0>
 __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool present, uint32_t gl,
                                             const uint32_t (&h)[12], Verdict& v, uint64_t c, Hist& hist,
                                             uint4* stage = nullptr) {
@@ -298,19 +301,13 @@ __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool 
             }
         }
         if (gl == 0 && p.hist) hist.add(v.status);
-#ifndef HALO_RX_FLOW_FUSE
-#define HALO_RX_FLOW_FUSE 1
-#endif
-        if (HALO_RX_FLOW_FUSE && gl == 0 && p.flow_hash) {  // the flow key from the record's fields (flow_key.h)
+        if (FUSE == 1 && gl == 0) {  // the flow key from the record's own fields (flow_key.h)
             const uint64_t fh = flowkey::nat_hash(lo.y & 0xFFu, lo.z, lo.w, hi.x & 0xFFFFu, hi.x >> 16,
                                                   p.flow_kind, p.flow_nat);
             p.flow_hash[i] = fh;
             if (p.flow_bucket) p.flow_bucket[i] = (uint32_t)(fh % p.flow_buckets);  // hashmap/hashmap.go:64
         }
-#ifndef HALO_RX_ROUTE_FUSE
-#define HALO_RX_ROUTE_FUSE 1
-#endif
-        if (HALO_RX_ROUTE_FUSE && gl == 0 && p.route_out)  // FindRoute(dst) (route_view.h)
+        if (FUSE == 2 && gl == 0)  // FindRoute(dst) (route_view.h)
             p.route_out[i] = find_route(LpmView{p.rt_tbl24, p.rt_tbl8, p.rt_lists, p.rt_ids}, lo.w);
     }
 }
@@ -319,7 +316,7 @@ __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool 
 // traffic). Every lane of a group calls it with the same i / present (other groups may be doing
 // the same for other frames); `present` false means "no frame": nothing is read or written,
 // but the group still executes the collective steps.
-template <int G>
+template <int G, int FUSE = 0>
 __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool present, uint32_t gl,
                                              uint32_t grp_base, FrameState<G>& st, Hist& hist,
                                              uint4* stage = nullptr) {
@@ -347,17 +344,17 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
             for (int u = 0; u < U; ++u) acc_segment(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
         }
     }
-    frame_store<G>(p, i, present, gl, h, v, c, hist, stage);
+    frame_store<G, FUSE>(p, i, present, gl, h, v, c, hist, stage);
 }
 
 // The whole chain for frame i on a group of G lanes.
-template <int G, int LAYOUT>
+template <int G, int LAYOUT, int FUSE>
 __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, bool present, uint32_t gl,
                                               uint32_t grp_base, Hist& hist) {
     FrameState<G> st;
     frame_meta<LAYOUT>(p, i, present, st);
     frame_loads<G>(gl, st);
-    frame_finish<G>(p, i, present, gl, grp_base, st, hist);
+    frame_finish<G, FUSE>(p, i, present, gl, grp_base, st, hist);
 }
 
 __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
@@ -371,7 +368,7 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
 }
 
 // Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
-template <int G, int LAYOUT>
+template <int G, int LAYOUT, int FUSE>
 __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     constexpr uint32_t FPW = 64 / G;  // frames per wave
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
@@ -386,7 +383,7 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t base = wave * FPW; base < p.n; base += nwaves * FPW) {
         const uint32_t i = base + lane / G;
-        process_frame<G, LAYOUT>(p, i, i < p.n, gl, grp_base, hist);
+        process_frame<G, LAYOUT, FUSE>(p, i, i < p.n, gl, grp_base, hist);
     }
     flush_hist(p, hist);
 }
@@ -397,7 +394,7 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
 // consecutive: they are staged in LDS and written with fully coalesced 16-byte stores (a lane
 // writing its own 32 B record at a 32 B stride stored the same bytes 25 % slower:
 // profiles/r01/probe_store_patterns.log).
-template <int LAYOUT>
+template <int LAYOUT, int FUSE>
 #ifndef HALO_RX_LANE_WAVES
 #define HALO_RX_LANE_WAVES 0
 #endif
@@ -421,7 +418,7 @@ rx_lane_kernel(const RxParams p) {
         FrameState<1> st;
         frame_meta<LAYOUT>(p, i, i < p.n, st);
         frame_loads<1>(0, st);
-        frame_finish<1>(p, i, i < p.n, 0, lane, st, hist, &s_rec[w][compact ? lane : 2 * lane]);
+        frame_finish<1, FUSE>(p, i, i < p.n, 0, lane, st, hist, &s_rec[w][compact ? lane : 2 * lane]);
         __builtin_amdgcn_wave_barrier();
         const uint32_t nrec = p.n - base < 64 ? p.n - base : 64;  // records of this wave
         if (compact) {
@@ -440,11 +437,11 @@ rx_lane_kernel(const RxParams p) {
 #ifndef HALO_RX_GROUP_WAVES
 #define HALO_RX_GROUP_WAVES 5
 #endif
-template <int G, int LAYOUT>
+template <int G, int LAYOUT, int FUSE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_RX_GROUP_WAVES)))
 rx_group_kernel(const RxParams p) {
     static_assert(G == 4 || G == 8 || G == 16, "G must be 4, 8 or 16");
-    group_kernel_body<G, LAYOUT>(p);
+    group_kernel_body<G, LAYOUT, FUSE>(p);
 }
 
 // Mixed sizes (IMIX): each wave takes a window of 256 consecutive frames (four per lane), sorts
@@ -459,7 +456,7 @@ rx_group_kernel(const RxParams p) {
 constexpr uint32_t kMixWindow = HALO_RX_MIX_WINDOW;  // frames per wave window (a multiple of 64)
 constexpr int kMixPer = (int)(kMixWindow / 64);      // frames per lane in the classification
 
-template <int G>
+template <int G, int FUSE>
 __device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, uint32_t e_end, uint32_t lane,
                                          const uint64_t* s_ptr, const uint32_t* s_idx, const uint16_t* s_len,
                                          uint32_t eth_max, Hist& hist) {
@@ -474,11 +471,11 @@ __device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, ui
         st.L = has ? s_len[e] : 0u;
         st.ndw = (has && st.L >= kEthMin && st.L <= eth_max) ? (st.L + 3) >> 2 : 0;
         frame_loads<G>(gl, st);
-        frame_finish<G>(p, has ? s_idx[e] : 0u, has, gl, grp_base, st, hist);
+        frame_finish<G, FUSE>(p, has ? s_idx[e] : 0u, has, gl, grp_base, st, hist);
     }
 }
 
-template <int LAYOUT>
+template <int LAYOUT, int FUSE>
 #ifndef HALO_RX_MIX_WAVES
 #define HALO_RX_MIX_WAVES 4
 #endif
@@ -536,10 +533,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
         }
         const uint32_t st0 = start[0], st1 = start[1], st2 = start[2], st3 = start[3], nall = start[4];
         __builtin_amdgcn_wave_barrier();
-        mix_pass<1>(p, st0, st1, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
-        mix_pass<4>(p, st1, st2, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
-        mix_pass<8>(p, st2, st3, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
-        mix_pass<16>(p, st3, nall, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        mix_pass<1, FUSE>(p, st0, st1, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        mix_pass<4, FUSE>(p, st1, st2, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        mix_pass<8, FUSE>(p, st2, st3, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        mix_pass<16, FUSE>(p, st3, nall, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
         __builtin_amdgcn_wave_barrier();
     }
     flush_hist(p, hist);
@@ -555,15 +552,15 @@ uint32_t grid_for(uint64_t n, uint32_t frames_per_wave) {
     return (uint32_t)(blocks > kMaxBlocks ? kMaxBlocks : blocks);
 }
 
-template <int LAYOUT>
+template <int LAYOUT, int FUSE = 0>
 hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     const dim3 block(256);
     switch (variant) {
-        case 1: hipLaunchKernelGGL((rx_lane_kernel<LAYOUT>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
-        case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
-        case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
-        case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
-        default: hipLaunchKernelGGL((rx_mix_kernel<LAYOUT>), dim3(grid_for(p.n, kMixWindow)), block, 0, s, p); break;
+        case 1: hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
+        case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT, FUSE>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
+        case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT, FUSE>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
+        case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT, FUSE>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
+        default: hipLaunchKernelGGL((rx_mix_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, kMixWindow)), block, 0, s, p); break;
     }
     return hipGetLastError();
 }
@@ -586,7 +583,10 @@ int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, 
     const int v = pick_variant(max_len, uniform);
     hipError_t e;
     switch (layout) {
-        case 0: e = launch_variant<0>(p, v, s); break;
+        case 0:  // ragged: the only layout with the fused passes
+            e = p.flow_hash ? launch_variant<0, 1>(p, v, s)
+              : p.route_out ? launch_variant<0, 2>(p, v, s) : launch_variant<0, 0>(p, v, s);
+            break;
         case 1: e = launch_variant<1>(p, v, s); break;
         default: e = launch_variant<2>(p, v, s); break;
     }
