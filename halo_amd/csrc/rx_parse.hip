@@ -207,11 +207,12 @@ template <int G>
 constexpr int kRound0 = 4;
 
 // One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
-template <int G>
+template <int G, int R0 = kRound0<G>>
 struct FrameState {
+    static constexpr int kR0 = R0;
     const uint8_t* frame;
     uint32_t L, ndw;
-    uint32_t buf[kRound0<G>][4];  // round 0: chunks (u*G + gl) of 16 bytes
+    uint32_t buf[R0][4];  // round 0: chunks (u*G + gl) of 16 bytes
 };
 
 template <int LAYOUT, typename FS>
@@ -226,15 +227,15 @@ __device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool p
 
 // Round 0: four 16-byte chunks per lane issued back to back, bounded by the frame length (the
 // L4 end is not known before the header is parsed, and never exceeds the frame length).
-template <int G>
-__device__ __forceinline__ void frame_loads(uint32_t gl, FrameState<G>& st) {
+template <int G, int R0>
+__device__ __forceinline__ void frame_loads(uint32_t gl, FrameState<G, R0>& st) {
 #pragma unroll
-    for (int u = 0; u < kRound0<G>; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
+    for (int u = 0; u < R0; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
 }
 
 // Header dwords 0..11 of the frame: the lane's own chunks (G = 1) or chunk 0 of group lanes 0..2.
-template <int G>
-__device__ __forceinline__ void frame_header(const FrameState<G>& st, uint32_t grp_base, uint32_t (&h)[12]) {
+template <int G, int R0>
+__device__ __forceinline__ void frame_header(const FrameState<G, R0>& st, uint32_t grp_base, uint32_t (&h)[12]) {
     if constexpr (G == 1) {
 #pragma unroll
         for (int j = 0; j < 12; ++j) h[j] = st.buf[j >> 2][j & 3];
@@ -316,18 +317,17 @@ __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool 
 // traffic). Every lane of a group calls it with the same i / present (other groups may be doing
 // the same for other frames); `present` false means "no frame": nothing is read or written,
 // but the group still executes the collective steps.
-template <int G, int FUSE = 0>
-__device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool present, uint32_t gl,
-                                             uint32_t grp_base, FrameState<G>& st, Hist& hist,
-                                             uint4* stage = nullptr) {
-    constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
-    constexpr int U0 = kRound0<G>;    // chunks already loaded
 #ifndef HALO_RX_LATER_CHUNKS
 #define HALO_RX_LATER_CHUNKS 8
 #endif
-    constexpr int U = HALO_RX_LATER_CHUNKS;  // 16-byte chunks in flight per lane per later round
+template <int G, int FUSE = 0, int U = HALO_RX_LATER_CHUNKS, int R0 = kRound0<G>>  // U: 16-byte chunks in flight per lane per later round
+__device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool present, uint32_t gl,
+                                             uint32_t grp_base, FrameState<G, R0>& st, Hist& hist,
+                                             uint4* stage = nullptr) {
+    constexpr uint32_t STEP = 4 * G;  // dwords per group per load step
+    constexpr int U0 = R0;            // chunks already loaded
     uint32_t h[12];
-    frame_header<G>(st, grp_base, h);
+    frame_header(st, grp_base, h);
     Verdict v = parse_header(h, st.L, present, p);
 
     // L4 segment sum over [34, seg_end): round 0 from registers, then U chunks per round
@@ -455,6 +455,34 @@ rx_group_kernel(const RxParams p) {
 #endif
 constexpr uint32_t kMixWindow = HALO_RX_MIX_WINDOW;  // frames per wave window (a multiple of 64)
 constexpr int kMixPer = (int)(kMixWindow / 64);      // frames per lane in the classification
+#ifndef HALO_RX_MIX_MAX_G
+#define HALO_RX_MIX_MAX_G 16  // 8: frames > 4096 B take the 8-lane pass (no 16-lane pass compiled)
+#endif
+
+// Later-round chunks per lane in the mix passes: just enough for each class's size range in one
+// later round trip (<= 128 B: 64 + 4*16 B; 570 B on 4 lanes: 256 + 5*64 B; 1500 B on 8 lanes:
+// 512 + 8*128 B), so the short classes' passes do not hold the buffers the long ones need.
+// IMIX 1.60 -> 1.58 ms, 570 B 150 -> 147 us (profiles/r01/ab_r43_mix_later_small.log, 5 vs 6
+// chunks for 570 B: ab_r43_mix_later_g4.log).
+#ifndef HALO_RX_MIX_LATER_SMALL
+#define HALO_RX_MIX_LATER_SMALL 1
+#endif
+#ifndef HALO_RX_MIX_LATER_G4
+#define HALO_RX_MIX_LATER_G4 5
+#endif
+template <int G>
+constexpr int kMixLater = !HALO_RX_MIX_LATER_SMALL ? HALO_RX_LATER_CHUNKS
+                        : G == 1 ? 4 : G == 4 ? HALO_RX_MIX_LATER_G4 : HALO_RX_LATER_CHUNKS;
+
+// Round-0 chunks per lane in the mix passes (HALO_RX_MIX_ROUND0=1): 570 B on 4 lanes in one round
+// trip (9 x 64 B >= 576 B), 1500 B on 8 lanes in one (12 x 128 B >= 1536 B). Off: the bigger round
+// 0 spills at occupancy 4 (IMIX 2.06 ms) and at occupancy 3 is slower still than two round trips
+// (IMIX 1.69 ms, 570 B 173 us; profiles/r01/ab_r43_mix_round0_rejected.log).
+#ifndef HALO_RX_MIX_ROUND0
+#define HALO_RX_MIX_ROUND0 0
+#endif
+template <int G>
+constexpr int kMixRound0 = !HALO_RX_MIX_ROUND0 ? kRound0<G> : G == 4 ? 9 : G == 8 && HALO_RX_MIX_ROUND0 >= 2 ? 12 : kRound0<G>;
 
 template <int G, int FUSE>
 __device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, uint32_t e_end, uint32_t lane,
@@ -466,12 +494,12 @@ __device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, ui
     for (uint32_t e0 = e_begin; e0 < e_end; e0 += FPW) {
         const uint32_t e = e0 + lane / G;
         const bool has = e < e_end;
-        FrameState<G> st;
+        FrameState<G, kMixRound0<G>> st;
         st.frame = has ? reinterpret_cast<const uint8_t*>(s_ptr[e]) : p.bytes;
         st.L = has ? s_len[e] : 0u;
         st.ndw = (has && st.L >= kEthMin && st.L <= eth_max) ? (st.L + 3) >> 2 : 0;
-        frame_loads<G>(gl, st);
-        frame_finish<G, FUSE>(p, has ? s_idx[e] : 0u, has, gl, grp_base, st, hist);
+        frame_loads(gl, st);
+        frame_finish<G, FUSE, kMixLater<G>, kMixRound0<G>>(p, has ? s_idx[e] : 0u, has, gl, grp_base, st, hist);
     }
 }
 
@@ -504,7 +532,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
             if (i < p.n) frame_at<LAYOUT>(p, i, fp[k], fl[k]);
             cls[k] = i >= p.n ? 4u
                    : (fl[k] <= 128 || fl[k] > eth_max) ? 0u
-                   : fl[k] <= 1024 ? 1u : fl[k] <= 4096 ? 2u : 3u;
+                   : fl[k] <= 1024 ? 1u : (HALO_RX_MIX_MAX_G < 16 || fl[k] <= 4096) ? 2u : 3u;
         }
         // counting sort by class: one ballot live at a time
         uint32_t pos[kMixPer];
@@ -536,7 +564,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
         mix_pass<1, FUSE>(p, st0, st1, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
         mix_pass<4, FUSE>(p, st1, st2, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
         mix_pass<8, FUSE>(p, st2, st3, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
-        mix_pass<16, FUSE>(p, st3, nall, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        if constexpr (HALO_RX_MIX_MAX_G >= 16)
+            mix_pass<16, FUSE>(p, st3, nall, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
         __builtin_amdgcn_wave_barrier();
     }
     flush_hist(p, hist);
