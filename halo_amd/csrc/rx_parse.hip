@@ -571,13 +571,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
     flush_hist(p, hist);
 }
 
+#ifndef HALO_RX_MAX_BLOCKS
+#define HALO_RX_MAX_BLOCKS (256ull * 8 * 8)  // 256 CUs x 8 resident blocks x 8 rounds
+#endif
+#ifndef HALO_RX_LANE_MAX_BLOCKS
+#define HALO_RX_LANE_MAX_BLOCKS HALO_RX_MAX_BLOCKS
+#endif
 constexpr int kVariantMix = -1;
 std::atomic<int> g_force_variant{0};  // tuning hook (halo_rx_tune_variant); 0 = automatic
 
-uint32_t grid_for(uint64_t n, uint32_t frames_per_wave) {
+uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS) {
     const uint64_t waves = (n + frames_per_wave - 1) / frames_per_wave;
     uint64_t blocks = (waves + 3) / 4;
-    const uint64_t kMaxBlocks = 256ull * 8 * 8;  // 256 CUs x 8 resident blocks x 8 rounds
+    const uint64_t kMaxBlocks = max_blocks;
     return (uint32_t)(blocks > kMaxBlocks ? kMaxBlocks : blocks);
 }
 
@@ -585,7 +591,7 @@ template <int LAYOUT, int FUSE = 0>
 hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     const dim3 block(256);
     switch (variant) {
-        case 1: hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
+        case 1: hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64, HALO_RX_LANE_MAX_BLOCKS)), block, 0, s, p); break;
         case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT, FUSE>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
         case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT, FUSE>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
         case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT, FUSE>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
