@@ -549,7 +549,9 @@ struct halo_rx_ring {
 };
 
 namespace {
-void free_ring(halo_rx_ring* r) {
+// Returns false when the ring memory could not be unregistered (the caller must not free it then:
+// the pages stay mapped for the device).
+bool free_ring(halo_rx_ring* r) {
     for (hipEvent_t e : r->ev)
         if (e) (void)hipEventDestroy(e);
     if (r->s_copy) (void)hipStreamDestroy(r->s_copy);
@@ -567,8 +569,11 @@ void free_ring(halo_rx_ring* r) {
     if (r->h_soff) (void)hipHostFree(r->h_soff);
     if (r->h_slen) (void)hipHostFree(r->h_slen);
     if (r->h_sres) (void)hipHostFree(r->h_sres);
-    if (r->registered) (void)hipHostUnregister(r->mem);
+    bool ok = true;
+    if (r->registered) ok = hipHostUnregister(r->mem) == hipSuccess;
+    if (!ok) (void)hipGetLastError();  // do not leave the error for a later launch check
     delete r;
+    return ok;
 }
 
 // Device address of host memory [p, p + bytes) when it is pinned or registered in one piece,
@@ -769,8 +774,7 @@ extern "C" HALO_API int halo_rx_ring_detach(halo_rx_ring_t* r) {
     if (r->s_copy) (void)hipStreamSynchronize(r->s_copy);
     if (r->s_comp) (void)hipStreamSynchronize(r->s_comp);
     if (r->s_d2h) (void)hipStreamSynchronize(r->s_d2h);
-    free_ring(r);
-    return HALO_OK;
+    return free_ring(r) ? HALO_OK : HALO_E_HIP;
 }
 
 // One poll, pipelined over 16 MiB pieces of the span: every piece's H2D copy is queued at once on

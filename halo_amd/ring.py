@@ -88,6 +88,9 @@ class RingBuffer:
         return self.data[idx].tobytes()
 
 
+_leaked: list = []  # arrays whose host registration could not be removed (see RingConsumer.close)
+
+
 class RingConsumer:
     """The GPU consumer of one ring (halo_rx_ring_attach). ``capacity`` is ReadPacket's
     ``len(data)`` (1514 in the DPDK driver and Wire). ``small_poll``: spans up to this many bytes
@@ -112,12 +115,20 @@ class RingConsumer:
                                                                            self._out.nbytes) == 0
 
     def close(self):
+        """Detach from the ring and unregister the record array. Raises HaloError if either
+        registration could not be removed: the memory then stays mapped for the device, so the
+        consumer keeps references to both arrays instead of letting them be freed."""
         if getattr(self, "_h", None):
-            _lib.lib.halo_rx_ring_detach(self._h)
+            rc = _lib.lib.halo_rx_ring_detach(self._h)
             self._h = None
+            rc2 = _lib.HALO_OK
             if self._out_registered:
-                _lib.lib.halo_rx_host_unregister(self._out.ctypes.data)
+                rc2 = _lib.lib.halo_rx_host_unregister(self._out.ctypes.data)
                 self._out_registered = False
+            if rc != _lib.HALO_OK or rc2 != _lib.HALO_OK:
+                _leaked.append((self.ring, self._out))  # still registered: never free them
+                _lib.check("halo_rx_ring_detach" if rc != _lib.HALO_OK else "halo_rx_host_unregister",
+                           rc if rc != _lib.HALO_OK else rc2)
 
     def __del__(self):
         self.close()

@@ -261,6 +261,8 @@ typedef struct halo_rx_ring halo_rx_ring_t;
 HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t offset, uint32_t capacity,
                                  uint64_t max_bytes, uint32_t max_frames, uint32_t attach_flags,
                                  halo_rx_ring_t** out);
+/* Synchronises the ring's streams and frees its resources. HALO_E_HIP: the ring memory could not be
+ * unregistered (the caller must then keep it allocated). */
 HALO_API int halo_rx_ring_detach(halo_rx_ring_t* ring);
 /* Parse the next frames (flags: HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT; full records). They
  * stay in the ring until commit: positions[i] (optional) is frame i's record position in the
