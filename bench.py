@@ -608,11 +608,18 @@ def e2e_host(dev, netif, steps: int):
                         ("e2e_host_imix_4M", dict(size_mode=1, proto_mode=3), 4 << 20)]:
         fr = make_batches(dev, netif, n=n, rotate=1, rank=0, **kw)[0]
         lay = fr["layout"]
-        host = fr["bytes"].cpu().numpy()
-        offs = lay["offsets_dw"].astype(np.uint64) * 4
+        # every array is registered below: each on pages of its own (_lib.host_array)
+        def own_pages(a):
+            b = _lib.host_array(a.shape, a.dtype)
+            b[...] = a
+            return b
+
+        host = own_pages(fr["bytes"].cpu().numpy())
+        offs = own_pages(lay["offsets_dw"].astype(np.uint64) * 4)
         hb = HostBatcher(dev.index or 0)
-        out = np.zeros(n, dtype=_lib.RESULT_DTYPE)  # touched once: no page faults in the timed loop
-        lens = np.ascontiguousarray(lay["lens"])
+        out = _lib.host_array(n, _lib.RESULT_DTYPE)
+        out.view(np.uint8)[:] = 0  # touched once: no page faults in the timed loop
+        lens = own_pages(np.ascontiguousarray(lay["lens"]))
         for registered in (True, False):
             # registered: frames, offsets, lengths and the record array all pinned in place (the
             # offsets then become dword offsets on the GPU, no per-frame host loop)

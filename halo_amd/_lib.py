@@ -94,6 +94,23 @@ assert RING_SCAN_DTYPE.itemsize == 24
 RING_STOP_NAMES = ("EMPTY", "BAD_LEN", "PARTIAL", "CAPACITY", "MAX", "BAD_CURSOR")
 RING_STOP = {name: code for code, name in enumerate(RING_STOP_NAMES)}
 RING_REGISTER = 0x1
+
+def host_array(shape, dtype=np.uint8) -> np.ndarray:
+    """A zeroed host array on pages of its own: an anonymous mmap, page-aligned, its size rounded
+    up to whole pages, unmapped when the array is freed. For every buffer handed to
+    ``halo_rx_host_register`` or attached with ``RING_REGISTER``: hipHostRegister pins whole pages,
+    so a heap array (np.zeros) can share its first or last page with an unrelated allocation that
+    outlives the registration, and a later transfer that pins that neighbour in place then meets a
+    stale mapping. Pages that only this array uses go back to the OS with it."""
+    import mmap
+
+    dt = np.dtype(dtype)
+    shape = (shape,) if isinstance(shape, (int, np.integer)) else tuple(shape)
+    nbytes = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    size = max(mmap.PAGESIZE, -(-nbytes // mmap.PAGESIZE) * mmap.PAGESIZE)
+    buf = mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    return np.frombuffer(buf, dtype=np.uint8, count=nbytes).view(dt).reshape(shape)
+
 RING_HEADER = 128  # sizeof(RingBuffer), mem/ring_buffer.go:18-26
 
 

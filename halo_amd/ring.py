@@ -28,17 +28,11 @@ WIRE_MAX_PACKET_SIZE = 1514  # engine/engine.go:507
 MAX_PACKET_SIZE = 1514       # dpdk/dpdk.go:20 (EthQueueRxPkt's receive buffer)
 
 
-def _aligned(nbytes: int, align: int = 64) -> np.ndarray:
-    raw = np.zeros(nbytes + align, dtype=np.uint8)
-    off = (-raw.ctypes.data) % align
-    return raw[off:off + nbytes]
-
-
 class RingBuffer:
     """A RingBuffer (128-byte header + ``data_size``-byte power-of-two data area) in host memory."""
 
     def __init__(self, data_size: int = 8 << 20):
-        self.mem = _aligned(RING_HEADER + data_size)
+        self.mem = _lib.host_array(RING_HEADER + data_size)  # pages of its own: it may be registered
         _lib.check("halo_ring_create", _lib.lib.halo_ring_create(self.mem.ctypes.data, self.mem.nbytes))
         self.size = data_size
 
@@ -109,7 +103,7 @@ class RingConsumer:
             _lib.check("halo_rx_ring_set_small_poll", _lib.lib.halo_rx_ring_set_small_poll(h, small_poll))
         cap = max_bytes or min(ring.size, 256 << 20)
         self.max_frames = min(max_frames or (1 << 32) - 1, min(cap, ring.size) // 8)
-        self._out = np.zeros(self.max_frames, dtype=RESULT_DTYPE)
+        self._out = _lib.host_array(self.max_frames, RESULT_DTYPE)  # registered below: pages of its own
         # the records come back by DMA straight into this array: pin it too
         self._out_registered = register and _lib.lib.halo_rx_host_register(self._out.ctypes.data,
                                                                            self._out.nbytes) == 0

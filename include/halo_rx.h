@@ -205,7 +205,10 @@ HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* by
 /* Frames whose offsets are ascending and 4-byte aligned relative to each other (a drained ring
  * segment, a packed batch) are sent with one DMA per chunk straight from `bytes`; registering
  * that memory (e.g. the ring's hugepages) makes the DMA run at full PCIe rate. Other batches
- * are repacked into pinned staging by the CPU.                                            */
+ * are repacked into pinned staging by the CPU.
+ * Registration pins whole pages: register memory whose pages no other allocation shares
+ * (page-aligned, as hugepages and mmap regions are; halo_amd._lib.host_array in Python), and
+ * unregister it before it is freed.                                                       */
 HALO_API int halo_rx_host_register(const void* ptr, uint64_t bytes);
 HALO_API int halo_rx_host_unregister(const void* ptr);
 
@@ -240,7 +243,8 @@ HALO_API int halo_rx_shard_multi(halo_rx_host_ctx_t* const* ctxs, uint32_t n_ctx
                                         ReadPacket leaves it, and the tail, in place              */
 #define HALO_RING_STOP_MAX 4u        /* max_frames taken, more records available                  */
 #define HALO_RING_STOP_BAD_CURSOR 5u /* head - tail > size: ReadPacket returns false              */
-#define HALO_RING_REGISTER 0x1u      /* attach: hipHostRegister the ring for full-rate DMA         */
+#define HALO_RING_REGISTER 0x1u      /* attach: hipHostRegister the ring for full-rate DMA (its pages
+                                        must not be shared: see halo_rx_host_register)              */
 
 typedef struct halo_rx_ring_scan {
     uint32_t n_frames;  /* frames taken                                                      */

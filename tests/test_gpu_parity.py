@@ -385,6 +385,9 @@ def test_host_path_direct_dma_registered(dev, oracle_lib):
     data = oracle_lib.synth_batch(synth.SEED, 9_000_000, lay["lens"], lay["kinds"], oracle_lib.NetIf.make(),
                                   offsets_dw=lay["offsets_dw"], fill=0x77)
     offs = lay["offsets_dw"].astype(np.uint64) * 4
+    reg = _lib.host_array(data.shape, data.dtype)  # registered below: pages of its own
+    reg[...] = data
+    data = reg
     want, whist = oracle_lib.rx_batch(data, lay["lens"], oracle_lib.NetIf.make(), 1, offsets_dw=lay["offsets_dw"])
     hb = HostBatcher(0, chunk_frames=3000, chunk_bytes=1 << 20)
     for registered in (False, True):

@@ -262,7 +262,8 @@ def test_small_poll_unpinned_out_and_unregistered_ring(dev, golden, oracle_lib):
         cons = RingConsumer(ring, capacity=1514, register=register)
         if not register:
             assert _lib.lib.halo_rx_ring_set_small_poll(cons._h, 1 << 16) == _lib.HALO_E_INVAL
-        out = np.full(len(sel) + 5, 0xEE, np.uint8).repeat(32).view(_lib.RESULT_DTYPE)
+        out = _lib.host_array(len(sel) + 5, _lib.RESULT_DTYPE)  # registered below: pages of its own
+        out.view(np.uint8)[:] = 0xEE
         info = np.zeros(1, RING_SCAN_DTYPE)
         hist = np.zeros(14, np.uint32)
         _lib.check("poll", _lib.lib.halo_rx_ring_poll(cons._h, 1, NetIf.make(), out.ctypes.data, hist.ctypes.data,
