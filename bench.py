@@ -20,6 +20,7 @@ cache-resident variant of the headline; N=1 only).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -624,16 +625,15 @@ def e2e_host(dev, netif, steps: int):
             # registered: frames, offsets, lengths and the record array all pinned in place (the
             # offsets then become dword offsets on the GPU, no per-frame host loop)
             pinned = (host, offs, lens, out) if registered else ()
-            for a in pinned:
-                _lib.check("register", _lib.lib.halo_rx_host_register(a.ctypes.data, a.nbytes))
-            hb.parse(host, offs, lens, netif, 1, out=out)  # warm
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                hb.parse(host, offs, lens, netif, 1, out=out)
-            el = (time.perf_counter() - t0) / steps
-            for a in pinned:
-                _lib.lib.halo_rx_host_unregister(a.ctypes.data)
+            with contextlib.ExitStack() as regs:  # unregistered on exit, checked, even on error
+                for a in pinned:
+                    regs.enter_context(_lib.registered(a))
+                hb.parse(host, offs, lens, netif, 1, out=out)  # warm
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    hb.parse(host, offs, lens, netif, 1, out=out)
+                el = (time.perf_counter() - t0) / steps
             fb = int(lay["lens"].astype(np.int64).sum())
             res[name + ("_registered" if registered else "_pageable")] = {
                 "frames": n, "mpps": round(n / el / 1e6, 1), "gbit_s": round(fb * 8 / el / 1e9, 1),

@@ -111,6 +111,52 @@ def host_array(shape, dtype=np.uint8) -> np.ndarray:
     buf = mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
     return np.frombuffer(buf, dtype=np.uint8, count=nbytes).view(dt).reshape(shape)
 
+def host_pages(nbytes: int) -> int:
+    """The whole-page size host_array maps for `nbytes` (what a registration of it covers)."""
+    import mmap
+
+    return max(mmap.PAGESIZE, -(-int(nbytes) // mmap.PAGESIZE) * mmap.PAGESIZE)
+
+
+_leaked: list = []  # host arrays whose registration could not be removed: never freed
+
+
+class registered:
+    """``with registered(arr):`` — halo_rx_host_register over the whole pages of a host_array for
+    the block, unregistered on exit even when the block raises. If the unregistration fails the
+    array is kept alive for the rest of the process (its pages may still be mapped for the
+    device) and HaloError is raised."""
+
+    def __init__(self, arr: np.ndarray):
+        self.arr = arr
+
+    def __enter__(self):
+        check("halo_rx_host_register", lib.halo_rx_host_register(self.arr.ctypes.data, host_pages(self.arr.nbytes)))
+        return self.arr
+
+    def __exit__(self, *exc):
+        rc = lib.halo_rx_host_unregister(self.arr.ctypes.data)
+        if rc != HALO_OK:
+            _leaked.append(self.arr)
+            if exc[0] is None:
+                check("halo_rx_host_unregister", rc)
+        return False
+
+
+def registered_count() -> int:
+    """Live host registrations made through the library (halo_rx_host_registered_count)."""
+    return int(lib.halo_rx_host_registered_count())
+
+
+def registrations() -> list:
+    """(base, bytes) of every live registration, in address order."""
+    n = int(lib.halo_rx_host_registrations(None, None, 0))
+    bases = (ctypes.c_void_p * max(n, 1))()
+    sizes = (ctypes.c_uint64 * max(n, 1))()
+    n = int(lib.halo_rx_host_registrations(bases, sizes, n))
+    return [(int(bases[i] or 0), int(sizes[i])) for i in range(n)]
+
+
 RING_HEADER = 128  # sizeof(RingBuffer), mem/ring_buffer.go:18-26
 
 
@@ -157,6 +203,8 @@ _PROTOS = {
         _u8p, _u8p]),
     "halo_rx_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "halo_rx_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
+    "halo_rx_host_registered_count": (ctypes.c_uint32, []),
+    "halo_rx_host_registrations": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "halo_rx_dispatch": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_rx_dispatch_compact": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_tx_fixup_batch_device": (ctypes.c_int, [

@@ -66,4 +66,14 @@ enum SynthSlot : uint32_t {
 
 int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 
+// Live host registrations (hipHostRegister) made through this library — halo_rx_host_register
+// and halo_rx_ring_attach(HALO_RING_REGISTER). A registration pins whole pages, so every one
+// must start on a page boundary and cover whole pages, and no two may share a page; both rules
+// are checked here, before any HIP call. Removal waits for every device this library has
+// launched on, unregisters, and checks that the runtime no longer maps the range.
+enum HostRegKind : int { kRegUser = 1, kRegRing = 2 };
+uint64_t host_page_size();
+int host_reg_add(void* base, uint64_t bytes, HostRegKind kind);  // bytes: a page multiple
+int host_reg_remove(void* base, HostRegKind kind);
+
 }  // namespace halo

@@ -4,12 +4,20 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <unistd.h>
+
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <new>
 
 #include "halo_common.h"
 
 namespace halo {
+
+namespace {
+std::atomic<uint64_t> g_devices_used{0};  // bit d: this library has launched work on device d
+}
 
 int check_device() {
     static std::atomic<int> verdict[64];  // 0 = unknown, 1 = gfx950, <0 = HALO_E_*
@@ -17,14 +25,98 @@ int check_device() {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0) return HALO_E_NODEV;
     if (dev < 64) {
         const int v = verdict[dev].load(std::memory_order_relaxed);
-        if (v == 1) return HALO_OK;
+        if (v == 1) {
+            g_devices_used.fetch_or(1ull << dev, std::memory_order_relaxed);
+            return HALO_OK;
+        }
         if (v < 0) return v;
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return HALO_E_NODEV;
     const int v = strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : HALO_E_ARCH;
     if (dev < 64) verdict[dev].store(v, std::memory_order_relaxed);
+    if (v == 1 && dev < 64) g_devices_used.fetch_or(1ull << dev, std::memory_order_relaxed);
     return v == 1 ? HALO_OK : v;
+}
+
+// ---- the registry of live host registrations --------------------------------------------
+namespace {
+struct Reg {
+    uint64_t bytes;
+    HostRegKind kind;
+};
+std::mutex g_reg_mu;
+std::map<uintptr_t, Reg> g_regs;  // base -> range (page-aligned, whole pages)
+
+// Waits for all work this library queued on any device: a DMA or kernel still reading or
+// writing the range must finish before its pages are unpinned.
+int sync_used_devices() {
+    const uint64_t used = g_devices_used.load(std::memory_order_relaxed);
+    if (!used) return HALO_OK;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return HALO_E_HIP;
+    int rc = HALO_OK;
+    for (int d = 0; d < 64; ++d)
+        if ((used >> d) & 1)
+            if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = HALO_E_HIP;
+    (void)hipSetDevice(cur);
+    return rc;
+}
+
+// True while the runtime still maps host address p for the device.
+bool runtime_maps(void* p) {
+    void* d = nullptr;
+    const bool mapped = hipHostGetDevicePointer(&d, p, 0) == hipSuccess && d;
+    (void)hipGetLastError();  // a failed query must not surface at a later launch check
+    return mapped;
+}
+}  // namespace
+
+uint64_t host_page_size() {
+    static const uint64_t page = [] {
+        const long p = sysconf(_SC_PAGESIZE);
+        return p > 0 ? (uint64_t)p : 4096ull;
+    }();
+    return page;
+}
+
+int host_reg_add(void* base, uint64_t bytes, HostRegKind kind) {
+    const uint64_t page = host_page_size();
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+    if (!base || !bytes || (b % page) || (bytes % page) || b + bytes < b) return HALO_E_INVAL;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    // the first live registration starting at or after b, and the one before it
+    auto it = g_regs.lower_bound(b);
+    if (it != g_regs.end() && it->first < b + bytes) return HALO_E_INVAL;
+    if (it != g_regs.begin()) {
+        auto pv = std::prev(it);
+        if (pv->first + pv->second.bytes > b) return HALO_E_INVAL;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        return HALO_E_NODEV;
+    }
+    if (hipHostRegister(base, bytes, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return HALO_E_HIP;
+    }
+    g_regs.emplace(b, Reg{bytes, kind});
+    return HALO_OK;
+}
+
+int host_reg_remove(void* base, HostRegKind kind) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_regs.find(reinterpret_cast<uintptr_t>(base));
+    if (it == g_regs.end() || it->second.kind != kind) return HALO_E_INVAL;  // not a live base of this kind
+    if (sync_used_devices() != HALO_OK) return HALO_E_HIP;  // the entry stays: the pages stay pinned
+    if (hipHostUnregister(base) != hipSuccess) {
+        (void)hipGetLastError();
+        return HALO_E_HIP;
+    }
+    if (runtime_maps(base)) return HALO_E_HIP;  // still mapped: keep it counted, the caller keeps the memory
+    g_regs.erase(it);
+    return HALO_OK;
 }
 
 }  // namespace halo
@@ -298,12 +390,26 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
 }
 
 extern "C" HALO_API int halo_rx_host_register(const void* ptr, uint64_t bytes) {
-    if (!ptr || !bytes) return HALO_E_INVAL;
-    return hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) == hipSuccess ? HALO_OK
-                                                                                                : HALO_E_HIP;
+    return halo::host_reg_add(const_cast<void*>(ptr), bytes, halo::kRegUser);
 }
 
 extern "C" HALO_API int halo_rx_host_unregister(const void* ptr) {
-    if (!ptr) return HALO_E_INVAL;
-    return hipHostUnregister(const_cast<void*>(ptr)) == hipSuccess ? HALO_OK : HALO_E_HIP;
+    return halo::host_reg_remove(const_cast<void*>(ptr), halo::kRegUser);
+}
+
+extern "C" HALO_API uint32_t halo_rx_host_registered_count(void) {
+    std::lock_guard<std::mutex> lk(halo::g_reg_mu);
+    return (uint32_t)halo::g_regs.size();
+}
+
+extern "C" HALO_API uint32_t halo_rx_host_registrations(void** bases, uint64_t* bytes, uint32_t cap) {
+    std::lock_guard<std::mutex> lk(halo::g_reg_mu);
+    uint32_t i = 0;
+    for (const auto& kv : halo::g_regs) {
+        if (i >= cap) break;
+        if (bases) bases[i] = reinterpret_cast<void*>(kv.first);
+        if (bytes) bytes[i] = kv.second.bytes;
+        ++i;
+    }
+    return (uint32_t)halo::g_regs.size();
 }

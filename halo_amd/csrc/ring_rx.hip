@@ -570,8 +570,7 @@ bool free_ring(halo_rx_ring* r) {
     if (r->h_slen) (void)hipHostFree(r->h_slen);
     if (r->h_sres) (void)hipHostFree(r->h_sres);
     bool ok = true;
-    if (r->registered) ok = hipHostUnregister(r->mem) == hipSuccess;
-    if (!ok) (void)hipGetLastError();  // do not leave the error for a later launch check
+    if (r->registered) ok = halo::host_reg_remove(r->mem, halo::kRegRing) == HALO_OK;
     delete r;
     return ok;
 }
@@ -719,6 +718,10 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     int rc = halo::validate_ring(mem, offset, &size, &tail);
     if (rc) return rc;
     if (attach_flags & ~HALO_RING_REGISTER) return HALO_E_INVAL;
+    // a registered ring pins the whole pages it spans: it must start on a page of its own
+    const uint64_t page = halo::host_page_size();
+    const uint64_t reg_bytes = (halo::kRbHeader + size + page - 1) / page * page;
+    if ((attach_flags & HALO_RING_REGISTER) && (reinterpret_cast<uintptr_t>(mem) % page)) return HALO_E_INVAL;
     if (capacity == 0) capacity = halo::kEthMax;
     if (capacity > halo::kMaxCapacity) return HALO_E_INVAL;
     if (max_bytes == 0) max_bytes = std::min<uint64_t>(size, 256ull << 20);
@@ -752,8 +755,10 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     ok = ok && hipMalloc((void**)&r->d_info, sizeof(halo_rx_ring_scan_t)) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&r->h_info, sizeof(halo_rx_ring_scan_t), hipHostMallocDefault) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&r->h_off, 4ull * max_frames, hipHostMallocDefault) == hipSuccess;
+    int reg_rc = HALO_OK;
     if (ok && (attach_flags & HALO_RING_REGISTER)) {
-        ok = hipHostRegister(mem, halo::kRbHeader + size, hipHostRegisterDefault) == hipSuccess;
+        reg_rc = halo::host_reg_add(mem, reg_bytes, halo::kRegRing);  // INVAL: shares a page with a live one
+        ok = reg_rc == HALO_OK;
         r->registered = ok;
         if (ok && size <= halo::kMaxSpan + (64ull << 10)) {  // dword offsets into the data area fit u32
             r->d_data = static_cast<uint8_t*>(device_view(r->data, size));
@@ -762,7 +767,7 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     }
     if (!ok) {
         free_ring(r);
-        return HALO_E_NOMEM;
+        return reg_rc != HALO_OK ? reg_rc : HALO_E_NOMEM;
     }
     *out = r;
     return HALO_OK;

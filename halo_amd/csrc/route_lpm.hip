@@ -18,6 +18,7 @@
 // reported as HALO_ROUTE_PANIC.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -34,16 +35,21 @@ struct halo_route_table {
     std::vector<Node> nodes;  // nodes[0] = Root
     std::vector<halo_route_entry_t> routes;
     mutable std::mutex mu;  // RouteTable.Lock
-    // device copy (last halo_route_sync_device)
+    // Device copies, double-buffered: lookups read gen[active]; a sync compiles into the other
+    // generation (after the device has drained every lookup that could still read it) and then
+    // publishes it, so a lookup in flight never sees a table being rewritten or freed.
+    struct Gen {
+        uint32_t* d_tbl24 = nullptr;
+        uint32_t* d_tbl8 = nullptr;
+        size_t tbl8_cap = 0;
+        uint2* d_lists = nullptr;  // (start, count) per list
+        size_t lists_cap = 0;
+        uint32_t* d_ids = nullptr;
+        size_t ids_cap = 0;
+    } gen[2];
     int device = -1;
-    uint32_t* d_tbl24 = nullptr;
-    uint32_t* d_tbl8 = nullptr;
-    size_t tbl8_cap = 0;
-    uint2* d_lists = nullptr;  // (start, count) per list
-    size_t lists_cap = 0;
-    uint32_t* d_ids = nullptr;
-    size_t ids_cap = 0;
-    bool synced = false;
+    std::atomic<int> active{-1};  // published generation, -1 before the first sync
+    std::mutex sync_mu;           // one sync at a time
 };
 
 namespace halo {
@@ -187,10 +193,13 @@ extern "C" HALO_API int halo_route_table_destroy(halo_route_table_t* t) {
     if (!t) return HALO_E_INVAL;
     if (t->device >= 0) {
         halo::DeviceScope ds(t->device);
-        if (t->d_tbl24) (void)hipFree(t->d_tbl24);
-        if (t->d_tbl8) (void)hipFree(t->d_tbl8);
-        if (t->d_lists) (void)hipFree(t->d_lists);
-        if (t->d_ids) (void)hipFree(t->d_ids);
+        (void)hipDeviceSynchronize();  // no lookup may still read the tables
+        for (auto& g : t->gen) {
+            if (g.d_tbl24) (void)hipFree(g.d_tbl24);
+            if (g.d_tbl8) (void)hipFree(g.d_tbl8);
+            if (g.d_lists) (void)hipFree(g.d_lists);
+            if (g.d_ids) (void)hipFree(g.d_ids);
+        }
     }
     delete t;
     return HALO_OK;
@@ -256,39 +265,51 @@ extern "C" HALO_API int halo_route_sync_device(halo_route_table_t* t, int device
         halo::Compiler c{*t, tbl24, tbl8, lists, ids};
         c.walk(0, 0, 0, 0u);
     }
-    if (!t->d_tbl24 && hipMalloc(&t->d_tbl24, tbl24.size() * sizeof(uint32_t)) != hipSuccess) return HALO_E_NOMEM;
+    std::lock_guard<std::mutex> sg(t->sync_mu);
+    const int cur = t->active.load(std::memory_order_acquire);
+    // the generation written now was last published before `cur`: lookups launched while it was
+    // active may still be running on any stream of the device, so drain the device first
+    if (cur >= 0 && hipDeviceSynchronize() != hipSuccess) return HALO_E_HIP;
+    auto& g = t->gen[cur < 0 ? 0 : 1 - cur];
+    if (!g.d_tbl24 && hipMalloc(&g.d_tbl24, tbl24.size() * sizeof(uint32_t)) != hipSuccess) return HALO_E_NOMEM;
     t->device = device;
-    if ((rc = halo::grow(t->d_tbl8, t->tbl8_cap, tbl8.size() ? tbl8.size() : 1))) return rc;
-    if ((rc = halo::grow(t->d_lists, t->lists_cap, lists.size() ? lists.size() : 1))) return rc;
-    if ((rc = halo::grow(t->d_ids, t->ids_cap, ids.size() ? ids.size() : 1))) return rc;
-    if (hipMemcpy(t->d_tbl24, tbl24.data(), tbl24.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess ||
+    if ((rc = halo::grow(g.d_tbl8, g.tbl8_cap, tbl8.size() ? tbl8.size() : 1))) return rc;
+    if ((rc = halo::grow(g.d_lists, g.lists_cap, lists.size() ? lists.size() : 1))) return rc;
+    if ((rc = halo::grow(g.d_ids, g.ids_cap, ids.size() ? ids.size() : 1))) return rc;
+    if (hipMemcpy(g.d_tbl24, tbl24.data(), tbl24.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess ||
         (tbl8.size() &&
-         hipMemcpy(t->d_tbl8, tbl8.data(), tbl8.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) ||
+         hipMemcpy(g.d_tbl8, tbl8.data(), tbl8.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) ||
         (lists.size() &&
-         hipMemcpy(t->d_lists, lists.data(), lists.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) ||
-        (ids.size() && hipMemcpy(t->d_ids, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess))
+         hipMemcpy(g.d_lists, lists.data(), lists.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess) ||
+        (ids.size() && hipMemcpy(g.d_ids, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess))
         return HALO_E_HIP;
-    t->synced = true;
+    // hipMemcpy from pageable memory returns once the host buffer is consumed, not when the copy
+    // has landed: wait for it before publishing
+    if (hipDeviceSynchronize() != hipSuccess) return HALO_E_HIP;
+    t->active.store(cur < 0 ? 0 : 1 - cur, std::memory_order_release);
     return HALO_OK;
 }
 
 namespace halo {
 int route_view(const halo_route_table_t* t, LpmView* out) {
-    if (!t || !t->synced || !out) return HALO_E_INVAL;
-    *out = LpmView{t->d_tbl24, t->d_tbl8, t->d_lists, t->d_ids};
+    if (!t || !out) return HALO_E_INVAL;
+    const int a = t->active.load(std::memory_order_acquire);
+    if (a < 0) return HALO_E_INVAL;  // never synced
+    const auto& g = t->gen[a];
+    *out = LpmView{g.d_tbl24, g.d_tbl8, g.d_lists, g.d_ids};
     return HALO_OK;
 }
 }  // namespace halo
 
 extern "C" HALO_API int halo_route_lookup_device(const halo_route_table_t* t, const uint32_t* d_ips, uint32_t n,
                                                  uint32_t* d_route_ids, halo_stream_t stream) {
-    if (!t || !t->synced) return HALO_E_INVAL;
+    halo::LpmView v;
+    if (halo::route_view(t, &v)) return HALO_E_INVAL;
     if (n == 0) return HALO_OK;
     if (!d_ips || !d_route_ids) return HALO_E_INVAL;
     if ((reinterpret_cast<uintptr_t>(d_ips) | reinterpret_cast<uintptr_t>(d_route_ids)) & 15u) return HALO_E_INVAL;
     int rc = halo::check_device();
     if (rc) return rc;
-    const halo::LpmView v{t->d_tbl24, t->d_tbl8, t->d_lists, t->d_ids};
     hipLaunchKernelGGL(halo::lpm_kernel, dim3(halo::lpm_blocks((n + 3) / 4)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), v, d_ips, n, d_route_ids);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
@@ -297,12 +318,12 @@ extern "C" HALO_API int halo_route_lookup_device(const halo_route_table_t* t, co
 extern "C" HALO_API int halo_route_lookup_records_device(const halo_route_table_t* t,
                                                          const halo_rx_result_t* d_records, uint32_t n,
                                                          uint32_t* d_route_ids, halo_stream_t stream) {
-    if (!t || !t->synced) return HALO_E_INVAL;
+    halo::LpmView v;
+    if (halo::route_view(t, &v)) return HALO_E_INVAL;
     if (n == 0) return HALO_OK;
     if (!d_records || !d_route_ids) return HALO_E_INVAL;
     int rc = halo::check_device();
     if (rc) return rc;
-    const halo::LpmView v{t->d_tbl24, t->d_tbl8, t->d_lists, t->d_ids};
     hipLaunchKernelGGL(halo::lpm_records_kernel, dim3(halo::lpm_blocks(n)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), v, d_records, n, d_route_ids);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;

@@ -82,9 +82,6 @@ class RingBuffer:
         return self.data[idx].tobytes()
 
 
-_leaked: list = []  # arrays whose host registration could not be removed (see RingConsumer.close)
-
-
 class RingConsumer:
     """The GPU consumer of one ring (halo_rx_ring_attach). ``capacity`` is ReadPacket's
     ``len(data)`` (1514 in the DPDK driver and Wire). ``small_poll``: spans up to this many bytes
@@ -105,8 +102,8 @@ class RingConsumer:
         self.max_frames = min(max_frames or (1 << 32) - 1, min(cap, ring.size) // 8)
         self._out = _lib.host_array(self.max_frames, RESULT_DTYPE)  # registered below: pages of its own
         # the records come back by DMA straight into this array: pin it too
-        self._out_registered = register and _lib.lib.halo_rx_host_register(self._out.ctypes.data,
-                                                                           self._out.nbytes) == 0
+        self._out_registered = register and _lib.lib.halo_rx_host_register(
+            self._out.ctypes.data, _lib.host_pages(self._out.nbytes)) == 0
 
     def close(self):
         """Detach from the ring and unregister the record array. Raises HaloError if either
@@ -120,7 +117,7 @@ class RingConsumer:
                 rc2 = _lib.lib.halo_rx_host_unregister(self._out.ctypes.data)
                 self._out_registered = False
             if rc != _lib.HALO_OK or rc2 != _lib.HALO_OK:
-                _leaked.append((self.ring, self._out))  # still registered: never free them
+                _lib._leaked.append((self.ring, self._out))  # still registered: never free them
                 _lib.check("halo_rx_ring_detach" if rc != _lib.HALO_OK else "halo_rx_host_unregister",
                            rc if rc != _lib.HALO_OK else rc2)
 

@@ -206,11 +206,20 @@ HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* by
  * segment, a packed batch) are sent with one DMA per chunk straight from `bytes`; registering
  * that memory (e.g. the ring's hugepages) makes the DMA run at full PCIe rate. Other batches
  * are repacked into pinned staging by the CPU.
- * Registration pins whole pages: register memory whose pages no other allocation shares
- * (page-aligned, as hugepages and mmap regions are; halo_amd._lib.host_array in Python), and
- * unregister it before it is freed.                                                       */
+ * Registration pins whole pages, so the library enforces: `ptr` page-aligned and `bytes` a
+ * multiple of the page size (hugepages, mmap regions; halo_amd._lib.host_array in Python), and
+ * no page shared with a live registration (this call's or a ring's) — otherwise HALO_E_INVAL,
+ * before any HIP call. Unregister before the memory is freed: `ptr` must be the base of a live
+ * registration made here (else HALO_E_INVAL); the call first waits for all work this library
+ * queued on every device it used, then unregisters and checks that the runtime no longer maps
+ * the range (HALO_E_HIP if it still does: keep the memory allocated then).                 */
 HALO_API int halo_rx_host_register(const void* ptr, uint64_t bytes);
 HALO_API int halo_rx_host_unregister(const void* ptr);
+/* Live registrations (halo_rx_host_register + rings attached with HALO_RING_REGISTER). The
+ * second form also copies up to `cap` (base, bytes) pairs, in address order; either array may
+ * be NULL. Both return the total count. */
+HALO_API uint32_t halo_rx_host_registered_count(void);
+HALO_API uint32_t halo_rx_host_registrations(void** bases, uint64_t* bytes, uint32_t cap);
 
 /* Multi-GPU host batch: frames [0, n) are split into n_ctx contiguous index
  * ranges balanced by bytes; ctxs[k] (one host context per device, or several on one device)
@@ -243,8 +252,11 @@ HALO_API int halo_rx_shard_multi(halo_rx_host_ctx_t* const* ctxs, uint32_t n_ctx
                                         ReadPacket leaves it, and the tail, in place              */
 #define HALO_RING_STOP_MAX 4u        /* max_frames taken, more records available                  */
 #define HALO_RING_STOP_BAD_CURSOR 5u /* head - tail > size: ReadPacket returns false              */
-#define HALO_RING_REGISTER 0x1u      /* attach: hipHostRegister the ring for full-rate DMA (its pages
-                                        must not be shared: see halo_rx_host_register)              */
+#define HALO_RING_REGISTER 0x1u      /* attach: hipHostRegister the ring for full-rate DMA. The ring
+                                        must start on a page boundary; the whole pages through the end
+                                        of its data area are registered and must not be shared with
+                                        another live registration (HALO_E_INVAL; see
+                                        halo_rx_host_register)                                      */
 
 typedef struct halo_rx_ring_scan {
     uint32_t n_frames;  /* frames taken                                                      */
@@ -411,7 +423,11 @@ HALO_API int halo_route_table_destroy(halo_route_table_t* t);
 HALO_API int halo_route_update(halo_route_table_t* t, const halo_route_entry_t* old_route,
                                const halo_route_entry_t* new_route, uint32_t* new_id);
 HALO_API int halo_route_get(const halo_route_table_t* t, uint32_t id, halo_route_entry_t* out);
-/* Compile the trie into the device table on `device` (allocates / grows HBM; synchronous). */
+/* Compile the trie into the device table on `device` (allocates / grows HBM; synchronous).
+ * Double-buffered: the new table is written into the generation not in use, after the device
+ * has drained every lookup that could still read that one (a device synchronisation), and is
+ * then published. A lookup sees the table last published when it was launched — never one
+ * being rewritten, as FindRoute under RouteTable.RLock never does (engine/ipv4_engine.go:351). */
 HALO_API int halo_route_sync_device(halo_route_table_t* t, int device);
 /* FindRoute for each address (IpAddrToU form) / each record's dst_ip: route id, HALO_ROUTE_NONE
  * or HALO_ROUTE_PANIC. Asynchronous on `stream`; uses the last synced table. */

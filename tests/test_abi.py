@@ -204,3 +204,35 @@ def test_tx_op_struct_layout_and_validation(tmp_path):
         rc = L.halo_tx_fixup_batch_device(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, 1,
                                           ops.ctypes.data, 1, 0, None, None)
         assert rc == _lib.HALO_E_NODEV
+
+
+def test_host_registration_rules_before_any_hip_call():
+    """halo_rx_host_register / ring attach with HALO_RING_REGISTER refuse, before any HIP call, a
+    base that is not page-aligned, a size that is not whole pages, and unregistering anything that
+    is not the base of a live registration (registrations pin whole pages)."""
+    import mmap
+
+    import torch
+
+    from halo_amd import _lib
+
+    L, P = _lib.lib, mmap.PAGESIZE
+    a = _lib.host_array(4 * P)
+    base = a.ctypes.data
+    assert base % P == 0
+    assert L.halo_rx_host_register(None, P) == _lib.HALO_E_INVAL
+    assert L.halo_rx_host_register(base, 0) == _lib.HALO_E_INVAL
+    assert L.halo_rx_host_register(base + 64, P) == _lib.HALO_E_INVAL      # base inside a page
+    assert L.halo_rx_host_register(base, P + 100) == _lib.HALO_E_INVAL     # a partial last page
+    assert L.halo_rx_host_unregister(None) == _lib.HALO_E_INVAL
+    assert L.halo_rx_host_unregister(base) == _lib.HALO_E_INVAL           # never registered
+    assert _lib.registered_count() == 0 and _lib.registrations() == []
+    # a ring that does not start on a page boundary cannot be attached with RING_REGISTER
+    mem = a[64:64 + 128 + 4096]
+    assert L.halo_ring_create(mem.ctypes.data, mem.nbytes) == 0
+    h = ctypes.c_void_p()
+    rc = L.halo_rx_ring_attach(0, mem.ctypes.data, 0, 1514, 0, 0, _lib.RING_REGISTER, ctypes.byref(h))
+    assert rc == _lib.HALO_E_INVAL and not h.value
+    if not torch.cuda.is_available():
+        assert L.halo_rx_host_register(base, 2 * P) == _lib.HALO_E_NODEV   # valid range, no device
+        assert _lib.registered_count() == 0

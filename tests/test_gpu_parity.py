@@ -390,16 +390,18 @@ def test_host_path_direct_dma_registered(dev, oracle_lib):
     data = reg
     want, whist = oracle_lib.rx_batch(data, lay["lens"], oracle_lib.NetIf.make(), 1, offsets_dw=lay["offsets_dw"])
     hb = HostBatcher(0, chunk_frames=3000, chunk_bytes=1 << 20)
-    for registered in (False, True):
-        if registered:
-            _lib.check("register", _lib.lib.halo_rx_host_register(data.ctypes.data, data.nbytes))
-        hist = np.zeros(14, np.uint32)
-        got = hb.parse(data, offs, lay["lens"], NetIf.make(), 1, hist)
-        if registered:
-            _lib.check("unregister", _lib.lib.halo_rx_host_unregister(data.ctypes.data))
-        assert_records_equal(got, want, None, f"host direct registered={registered}")
-        assert np.array_equal(hist, whist)
-    hb.close()
+    import contextlib
+
+    try:
+        for registered in (False, True):
+            hist = np.zeros(14, np.uint32)
+            with _lib.registered(data) if registered else contextlib.nullcontext():
+                got = hb.parse(data, offs, lay["lens"], NetIf.make(), 1, hist)
+            assert_records_equal(got, want, None, f"host direct registered={registered}")
+            assert np.array_equal(hist, whist)
+    finally:
+        hb.close()
+    assert _lib.registered_count() == 0, _lib.registrations()
 
 
 def test_netif_packet_handle_batch(dev, golden, oracle_lib):

@@ -27,7 +27,23 @@ def dev():
     from halo_amd import _lib
 
     _lib.check("halo_rx_init", _lib.lib.halo_rx_init(0))
-    return torch.device("cuda:0")
+    yield torch.device("cuda:0")
+    # every ring and record array these tests registered was unregistered again
+    assert _lib.registered_count() == 0, _lib.registrations()
+
+
+@pytest.fixture(autouse=True)
+def _no_registration_outlives_a_test():
+    """Each test ends with no live host registration: a registration outliving its test (a
+    consumer left attached, an array left registered) is what could leave a stale mapping behind
+    for a later pageable copy."""
+    import gc
+
+    from halo_amd import _lib
+
+    yield
+    gc.collect()  # consumers dropped without close() detach in __del__
+    assert _lib.registered_count() == 0, _lib.registrations()
 
 
 def _seek(ring, pos: int):
@@ -277,7 +293,7 @@ def test_small_poll_unpinned_out_and_unregistered_ring(dev, golden, oracle_lib):
         assert ring.tail == tail
         if register:  # the same array registered for one poll, unregistered for the next
             ring.write_batch(data, offs[sel].astype(np.uint64) * 4, lens[sel])
-            _lib.check("register", _lib.lib.halo_rx_host_register(out.ctypes.data, out.nbytes))
+            _lib.check("register", _lib.lib.halo_rx_host_register(out.ctypes.data, _lib.host_pages(out.nbytes)))
             for k in range(2):
                 if k:
                     _lib.check("unregister", _lib.lib.halo_rx_host_unregister(out.ctypes.data))
@@ -375,3 +391,47 @@ def test_shard_multi_two_contexts_one_device(dev, oracle_lib):
     assert abs(half - total / 2) <= 1514
     a.close()
     b.close()
+
+
+def test_registration_registry_refuses_shared_pages(dev):
+    """Live registrations never share a page: a second registration or a registered ring attach
+    touching a registered page is refused (HALO_E_INVAL), only the base of a live registration can
+    be unregistered, and after unregistering the runtime no longer maps the range."""
+    import ctypes
+    import mmap
+
+    from halo_amd import _lib
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    L, P = _lib.lib, mmap.PAGESIZE
+    a = _lib.host_array(8 * P)
+    base = a.ctypes.data
+    _lib.check("register", L.halo_rx_host_register(base, 4 * P))
+    try:
+        assert _lib.registrations() == [(base, 4 * P)]
+        assert L.halo_rx_host_register(base, 4 * P) == _lib.HALO_E_INVAL          # the same range
+        assert L.halo_rx_host_register(base + P, P) == _lib.HALO_E_INVAL          # inside it
+        assert L.halo_rx_host_register(base + 3 * P, 2 * P) == _lib.HALO_E_INVAL  # overlapping its end
+        # a ring laid out on the registered pages cannot be attached registered
+        mem = a[:128 + 4096]
+        _lib.check("ring_create", L.halo_ring_create(mem.ctypes.data, mem.nbytes))
+        h = ctypes.c_void_p()
+        assert L.halo_rx_ring_attach(0, mem.ctypes.data, 0, 1514, 0, 0, _lib.RING_REGISTER,
+                                     ctypes.byref(h)) == _lib.HALO_E_INVAL
+        # the next page is free: a registration starting there is fine
+        _lib.check("register next", L.halo_rx_host_register(base + 4 * P, P))
+        assert _lib.registered_count() == 2
+        assert L.halo_rx_host_unregister(base + P) == _lib.HALO_E_INVAL           # not a base
+        _lib.check("unregister next", L.halo_rx_host_unregister(base + 4 * P))
+        assert L.halo_rx_host_unregister(base + 4 * P) == _lib.HALO_E_INVAL       # already gone
+    finally:
+        _lib.check("unregister", L.halo_rx_host_unregister(base))
+    assert _lib.registered_count() == 0
+    # a ring consumer's ring and record array are two registrations, removed by close()
+    ring = RingBuffer(1 << 16)
+    cons = RingConsumer(ring, capacity=1514)
+    regs = dict(_lib.registrations())
+    assert regs.get(ring.mem.ctypes.data) == _lib.host_pages(ring.mem.nbytes), regs
+    assert regs.get(cons._out.ctypes.data) == _lib.host_pages(cons._out.nbytes), regs
+    cons.close()
+    assert _lib.registered_count() == 0
