@@ -27,6 +27,15 @@ HALO_E_RANGE = -6
 HALO_RX_CSUM_ENABLE = 0x1
 HALO_RX_JUMBO_EXT = 0x2
 HALO_RX_RECORD_COMPACT = 0x4
+HALO_RX_UNIFORM_LEN = 0x8
+HALO_RX_VARIANT_SHIFT = 8
+# lanes per frame -> HALO_RX_VARIANT_* (0 = automatic, -1 = the size-class mix kernel)
+_VARIANT_CODE = {0: 0, 1: 1, 4: 2, 8: 3, 16: 4, -1: 5}
+
+
+def variant_flags(lanes_per_frame: int) -> int:
+    """The flags bits that force a kernel variant for one call (HALO_RX_VARIANT_*)."""
+    return _VARIANT_CODE[lanes_per_frame] << HALO_RX_VARIANT_SHIFT
 
 STATUS_NAMES = (
     "OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_PROTO", "IP_HDR_CKSUM",
@@ -194,7 +203,6 @@ _PROTOS = {
     "halo_rx_parse_strided_device": (ctypes.c_int, [
         _u8p, ctypes.c_uint64, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.POINTER(NetIf), _u8p, _u8p, ctypes.c_void_p]),
-    "halo_rx_tune_variant": (ctypes.c_int, [ctypes.c_int]),
     "halo_rx_host_ctx_create": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "halo_rx_host_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),

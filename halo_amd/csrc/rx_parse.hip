@@ -578,7 +578,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
 #define HALO_RX_LANE_MAX_BLOCKS HALO_RX_MAX_BLOCKS
 #endif
 constexpr int kVariantMix = -1;
-std::atomic<int> g_force_variant{0};  // tuning hook (halo_rx_tune_variant); 0 = automatic
 
 uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS) {
     const uint64_t waves = (n + frames_per_wave - 1) / frames_per_wave;
@@ -600,12 +599,20 @@ hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Kernel variant (from the sweeps in profiles/r01/tune_*.log): a known uniform
-// length picks the best lanes-per-frame; a ragged batch whose frames are all <= 64 B goes lane
-// per frame, and any other ragged batch goes to the size-class mix kernel.
-int pick_variant(uint32_t max_len, bool uniform) {
-    const int forced = g_force_variant.load(std::memory_order_relaxed);
-    if (forced) return forced;
+// Kernel variant (from the sweeps in profiles/r01/tune_*.log): a variant named in
+// the call's flags wins; a known uniform length (strided with one length, or a ragged batch flagged
+// HALO_RX_UNIFORM_LEN) picks the best lanes-per-frame; a ragged batch whose frames are all <= 64 B
+// goes lane per frame, and any other ragged batch goes to the size-class mix kernel.
+int pick_variant(uint32_t max_len, bool uniform, uint32_t flags) {
+    switch ((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) {
+        case HALO_RX_VARIANT_LANE: return 1;
+        case HALO_RX_VARIANT_G4: return 4;
+        case HALO_RX_VARIANT_G8: return 8;
+        case HALO_RX_VARIANT_G16: return 16;
+        case HALO_RX_VARIANT_MIX: return kVariantMix;
+        default: break;
+    }
+    if (flags & HALO_RX_UNIFORM_LEN) uniform = max_len != 0;
     if (max_len != 0 && max_len <= 64) return 1;
     if (!uniform) return kVariantMix;
     if (max_len <= 128) return 1;
@@ -615,7 +622,7 @@ int pick_variant(uint32_t max_len, bool uniform) {
 }
 
 int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, hipStream_t s) {
-    const int v = pick_variant(max_len, uniform);
+    const int v = pick_variant(max_len, uniform, p.flags);
     hipError_t e;
     switch (layout) {
         case 0:  // ragged: the only layout with the fused passes
@@ -631,7 +638,10 @@ int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, 
 int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
                 halo_rx_result_t* d_out, uint32_t* d_hist) {
     if (!netif || !d_out) return HALO_E_INVAL;
-    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_RECORD_COMPACT)) return HALO_E_INVAL;
+    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_RECORD_COMPACT | HALO_RX_UNIFORM_LEN |
+                  HALO_RX_VARIANT_MASK))
+        return HALO_E_INVAL;
+    if (((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) > HALO_RX_VARIANT_MIX) return HALO_E_INVAL;
     if (reinterpret_cast<uintptr_t>(d_out) & 15u) return HALO_E_INVAL;
     p.n = n;
     p.flags = flags;
@@ -734,11 +744,4 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
     // with per-frame lengths only the stride bounds them (mixed sizes possible)
     const uint32_t max_len = d_lens ? (uint32_t)(stride < 65535 ? stride : 65535) : len;
     return halo::launch_parse(p, d_lens ? 1 : 2, max_len, d_lens == nullptr, static_cast<hipStream_t>(stream));
-}
-
-extern "C" HALO_API int halo_rx_tune_variant(int variant) {
-    if (variant != 0 && variant != 1 && variant != 4 && variant != 8 && variant != 16 && variant != -1)
-        return HALO_E_INVAL;
-    halo::g_force_variant.store(variant, std::memory_order_relaxed);
-    return HALO_OK;
 }

@@ -63,9 +63,11 @@ ERROR_TEXT = {
 }
 
 
-def flags_word(check_sum_enable: bool = True, jumbo: bool = False) -> int:
-    """The ABI ``flags`` word that replaces the ``CheckSumEnable`` package global."""
-    return (HALO_RX_CSUM_ENABLE if check_sum_enable else 0) | (HALO_RX_JUMBO_EXT if jumbo else 0)
+def flags_word(check_sum_enable: bool = True, jumbo: bool = False, variant: int = 0, uniform_len: bool = False) -> int:
+    """The ABI ``flags`` word that replaces the ``CheckSumEnable`` package global (plus the
+    per-call kernel variant, lanes per frame with -1 = mix, and the uniform-length hint)."""
+    return ((HALO_RX_CSUM_ENABLE if check_sum_enable else 0) | (HALO_RX_JUMBO_EXT if jumbo else 0)
+            | _lib.variant_flags(variant) | (_lib.HALO_RX_UNIFORM_LEN if uniform_len else 0))
 
 
 def _stream_handle(stream):
@@ -82,12 +84,15 @@ def _check_out(out, n: int):
 
 
 def parse_frames_batch(frames, offsets_dw, lens, *, netif: NetIf, check_sum_enable: bool = True,
-                       jumbo: bool = False, max_len_hint: int = 0, out=None, hist=None, stream=None):
+                       jumbo: bool = False, max_len_hint: int = 0, uniform_len: bool = False, variant: int = 0,
+                       out=None, hist=None, stream=None):
     """Parse + verify a ragged, device-resident batch (ParseEthFrm..ParseIcmpPkt per frame).
 
     frames: cuda uint8 tensor; offsets_dw: cuda int32 tensor (frame i at 4*offsets_dw[i]);
     lens: cuda int16 tensor (u16 lengths). Returns the cuda uint8 [n, 32] result tensor.
     ``hist`` (cuda int32[14]) is incremented per status. Asynchronous on ``stream``.
+    ``uniform_len``: every frame is ``max_len_hint`` bytes; ``variant``: force lanes per frame
+    (1/4/8/16, -1 = mix) for this call — speed only, records are identical.
     """
     import torch
 
@@ -97,7 +102,7 @@ def parse_frames_batch(frames, offsets_dw, lens, *, netif: NetIf, check_sum_enab
     _check_out(out, n)
     rc = _lib.lib.halo_rx_parse_batch_device(
         _lib.ptr(frames), _lib.ptr(offsets_dw), _lib.ptr(lens), n,
-        flags_word(check_sum_enable, jumbo), netif, max_len_hint, _lib.ptr(out), _lib.ptr(hist),
+        flags_word(check_sum_enable, jumbo, variant, uniform_len), netif, max_len_hint, _lib.ptr(out), _lib.ptr(hist),
         _stream_handle(stream))
     _lib.check("halo_rx_parse_batch_device", rc)
     return out

@@ -69,6 +69,21 @@ extern "C" {
                                  /* to 9014/9000/8980 (MTU 9000); arithmetic unchanged      */
 #define HALO_RX_RECORD_COMPACT 0x4u /* write halo_rx_record16_t (16 B) instead of            */
                                     /* halo_rx_result_t (32 B); device entry points only     */
+#define HALO_RX_UNIFORM_LEN 0x8u    /* ragged batch whose frames all have length max_len_hint */
+                                    /* (a speed hint: picks the uniform-length kernel table)  */
+/* Per-call kernel variant (tuning and tests; results are identical for every value, only speed
+ * changes): flags |= HALO_RX_VARIANT_x << HALO_RX_VARIANT_SHIFT. AUTO picks from max_len_hint /
+ * the uniform length; LANE = one lane per frame; G4/G8/G16 = that many lanes per frame; MIX =
+ * the size-class kernel (each wave sorts 256 frames by size and runs lane-per-frame, 4-, 8- and
+ * 16-lane passes). Device parse entry points only.                                          */
+#define HALO_RX_VARIANT_SHIFT 8
+#define HALO_RX_VARIANT_MASK 0x700u
+#define HALO_RX_VARIANT_AUTO 0u
+#define HALO_RX_VARIANT_LANE 1u
+#define HALO_RX_VARIANT_G4 2u
+#define HALO_RX_VARIANT_G8 3u
+#define HALO_RX_VARIANT_G16 4u
+#define HALO_RX_VARIANT_MIX 5u
 
 /* ---- per-frame status: the FIRST failing check in reference order, 0 = OK ---------- */
 typedef enum halo_rx_status {
@@ -170,7 +185,8 @@ HALO_API const char* halo_rx_status_name(int status);
  * All pointers are device pointers. `d_out` receives n records (halo_rx_result_t, or
  * halo_rx_record16_t with HALO_RX_RECORD_COMPACT; 16-byte aligned). `d_status_hist`, if not
  * NULL, receives HALO_RX_STATUS_COUNT u32 counters that are INCREMENTED (the caller
- * zeroes them). `max_len_hint` (0 = unknown) selects the lanes-per-frame variant.
+ * zeroes them). `max_len_hint` (a bound on every frame's length; 0 = unknown) selects the
+ * lanes-per-frame variant; with HALO_RX_UNIFORM_LEN every frame has exactly that length.
  * Asynchronous on `stream`.                                                              */
 HALO_API int halo_rx_parse_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
                                         const uint16_t* d_lens, uint32_t n, uint32_t flags,
@@ -183,12 +199,6 @@ HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uint64_t strid
                                           uint32_t flags, const halo_rx_netif_t* netif,
                                           halo_rx_result_t* d_out, uint32_t* d_status_hist,
                                           halo_stream_t stream);
-
-/* Tuning hook: force the kernel variant process-wide. 1, 4, 8, 16 = that many lanes per frame
- * for every frame; -1 = size-class mix kernel (each wave sorts 256 frames by size and runs
- * lane-per-frame, 4-, 8- and 16-lane passes); 0 = automatic (from max_len_hint / the uniform
- * length). Results are identical for every value; only speed changes. */
-HALO_API int halo_rx_tune_variant(int variant);
 
 /* ---- host-memory batch parse -----------------------------------
  * Frames in HOST memory (any alignment, ragged byte offsets). Stages them into pinned

@@ -136,30 +136,27 @@ def test_fused_parse_flow_hash(dev, oracle_lib, golden, variant):
                for d, o, ln, hint in ((data, offs, lens, 0), (fdata, foffs, flens, 0))]
     batches.append((fr["bytes"], fr["offsets_dw"], fr["lens"], 1500))
     stream = torch.cuda.current_stream().cuda_stream
-    _lib.check("variant", _lib.lib.halo_rx_tune_variant(variant))
-    try:
-        for d, o, ln, hint in batches:
-            n = int(ln.numel())
-            for compact in (False, True):
-                flags = 1 | (_lib.HALO_RX_RECORD_COMPACT if compact else 0)
-                width = 16 if compact else 32
-                ref = torch.empty((n, width), dtype=torch.uint8, device=dev)
-                _lib.check("parse", _lib.lib.halo_rx_parse_batch_device(
-                    d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, ref.data_ptr(), None,
-                    stream))
-                full = protocol.parse_frames_batch(d, o, ln, netif=NetIf.make(), max_len_hint=hint)
-                for kind, nat, buckets in ((1, 0, 1 << 20), (0, 1, 0), (0, 0, 1000003)):
-                    got = torch.full((n, width), 0xEE, dtype=torch.uint8, device=dev)
-                    h = torch.zeros(n, dtype=torch.int64, device=dev)
-                    b = torch.zeros(n, dtype=torch.int32, device=dev)
-                    _lib.check("fused", _lib.lib.halo_rx_parse_flow_batch_device(
-                        d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, got.data_ptr(),
-                        None, kind, nat, h.data_ptr(), buckets, b.data_ptr() if buckets else None, stream))
-                    torch.cuda.synchronize()
-                    assert torch.equal(got, ref), (variant, compact, kind)
-                    wh, wb = oracle_lib.flow_hash_batch(protocol.records(full), kind, nat, buckets)
-                    assert np.array_equal(h.cpu().numpy().view(np.uint64), wh), (variant, compact, kind, nat)
-                    if buckets:
-                        assert np.array_equal(b.cpu().numpy().view(np.uint32), wb)
-    finally:
-        _lib.lib.halo_rx_tune_variant(0)
+    vf = _lib.variant_flags(variant)
+    for d, o, ln, hint in batches:
+        n = int(ln.numel())
+        for compact in (False, True):
+            flags = 1 | vf | (_lib.HALO_RX_RECORD_COMPACT if compact else 0)
+            width = 16 if compact else 32
+            ref = torch.empty((n, width), dtype=torch.uint8, device=dev)
+            _lib.check("parse", _lib.lib.halo_rx_parse_batch_device(
+                d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, ref.data_ptr(), None,
+                stream))
+            full = protocol.parse_frames_batch(d, o, ln, netif=NetIf.make(), max_len_hint=hint)
+            for kind, nat, buckets in ((1, 0, 1 << 20), (0, 1, 0), (0, 0, 1000003)):
+                got = torch.full((n, width), 0xEE, dtype=torch.uint8, device=dev)
+                h = torch.zeros(n, dtype=torch.int64, device=dev)
+                b = torch.zeros(n, dtype=torch.int32, device=dev)
+                _lib.check("fused", _lib.lib.halo_rx_parse_flow_batch_device(
+                    d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, got.data_ptr(),
+                    None, kind, nat, h.data_ptr(), buckets, b.data_ptr() if buckets else None, stream))
+                torch.cuda.synchronize()
+                assert torch.equal(got, ref), (variant, compact, kind)
+                wh, wb = oracle_lib.flow_hash_batch(protocol.records(full), kind, nat, buckets)
+                assert np.array_equal(h.cpu().numpy().view(np.uint64), wh), (variant, compact, kind, nat)
+                if buckets:
+                    assert np.array_equal(b.cpu().numpy().view(np.uint32), wb)

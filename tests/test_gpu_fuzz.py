@@ -80,17 +80,14 @@ def test_fuzz_every_variant_full_and_compact(dev, corpus, variant):
     from halo_amd._lib import RECORD16_DTYPE, RESULT_DTYPE, compact_of
 
     _, (d, o, ln), want = corpus
-    _lib.check("halo_rx_tune_variant", _lib.lib.halo_rx_tune_variant(variant))
-    try:
-        for flags in (1, 3):
-            wrec = want[flags][0][:N_VARIANT]
-            got, hist = _parse(dev, d, o, ln, N_VARIANT, flags)
-            assert_records_equal(got.reshape(-1).view(RESULT_DTYPE), wrec, None, f"fuzz G={variant} flags={flags}")
-            assert np.array_equal(hist, np.bincount(wrec["status"], minlength=14))
-            got16, _ = _parse(dev, d, o, ln, N_VARIANT, flags, compact=True)
-            w16 = compact_of(wrec)
-            bad = np.nonzero(np.any(got16.reshape(-1, 16) != w16.view(np.uint8).reshape(-1, 16), axis=1))[0]
-            assert bad.size == 0, (variant, flags, bad[:5])
-            assert got16.reshape(-1).view(RECORD16_DTYPE).shape[0] == N_VARIANT
-    finally:
-        _lib.lib.halo_rx_tune_variant(0)
+    vf = _lib.variant_flags(variant)
+    for flags in (1, 3):
+        wrec = want[flags][0][:N_VARIANT]
+        got, hist = _parse(dev, d, o, ln, N_VARIANT, flags | vf)
+        assert_records_equal(got.reshape(-1).view(RESULT_DTYPE), wrec, None, f"fuzz G={variant} flags={flags}")
+        assert np.array_equal(hist, np.bincount(wrec["status"], minlength=14))
+        got16, _ = _parse(dev, d, o, ln, N_VARIANT, flags | vf, compact=True)
+        w16 = compact_of(wrec)
+        bad = np.nonzero(np.any(got16.reshape(-1, 16) != w16.view(np.uint8).reshape(-1, 16), axis=1))[0]
+        assert bad.size == 0, (variant, flags, bad[:5])
+        assert got16.reshape(-1).view(RECORD16_DTYPE).shape[0] == N_VARIANT

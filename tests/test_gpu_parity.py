@@ -36,7 +36,7 @@ def _to_dev(a, dev, dtype=None):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
 
-def _parse_ragged(dev, data, offs_dw, lens, flags, hint=0, netif=None):
+def _parse_ragged(dev, data, offs_dw, lens, flags, hint=0, netif=None, variant=0):
     import torch
 
     from halo_amd import protocol
@@ -48,19 +48,15 @@ def _parse_ragged(dev, data, offs_dw, lens, flags, hint=0, netif=None):
     ln = _to_dev(lens.astype(np.uint16), dev, np.int16)
     hist = torch.zeros(14, dtype=torch.int32, device=dev)
     out = protocol.parse_frames_batch(d, o, ln, netif=netif, check_sum_enable=bool(flags & 1),
-                                      jumbo=bool(flags & 2), max_len_hint=hint, hist=hist)
+                                      jumbo=bool(flags & 2), max_len_hint=hint, hist=hist, variant=variant)
     torch.cuda.synchronize()
     return protocol.records(out), hist.cpu().numpy().astype(np.int64)
 
 
 @pytest.fixture
 def lanes_per_frame(request):
-    """Force the kernel variant (G lanes per frame) for one test, restore automatic after."""
-    from halo_amd import _lib
-
-    _lib.check("halo_rx_tune_variant", _lib.lib.halo_rx_tune_variant(request.param))
-    yield request.param
-    _lib.lib.halo_rx_tune_variant(0)
+    """The kernel variant (G lanes per frame, -1 = mix, 0 = automatic) a test forces per call."""
+    return request.param
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2, 3])
@@ -70,7 +66,7 @@ def test_golden_ragged_all_group_widths(dev, golden, flags, lanes_per_frame):
 
     meta, blob = golden
     data, offs, lens, names = golden_arrays(meta, blob)
-    got, hist = _parse_ragged(dev, data, offs, lens, flags, 0)
+    got, hist = _parse_ragged(dev, data, offs, lens, flags, 0, variant=lanes_per_frame)
     want = expected_records(meta, flags, RESULT_DTYPE)
     assert_records_equal(got, want, names, f"GPU ragged flags={flags} G={lanes_per_frame}")
     assert np.array_equal(hist, np.bincount(want["status"], minlength=14))
@@ -97,7 +93,8 @@ def test_random_imix_every_group_width(dev, oracle_lib, lanes_per_frame):
     n = 30_000
     lay = synth.layout(n, size_mode=1, proto_mode=3, mutate_shift=2, first_index=77_000_000)
     fr = synth.frames_device(lay, NetIf.make(), device=dev, fill=0x3C)
-    out = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make())
+    out = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                      variant=lanes_per_frame)
     torch.cuda.synchronize()
     want, _ = oracle_lib.rx_batch(fr["bytes"].cpu().numpy(), lay["lens"], oracle_lib.NetIf.make(), 1,
                                   offsets_dw=lay["offsets_dw"], threads=8)
@@ -120,7 +117,8 @@ def test_golden_compact_records(dev, golden, lanes_per_frame):
     for flags in (1, 3):
         out = torch.full((len(lens), 16), 0xEE, dtype=torch.uint8, device=dev)
         rc = _lib.lib.halo_rx_parse_batch_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens),
-                                                 flags | _lib.HALO_RX_RECORD_COMPACT, NetIf.make(), 0,
+                                                 flags | _lib.HALO_RX_RECORD_COMPACT | _lib.variant_flags(lanes_per_frame),
+                                                 NetIf.make(), 0,
                                                  out.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
         assert rc == 0
         torch.cuda.synchronize()
@@ -299,6 +297,103 @@ def test_config3_full_size_16M_imix(dev, oracle_lib):
     recs = protocol.records(out[torch.from_numpy(sample).to(dev)])
     _sample_check(dev, oracle_lib, fr, lay, recs, 1, sample)
     del fr, out
+
+
+def test_config4_shard_16M_64B_whole_batch(dev, oracle_lib):
+    """BASELINE config 4: one GPU's shard — the last of eight, 16M x 64 B UDP at first_index
+    7 * 16M — through halo_rx_parse_batch_device. 16M frames take the lane kernel's grid-stride
+    loop over several passes (its grid covers 4M frames per pass). Whole batch vs the oracle,
+    histogram == records == the oracle's, every clean frame OK and every mutated one rejected."""
+    import torch
+
+    from halo_amd import protocol, synth
+    from halo_amd._lib import NetIf
+
+    n = 16 << 20
+    first = 7 * n
+    lay = synth.layout(n, length=64, mutate_shift=6, first_index=first)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    hist = torch.zeros(14, dtype=torch.int32, device=dev)
+    out = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                      max_len_hint=64, hist=hist)
+    torch.cuda.synchronize()
+    recs = protocol.records(out)
+    del out
+    h = hist.cpu().numpy().astype(np.int64)
+    mutated = (lay["kinds"] & 0x80) != 0
+    assert 0 < mutated.sum() < n // 32
+    assert h.sum() == n and h[0] == (~mutated).sum()
+    assert np.array_equal(np.bincount(recs["status"], minlength=14), h)
+    assert np.all(recs["status"][~mutated] == 0) and np.all(recs["status"][mutated] != 0)
+    host = fr["bytes"].cpu().numpy()
+    del fr
+    want, whist = oracle_lib.rx_batch(host, lay["lens"], oracle_lib.NetIf.make(), 1,
+                                      offsets_dw=lay["offsets_dw"], threads=16)
+    assert np.array_equal(h, whist.astype(np.int64))
+    assert_records_equal(recs, want, None, "config4 shard 7 of 8 (16M x 64 B)")
+
+
+def test_config5_full_size_4M_9000B(dev, oracle_lib):
+    """BASELINE config 5 at full size: 4M x 9000 B TCP, strided, 37.7 GB in one call (frame
+    addresses past 2^32 and 2^35). Reference verdict (caps kept): ETH_LEN for every frame. Jumbo
+    extension: every clean frame OK, every mutated one rejected, histogram == records, and 4096
+    frames sampled across the whole batch (first, last, spread) bit-exact vs the oracle."""
+    import torch
+
+    from halo_amd import protocol, synth
+    from halo_amd._lib import NetIf
+
+    n = 4 << 20
+    lay = synth.layout(n, length=9000, proto_mode=1, mutate_shift=6, ragged=False, first_index=3 << 22)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev, stride=9000)
+    mutated = (lay["kinds"] & 0x80) != 0
+    for flags in (1, 3):
+        hist = torch.zeros(14, dtype=torch.int32, device=dev)
+        out = protocol.parse_frames_strided(fr["bytes"], 9000, n, netif=NetIf.make(), length=9000,
+                                            check_sum_enable=True, jumbo=bool(flags & 2), hist=hist)
+        torch.cuda.synchronize()
+        h = hist.cpu().numpy().astype(np.int64)
+        st = out[:, 0].cpu().numpy()
+        assert np.array_equal(np.bincount(st, minlength=14), h)
+        if flags == 1:
+            assert h[1] == n  # ETH_LEN: len > 1514 (protocol/ethernet.go:31)
+        else:
+            assert h[0] == (~mutated).sum() and h.sum() == n
+            assert np.all(st[~mutated] == 0) and np.all(st[mutated] != 0)
+            idx = np.unique(np.concatenate([np.arange(1024), np.arange(n - 1024, n),
+                                            np.random.default_rng(5).choice(n, 2048, replace=False)]))
+            recs = protocol.records(out[torch.from_numpy(idx).to(dev)])
+            _sample_check(dev, oracle_lib, fr, lay, recs, flags, idx, stride=9000)
+        del out
+    del fr
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("length", [570, 1500])
+def test_uniform_ragged_batch_uniform_len_flag(dev, oracle_lib, length):
+    """A ragged batch of one frame length flagged HALO_RX_UNIFORM_LEN takes the uniform-length
+    kernel table (570 B: 4 lanes, 1500 B: 8 lanes per frame) instead of the mix kernel: records
+    bit-exact vs the oracle and identical to the automatic (mix) choice."""
+    import torch
+
+    from halo_amd import protocol, synth
+    from halo_amd._lib import NetIf
+
+    n = 200_000
+    lay = synth.layout(n, length=length, proto_mode=3, mutate_shift=4, first_index=31_000_000)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    outs = []
+    for uniform in (True, False):
+        hist = torch.zeros(14, dtype=torch.int32, device=dev)
+        out = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                          max_len_hint=length, uniform_len=uniform, hist=hist)
+        torch.cuda.synchronize()
+        outs.append((protocol.records(out), hist.cpu().numpy().astype(np.int64)))
+    want, whist = oracle_lib.rx_batch(fr["bytes"].cpu().numpy(), lay["lens"], oracle_lib.NetIf.make(), 1,
+                                      offsets_dw=lay["offsets_dw"], threads=16)
+    for recs, h in outs:
+        assert_records_equal(recs, want, None, f"{length} B uniform")
+        assert np.array_equal(h, whist.astype(np.int64))
 
 
 def test_config5_jumbo_9000B(dev, oracle_lib):

@@ -131,29 +131,26 @@ def test_fused_parse_route(dev, oracle_lib, golden, variant):
     batches = [(torch.from_numpy(data).to(dev), torch.from_numpy(offs.view(np.int32)).to(dev),
                 torch.from_numpy(lens.view(np.int16)).to(dev), 0), (fr["bytes"], fr["offsets_dw"], fr["lens"], 1500)]
     stream = torch.cuda.current_stream().cuda_stream
-    _lib.check("variant", _lib.lib.halo_rx_tune_variant(variant))
-    try:
-        for d, o_, ln, hint in batches:
-            n = int(ln.numel())
-            full = protocol.parse_frames_batch(d, o_, ln, netif=NetIf.make(), max_len_hint=hint)
-            want_ids = o.find_batch(protocol.records(full)["dst_ip"])
-            for compact in (False, True):
-                flags = 1 | (_lib.HALO_RX_RECORD_COMPACT if compact else 0)
-                width = 16 if compact else 32
-                ref = torch.empty((n, width), dtype=torch.uint8, device=dev)
-                _lib.check("parse", _lib.lib.halo_rx_parse_batch_device(
-                    d.data_ptr(), o_.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, ref.data_ptr(), None,
-                    stream))
-                got = torch.full((n, width), 0xEE, dtype=torch.uint8, device=dev)
-                rid = torch.zeros(n, dtype=torch.int32, device=dev)
-                _lib.check("fused", _lib.lib.halo_rx_parse_route_batch_device(
-                    d.data_ptr(), o_.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, got.data_ptr(), None,
-                    g._t, rid.data_ptr(), stream))
-                torch.cuda.synchronize()
-                assert torch.equal(got, ref), (variant, compact)
-                assert np.array_equal(rid.cpu().numpy().view(np.uint32), want_ids), (variant, compact)
-    finally:
-        _lib.lib.halo_rx_tune_variant(0)
+    vf = _lib.variant_flags(variant)
+    for d, o_, ln, hint in batches:
+        n = int(ln.numel())
+        full = protocol.parse_frames_batch(d, o_, ln, netif=NetIf.make(), max_len_hint=hint)
+        want_ids = o.find_batch(protocol.records(full)["dst_ip"])
+        for compact in (False, True):
+            flags = 1 | vf | (_lib.HALO_RX_RECORD_COMPACT if compact else 0)
+            width = 16 if compact else 32
+            ref = torch.empty((n, width), dtype=torch.uint8, device=dev)
+            _lib.check("parse", _lib.lib.halo_rx_parse_batch_device(
+                d.data_ptr(), o_.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, ref.data_ptr(), None,
+                stream))
+            got = torch.full((n, width), 0xEE, dtype=torch.uint8, device=dev)
+            rid = torch.zeros(n, dtype=torch.int32, device=dev)
+            _lib.check("fused", _lib.lib.halo_rx_parse_route_batch_device(
+                d.data_ptr(), o_.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), hint, got.data_ptr(), None,
+                g._t, rid.data_ptr(), stream))
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref), (variant, compact)
+            assert np.array_equal(rid.cpu().numpy().view(np.uint32), want_ids), (variant, compact)
     assert _lib.lib.halo_rx_parse_route_batch_device(None, None, None, 0, 1, NetIf.make(), 0, None, None, None,
                                                      None, None) == _lib.HALO_E_INVAL  # no table
 

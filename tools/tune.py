@@ -52,9 +52,9 @@ def main():
         ref = None
         res[name] = {}
         for g in gs:
-            _lib.check("tune", _lib.lib.halo_rx_tune_variant(g))
             # the last of the 20 steps parses batch 19 % rot: the same batch for every variant
-            wall, kms = bench.time_steps(bs, out, netif, flags=flags, hint=0, steps=20, warmup=3, d=d,
+            wall, kms = bench.time_steps(bs, out, netif, flags=flags | _lib.variant_flags(g), hint=0, steps=20,
+                                         warmup=3, d=d,
                                          strided_len=kw["length"] if strided else 0)
             h = torch.sum(out.view(torch.int64).view(-1, 4) * torch.arange(1, 5, device=dev)).item()
             if ref is None:
@@ -64,7 +64,6 @@ def main():
                             "GBps": round(alg / kms / 1e6, 1), "Mpps": round(n / kms / 1e3, 1), "same": ok}
             print(f"{name:10s} V={g:2d} {kms*1e3:9.1f} us  {alg / kms / 1e6:8.1f} GB/s  "
                   f"{n / kms / 1e3:9.1f} Mpps  {'ok' if ok else 'MISMATCH'}", flush=True)
-        _lib.lib.halo_rx_tune_variant(0)
         del bs, out
         torch.cuda.empty_cache()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
