@@ -8,9 +8,12 @@ one batch of 1M frames. Batches rotate over --rotate distinct slices of the synt
 so the working set (8 x 102 MB) exceeds the 256 MB Infinity Cache and every step streams
 from HBM.
 
-Multi-GPU (torchrun, one process per GPU): every rank parses its own shard of the global
-frame stream (weak scaling, no data-path collective; the gloo group only carries the
-barrier and the max-over-ranks timing). value = frames all ranks parsed / max wall time.
+Multi-GPU (torchrun, one process per GPU, --gpus N > 1): BASELINE config 4, the scaling run —
+128M x 64 B frames sharded by index, 128M/N per rank (strong scaling), one launch per step over
+the rank's whole shard. No data-path collective: the gloo group carries only the barrier, the
+max-over-ranks wall time and every rank's own average launch duration (per_rank_kernel_ms).
+value = 128M x steps / max wall time. At N=1 the headline stays config 2 (BASELINE's metric
+config) and the same config-4 run on one GPU is reported under "config4", the curve's 1-GPU point.
 
 Extra fields: roofline (dominant kernel, algorithmic bytes / HIP-event kernel time vs the
 8 TB/s HBM3E spec peak), cpu_baseline (the C oracle, a scalar port of the Go path, timed on
@@ -76,6 +79,16 @@ class Dist:
         t = torch.tensor([x], dtype=torch.float64)
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
+
+    def gather(self, x: float) -> list:
+        """x from every rank, in rank order."""
+        if not self.pg:
+            return [x]
+        import torch
+
+        parts = [torch.zeros(1, dtype=torch.float64) for _ in range(self.world)]
+        self.pg.all_gather(parts, torch.tensor([x], dtype=torch.float64))
+        return [float(t.item()) for t in parts]
 
     def close(self):
         if self.pg:
@@ -180,6 +193,49 @@ def time_steps(batches, out, netif, *, flags, hint, steps, warmup, d: Dist, stri
     torch.cuda.synchronize()
     d.barrier()
     return d.max(wall.value), region.value / steps
+
+
+CONFIG4_FRAMES = 128 << 20  # BASELINE configs[3]: 128M x 64 B IPv4/UDP, sharded by index
+
+
+def config4_shard(rank: int, world: int, total: int = CONFIG4_FRAMES):
+    """(first global frame index, frame count) of `rank`'s config-4 shard: contiguous, disjoint,
+    equal ranges covering [0, total) (total is a multiple of 1, 2, 4 and 8)."""
+    per = total // world
+    assert per * world == total, (total, world)
+    return rank * per, per
+
+
+def config4_run(dev, netif, d: Dist, steps: int, warmup: int) -> dict:
+    """BASELINE config 4 on the ranks of this job: the 128M x 64 B frame stream sharded by index,
+    rank r parsing global frames [r * 128M/N, (r + 1) * 128M/N) on its own GPU, one launch per step
+    over its whole shard (strong scaling: the total is fixed). No data-path collective: the gloo
+    group carries only the start barrier, the max-over-ranks wall time and each rank's own average
+    launch duration. value = 128M frames x steps / max wall."""
+    import torch
+
+    first, per = config4_shard(d.rank, d.world)
+    log(f"[rank {d.rank}] config4: generating {per} frames of 64 B (global frames {first}..)")
+    assert shard_first_index(d.rank, 0, per, 1) == first
+    fr = make_batches(dev, netif, n=per, rotate=1, rank=d.rank)
+    out = torch.empty((per, RESULT_BYTES), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    wall, kms = time_steps(fr, out, netif, flags=1, hint=64, steps=steps, warmup=warmup, d=d)
+    per_rank = d.gather(kms)
+    fb = frame_bytes(fr[0])
+    alg = fb + per * (4 + 2 + RESULT_BYTES)
+    res = {"workload": f"config4: {CONFIG4_FRAMES >> 20}M x 64B IPv4/UDP frames sharded by index over {d.world} "
+                       f"GPU(s), {per >> 20}M frames per GPU per step, CheckSumEnable=true, 32B record/frame",
+           "frames_total": CONFIG4_FRAMES, "frames_per_rank": per, "steps": steps,
+           "value": round(CONFIG4_FRAMES * steps / wall / 1e6, 2), "unit": "Mpps",
+           "gbit_s": round(fb * d.world * steps * 8 / wall / 1e9, 2),
+           "ms_per_step": round(wall / steps * 1e3, 4), "scaling": "strong",
+           "per_rank_kernel_ms": [round(k, 5) for k in per_rank],
+           "roofline_rank0": roofline(alg, per_rank[0], load_traffic(f"config4_{per >> 20}M")),
+           "alg_bytes_per_rank_launch": alg}
+    del fr, out
+    torch.cuda.empty_cache()
+    return res
 
 
 TX_BENCH_STEPS = 0x01 | 0x04 | 0x10  # NatChangeDst + NatChangeSrc + eth_tx DPDK fill
@@ -655,7 +711,11 @@ def cpu_baseline(fr, seconds: float):
     host = fr["bytes"].cpu().numpy()
     netif = oracle.NetIf.make()
     res = {}
-    for threads in (1, min(os.cpu_count() or 1, 16)):
+    # all cores this process may run on, bounded by the host's CPU share for it when one is set
+    # (the GPU box exports OMP_NUM_THREADS = its per-GPU share; sched_getaffinity shows the machine)
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS") or affinity)
+    for threads in (1, max(1, min(affinity, share))):
         oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads)  # warm
         passes, t0 = 0, time.perf_counter()
         while True:
@@ -678,7 +738,9 @@ def cpu_baseline(fr, seconds: float):
             "sample": f"{lay['n']} x {int(lay['lens'][0])}B UDP frames (batch 0 of the workload), "
                       f"{one[1]} passes in {one[2]:.1f}s, oracle/halo_rx_oracle.c -O2, one thread "
                       f"(the reference's one goroutine per NetIf); cpu={model}",
-            "multi_thread": {"value": round(mt[0], 3), "threads": max(res), "passes": mt[1]}}
+            "multi_thread": {"value": round(mt[0], 3), "threads": max(res), "passes": mt[1],
+                             "cpus_in_affinity": affinity, "cpu_share": share,
+                             "note": "index-sharded over threads = min(sched_getaffinity, OMP_NUM_THREADS)"}}
 
 
 def main():
@@ -698,6 +760,26 @@ def main():
     netif = NetIf.make()  # eth0 of example.UsePcapDev (example/example.go:768-773)
     measure_read_peak(dev, d)
     n = args.frames
+    if d.world > 1:
+        # BASELINE config 4, the scaling-curve run: 128M x 64 B sharded by index over the N GPUs
+        c4 = config4_run(dev, netif, d, args.steps, args.warmup)
+        line = {
+            "metric": METRIC, "value": c4["value"], "unit": "Mpps", "n_gpus": d.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": c4["ms_per_step"], "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": c4["workload"], "frames_total": CONFIG4_FRAMES,
+                       "frames_per_gpu_per_step": c4["frames_per_rank"], "frame_bytes": 64,
+                       "parallelism": f"index-sharded x{d.world}, no collective"},
+            "gbit_s": c4["gbit_s"], "per_rank_kernel_ms": c4["per_rank_kernel_ms"],
+            "kernel_ms": max(c4["per_rank_kernel_ms"]),
+            "kernel": "rx_lane_kernel<0, 0> (lane per frame, ragged, no fused pass)",
+            "roofline": c4["roofline_rank0"], "cpu_baseline": None,
+            "note": "N=1 runs report BASELINE config 2 as value and this same config-4 run on one GPU under "
+                    "'config4' (the 1-GPU point of this curve)"}
+        d.close()
+        if d.rank == 0:
+            print(json.dumps(line), flush=True)
+        return
 
     log(f"[rank {d.rank}] generating {args.rotate} x {n} frames of 64 B")
     batches = make_batches(dev, netif, n=n, rotate=args.rotate, rank=d.rank)
@@ -780,9 +862,10 @@ def main():
         torch.cuda.empty_cache()
         sec["route_lpm_500k_prefixes"] = route_secondary(dev, max(10, args.steps // 4), 3, d, with_cpu=not args.no_cpu)
         torch.cuda.empty_cache()
+        line["config4"] = config4_run(dev, netif, d, max(20, args.steps // 4), 3)
         for name, kw, hint, strided_len, flags in [
             ("config4_shard_16M_64B", dict(length=64), 64, 0, 1),
-            ("1500B_udp_1M", dict(length=1500), 1500, 0, 1),
+            ("1500B_udp_1M", dict(length=1500), 1500, 0, 1 | _lib.HALO_RX_UNIFORM_LEN),
             ("config3_imix_16M", dict(size_mode=1, proto_mode=3), 1500, 0, 1),
             ("config5_jumbo_9000B_tcp_4M_ext", dict(length=9000, proto_mode=1, strided=True), 0, 9000, 3),
         ]:
