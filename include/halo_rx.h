@@ -369,6 +369,64 @@ HALO_API int halo_tx_fixup_batch_device(uint8_t* d_bytes, const uint32_t* d_offs
                                         uint32_t max_len_hint, uint8_t* d_result,
                                         halo_stream_t stream);
 
+/* ---- transmit direction: batch packet construction (the Build* half) --
+ * The locally originated send chain, one frame per descriptor:
+ *   NetIf.TxUdp / TxTcp / TxIcmp   engine/{udp,tcp,icmp}_engine.go:24-32 / :29-37 / :26-34
+ *    -> protocol.BuildUdpPkt        protocol/udp.go:52-91   (payload <= 1472)
+ *       protocol.BuildTcpPkt        protocol/tcp.go:73-123  (payload <= 1460; 20 B header, window 256)
+ *       protocol.BuildIcmpPkt       protocol/icmp.go:66-89  (payload <= 1472; code 0)
+ *    -> NetIf.TxIpv4                engine/ipv4_engine.go:50-99
+ *       protocol.BuildIpv4Pkt       protocol/ipv4.go:89-131 (iphId++ per packet, TTL 0x80, no frag)
+ *    -> NetIf.TxEthernet            engine/ethernet_engine.go:34-50
+ *       protocol.BuildEthFrm        protocol/ethernet.go:58-82 (src MAC = the NetIf's, pad to 60 B)
+ * `flags & HALO_RX_CSUM_ENABLE` is protocol.CheckSumEnable: it gates the IPv4 header, UDP and
+ * TCP checksums (0 when off); the ICMP checksum is always filled (icmp.go:84-87). TxIpv4's
+ * control-plane decisions (FindRoute, the ARP cache, broadcast) are the caller's: each
+ * descriptor carries the destination MAC they produced and its mode:
+ *   HALO_TX_BUILD_ETH       the Ethernet frame TxEthernet hands to EthTxFunc
+ *   HALO_TX_BUILD_LOOPBACK  the IPv4 packet alone: the copy TxIpv4 puts into the NetIf's LoChan
+ *                           when the destination is its own address (engine/ipv4_engine.go:72-79),
+ *                           which the L3 loopback parse (HALO_RX_L3_START) consumes.
+ * iphId (protocol/ipv4.go:33, process-global in Go) is the device u16 *d_ip_id: BuildIpv4Pkt's
+ * `iphId++` runs once per packet that reaches it, in descriptor order, so the k-th successfully
+ * built packet of the batch (k = 1, 2, ...) carries id *d_ip_id + k, and *d_ip_id is advanced by
+ * the number built. A descriptor whose Build* call returns an error is not built (no iphId step,
+ * length 0, result code below). */
+#define HALO_TX_BUILD_ETH 0u
+#define HALO_TX_BUILD_LOOPBACK 1u
+#define HALO_TX_B_OK 0u
+#define HALO_TX_B_PAYLOAD_LEN 1u /* "payload len must <= 1472" (udp.go:55, icmp.go:71) / "<= 1460" (tcp.go:78) */
+#define HALO_TX_B_PROTO 2u       /* build-defined: proto is not UDP (17), TCP (6) or ICMP (1)          */
+#define HALO_TX_B_SLOT 3u        /* build-defined: the frame is longer than out_stride                  */
+typedef struct halo_tx_build_desc {
+    uint64_t payload_off;  /* byte offset of the L4 payload in d_payload (any alignment)         */
+    uint16_t payload_len;
+    uint8_t proto;         /* IPH_PROTO_UDP / _TCP / _ICMP (protocol/ipv4.go:27-32)               */
+    uint8_t aux;           /* TCP flags; ICMP type                                                */
+    uint16_t src_port;     /* UDP/TCP source port; ICMP: the 2 icmpId bytes as a big-endian u16  */
+    uint16_t dst_port;     /* UDP/TCP destination port; ICMP: icmpSeq                            */
+    uint32_t src_ip;       /* IpAddrToU(srcAddr): the NetIf's address for Tx*                    */
+    uint32_t dst_ip;       /* IpAddrToU(dstAddr)                                                 */
+    uint32_t seq;          /* TCP seqNum                                                         */
+    uint32_t ack;          /* TCP ackNum                                                         */
+    uint8_t dst_mac[6];    /* ETH mode: TxIpv4's broadcast / ARP-cache result                    */
+    uint8_t mode;          /* HALO_TX_BUILD_*                                                    */
+    uint8_t pad;
+} halo_tx_build_desc_t;    /* 40 B */
+
+/* Device workspace for n descriptors. Zero it once before its first use (hipMemset); every
+ * launch leaves it zeroed again for the next one. One launch at a time per workspace. */
+HALO_API uint64_t halo_tx_build_workspace(uint32_t n);
+/* Build n frames into fixed output slots: frame i at d_frames + i * out_stride (a multiple of
+ * 4, at least 60), d_out_lens[i] = its length (0 when not built), d_result[i] (optional) =
+ * HALO_TX_B_*. The bytes of a slot past the frame's last 4-byte word are left untouched.
+ * `max_payload_hint` (0 = unknown) picks the lanes per frame. Asynchronous on `stream`.     */
+HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d_desc, uint32_t n, const uint8_t* d_payload,
+                                        uint32_t flags, const halo_rx_netif_t* netif, uint32_t max_payload_hint,
+                                        uint8_t* d_frames, uint32_t out_stride, uint16_t* d_out_lens,
+                                        uint8_t* d_result, uint16_t* d_ip_id, void* d_workspace,
+                                        uint64_t workspace_bytes, halo_stream_t stream);
+
 /* ---- flow-key hashing --------------------------------------------
  * hashcode.GetHashCodeXXH3 (hashcode/hashcode.go:15-17 -> hashcode/xxh3.go:43-287, XXH3-64 with
  * the default secret and seed 0, ported from github.com/zeebo/xxh3 v1.1.0) over a batch of byte

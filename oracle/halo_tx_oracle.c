@@ -261,3 +261,202 @@ ORA_API int ora_tx_batch(uint8_t* bytes, const uint32_t* offsets_dw, const uint1
     free(tid);
     return rc;
 }
+
+/* ================================================================================================
+ * The Build* half of row f2: locally originated packets, restated one Go function at a time
+ * (TEST INFRASTRUCTURE ONLY; the product is halo_tx_build_batch_device in tx_build.hip).
+ *   BuildUdpPkt   protocol/udp.go:52-91      BuildTcpPkt  protocol/tcp.go:73-123
+ *   BuildIcmpPkt  protocol/icmp.go:66-89     BuildIpv4Pkt protocol/ipv4.go:89-131 (iphId, :33)
+ *   BuildEthFrm   protocol/ethernet.go:58-82
+ *   drivers       NetIf.TxUdp/TxTcp/TxIcmp (engine/{udp,tcp,icmp}_engine.go), TxIpv4
+ *                 (engine/ipv4_engine.go:50-99: the LoChan copy for the NetIf's own address),
+ *                 TxEthernet (engine/ethernet_engine.go:34-50)
+ * Every Tx* driver passes an empty buffer (`make([]byte, 0, cap)`), so each Build* writes its
+ * header at offset 0 of its own slice; `append` becomes a write at the running length.
+ * ============================================================================================== */
+
+/* protocol/udp.go:52-91. Returns the packet length, or -1 (payload len must <= 1472). */
+static long build_udp(uint8_t* pkt, const uint8_t* payload, size_t plen, uint16_t src_port, uint16_t dst_port,
+                      const uint8_t src[4], const uint8_t dst[4], int csum_enable) {
+    if (plen > 1472) return -1;
+    size_t n = 0;
+    pkt[n++] = (uint8_t)(src_port >> 8); pkt[n++] = (uint8_t)src_port;
+    pkt[n++] = (uint8_t)(dst_port >> 8); pkt[n++] = (uint8_t)dst_port;
+    const uint16_t udp_len = (uint16_t)(plen + 8);
+    pkt[n++] = (uint8_t)(udp_len >> 8); pkt[n++] = (uint8_t)udp_len;
+    pkt[n++] = 0x00; pkt[n++] = 0x00;
+    memcpy(pkt + n, payload, plen);
+    n += plen;
+    if (csum_enable) {
+        uint8_t* sum_data = (uint8_t*)malloc(12 + n);  /* fakeHeader + pkt (:74-84) */
+        memcpy(sum_data, src, 4);
+        memcpy(sum_data + 4, dst, 4);
+        sum_data[8] = 0x00; sum_data[9] = 0x11;
+        sum_data[10] = (uint8_t)(udp_len >> 8); sum_data[11] = (uint8_t)udp_len;
+        memcpy(sum_data + 12, pkt, n);
+        const uint16_t sum = ora_get_checksum(sum_data, 12 + n);
+        free(sum_data);
+        pkt[6] = (uint8_t)(sum >> 8); pkt[7] = (uint8_t)sum;
+    } else {
+        pkt[6] = 0x00; pkt[7] = 0x00;
+    }
+    return (long)n;
+}
+
+/* protocol/tcp.go:73-123. Returns the packet length, or -1 (payload len must <= 1460). */
+static long build_tcp(uint8_t* pkt, const uint8_t* payload, size_t plen, uint16_t src_port, uint16_t dst_port,
+                      const uint8_t src[4], const uint8_t dst[4], uint32_t seq, uint32_t ack, uint8_t flags,
+                      int csum_enable) {
+    if (plen > 1460) return -1;
+    size_t n = 0;
+    pkt[n++] = (uint8_t)(src_port >> 8); pkt[n++] = (uint8_t)src_port;
+    pkt[n++] = (uint8_t)(dst_port >> 8); pkt[n++] = (uint8_t)dst_port;
+    pkt[n++] = (uint8_t)(seq >> 24); pkt[n++] = (uint8_t)(seq >> 16); pkt[n++] = (uint8_t)(seq >> 8); pkt[n++] = (uint8_t)seq;
+    pkt[n++] = (uint8_t)(ack >> 24); pkt[n++] = (uint8_t)(ack >> 16); pkt[n++] = (uint8_t)(ack >> 8); pkt[n++] = (uint8_t)ack;
+    pkt[n++] = 0x50; pkt[n++] = flags;       /* data offset 5 words + flags (:96) */
+    pkt[n++] = 0x01; pkt[n++] = 0x00;        /* window 256 (:98) */
+    pkt[n++] = 0x00; pkt[n++] = 0x00;        /* checksum */
+    pkt[n++] = 0x00; pkt[n++] = 0x00;        /* urgent pointer */
+    memcpy(pkt + n, payload, plen);
+    n += plen;
+    if (csum_enable) {
+        const size_t total = 20 + plen;      /* totalLen (:113) */
+        uint8_t* sum_data = (uint8_t*)malloc(12 + n);
+        memcpy(sum_data, src, 4);
+        memcpy(sum_data + 4, dst, 4);
+        sum_data[8] = 0x00; sum_data[9] = 0x06;
+        sum_data[10] = (uint8_t)(total >> 8); sum_data[11] = (uint8_t)total;
+        memcpy(sum_data + 12, pkt, n);
+        const uint16_t sum = ora_get_checksum(sum_data, 12 + n);
+        free(sum_data);
+        pkt[16] = (uint8_t)(sum >> 8); pkt[17] = (uint8_t)sum;
+    } else {
+        pkt[16] = 0x00; pkt[17] = 0x00;
+    }
+    return (long)n;
+}
+
+/* protocol/icmp.go:66-89 (icmpId: two bytes). Always checksummed. -1: payload len must <= 1472. */
+static long build_icmp(uint8_t* pkt, const uint8_t* payload, size_t plen, uint8_t type, const uint8_t id[2],
+                       uint16_t seq) {
+    if (plen > 1472) return -1;
+    size_t n = 0;
+    pkt[n++] = type;
+    pkt[n++] = 0x00;
+    pkt[n++] = 0x00; pkt[n++] = 0x00;
+    pkt[n++] = id[0]; pkt[n++] = id[1];
+    pkt[n++] = (uint8_t)(seq >> 8); pkt[n++] = (uint8_t)seq;
+    memcpy(pkt + n, payload, plen);
+    n += plen;
+    const uint16_t sum = ora_get_checksum(pkt, n);
+    pkt[2] = (uint8_t)(sum >> 8); pkt[3] = (uint8_t)sum;
+    return (long)n;
+}
+
+/* protocol/ipv4.go:89-131; *iph_id is the package global iphId (:33), incremented before use. */
+static long build_ipv4(uint8_t* pkt, const uint8_t* payload, size_t plen, uint8_t proto, const uint8_t src[4],
+                       const uint8_t dst[4], uint16_t* iph_id, int csum_enable) {
+    if (plen > 1480) return -1;
+    size_t n = 0;
+    pkt[n++] = 0x45; pkt[n++] = 0x00;
+    const uint16_t ip_len = (uint16_t)(plen + 20);
+    pkt[n++] = (uint8_t)(ip_len >> 8); pkt[n++] = (uint8_t)ip_len;
+    *iph_id = (uint16_t)(*iph_id + 1);
+    pkt[n++] = (uint8_t)(*iph_id >> 8); pkt[n++] = (uint8_t)*iph_id;
+    pkt[n++] = 0x00; pkt[n++] = 0x00;
+    pkt[n++] = 0x80;
+    pkt[n++] = proto;
+    pkt[n++] = 0x00; pkt[n++] = 0x00;
+    memcpy(pkt + n, src, 4); n += 4;
+    memcpy(pkt + n, dst, 4); n += 4;
+    if (csum_enable) {
+        const uint16_t sum = ora_get_checksum(pkt, n);
+        pkt[10] = (uint8_t)(sum >> 8); pkt[11] = (uint8_t)sum;
+    } else {
+        pkt[10] = 0x00; pkt[11] = 0x00;
+    }
+    memcpy(pkt + n, payload, plen);
+    n += plen;
+    return (long)n;
+}
+
+/* protocol/ethernet.go:58-82: dst, src, EtherType, payload, zero padding to 60. */
+static long build_eth(uint8_t* frm, const uint8_t* payload, size_t plen, const uint8_t dst_mac[6],
+                      const uint8_t src_mac[6], uint16_t eth_proto) {
+    if (plen > 1500) return -1;
+    size_t n = 0;
+    memcpy(frm, dst_mac, 6); n += 6;
+    memcpy(frm + n, src_mac, 6); n += 6;
+    frm[n++] = (uint8_t)(eth_proto >> 8); frm[n++] = (uint8_t)eth_proto;
+    memcpy(frm + n, payload, plen);
+    n += plen;
+    while (n < 60) frm[n++] = 0x00;
+    return (long)n;
+}
+
+static void be32_put(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+
+/* One descriptor through Tx{Udp,Tcp,Icmp} -> TxIpv4 -> TxEthernet (or TxIpv4's LoChan copy).
+ * Writes the frame into out[0 .. *out_len) and returns HALO_TX_B_*; `out` holds >= 1514 B. */
+ORA_API uint8_t ora_tx_build_frame(const halo_tx_build_desc_t* d, const uint8_t* payload_base,
+                                   const uint8_t src_mac[6], uint32_t flags, uint16_t* iph_id, uint8_t* out,
+                                   uint16_t* out_len) {
+    const int csum = (flags & HALO_RX_CSUM_ENABLE) != 0;
+    const uint8_t* payload = payload_base + d->payload_off;
+    uint8_t src[4], dst[4], l4[1514], ip[1514];
+    be32_put(src, d->src_ip);
+    be32_put(dst, d->dst_ip);
+    long l4n;
+    *out_len = 0;
+    if (d->proto == 0x11) {
+        l4n = build_udp(l4, payload, d->payload_len, d->src_port, d->dst_port, src, dst, csum);
+    } else if (d->proto == 0x06) {
+        l4n = build_tcp(l4, payload, d->payload_len, d->src_port, d->dst_port, src, dst, d->seq, d->ack, d->aux, csum);
+    } else if (d->proto == 0x01) {
+        const uint8_t id[2] = {(uint8_t)(d->src_port >> 8), (uint8_t)d->src_port};
+        l4n = build_icmp(l4, payload, d->payload_len, d->aux, id, d->dst_port);
+    } else {
+        return HALO_TX_B_PROTO;
+    }
+    if (l4n < 0) return HALO_TX_B_PAYLOAD_LEN;
+    const long ipn = build_ipv4(ip, l4, (size_t)l4n, d->proto, src, dst, iph_id, csum);
+    if (ipn < 0) return HALO_TX_B_PAYLOAD_LEN; /* unreachable: every L4 limit keeps ipv4 payload <= 1480 */
+    if (d->mode == HALO_TX_BUILD_LOOPBACK) {    /* engine/ipv4_engine.go:72-79: copy of ipv4Pkt */
+        memcpy(out, ip, (size_t)ipn);
+        *out_len = (uint16_t)ipn;
+        return HALO_TX_B_OK;
+    }
+    const long fn = build_eth(out, ip, (size_t)ipn, d->dst_mac, src_mac, 0x0800);
+    *out_len = (uint16_t)fn;
+    return HALO_TX_B_OK;
+}
+
+/* Serial batch in descriptor order (iphId is a sequence): frames into slots of out_stride bytes.
+ * A frame longer than its slot (build-defined; Go has no slots) gets HALO_TX_B_SLOT and is
+ * refused before Build* runs: no iphId step, nothing stored. */
+ORA_API int ora_tx_build_batch(const halo_tx_build_desc_t* desc, uint32_t n, const uint8_t* payload, uint32_t flags,
+                               const uint8_t src_mac[6], uint8_t* frames, uint32_t out_stride, uint16_t* out_lens,
+                               uint8_t* result, uint16_t* iph_id) {
+    uint8_t tmp[1514];
+    for (uint32_t i = 0; i < n; ++i) {
+        const halo_tx_build_desc_t* d = &desc[i];
+        /* the slot check needs only the descriptor: frame length from the Build* arithmetic */
+        const uint32_t l4 = (d->proto == 0x06 ? 20u : 8u) + d->payload_len;
+        const uint32_t fl = d->mode == HALO_TX_BUILD_LOOPBACK ? 20u + l4 : (34u + l4 < 60u ? 60u : 34u + l4);
+        uint16_t len = 0;
+        uint8_t r;
+        const int known = d->proto == 0x11 || d->proto == 0x06 || d->proto == 0x01;
+        const uint32_t lim = d->proto == 0x06 ? 1460u : 1472u;
+        if (known && d->payload_len <= lim && fl > out_stride) {
+            r = HALO_TX_B_SLOT; /* refused before Build*: no iphId step */
+        } else {
+            r = ora_tx_build_frame(d, payload, src_mac, flags, iph_id, tmp, &len);
+            if (r == HALO_TX_B_OK) memcpy(frames + (uint64_t)i * out_stride, tmp, len);
+        }
+        if (out_lens) out_lens[i] = r == HALO_TX_B_OK ? len : 0;
+        if (result) result[i] = r;
+    }
+    return 0;
+}

@@ -95,6 +95,8 @@ def lib() -> ctypes.CDLL:
         L.ora_route_find_batch.argtypes = [vp, vp, u32, vp]
         L.ora_tx_batch.restype = ctypes.c_int
         L.ora_tx_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, ctypes.c_int]
+        L.ora_tx_build_batch.restype = ctypes.c_int
+        L.ora_tx_build_batch.argtypes = [vp, u32, vp, u32, vp, vp, u32, vp, vp, ctypes.POINTER(ctypes.c_uint16)]
         u64p = ctypes.POINTER(ctypes.c_uint64)
         u32p = ctypes.POINTER(ctypes.c_uint32)
         L.ora_ring_create.restype = ctypes.c_int
@@ -211,6 +213,31 @@ def tx_batch(data: np.ndarray, offsets_dw: np.ndarray, lens: np.ndarray, ops: np
     ops_c = np.ascontiguousarray(ops, dtype=TX_OP_DTYPE)
     assert lib().ora_tx_batch(_p(out), _p(offs), _p(lens_c), n, _p(ops_c), flags, _p(res), threads) == 0
     return out, res
+
+
+# halo_tx_build_desc_t (40 B), include/halo_rx.h
+BUILD_DESC_DTYPE = np.dtype([("payload_off", "<u8"), ("payload_len", "<u2"), ("proto", "u1"), ("aux", "u1"),
+                             ("src_port", "<u2"), ("dst_port", "<u2"), ("src_ip", "<u4"), ("dst_ip", "<u4"),
+                             ("seq", "<u4"), ("ack", "<u4"), ("dst_mac", "u1", (6,)), ("mode", "u1"),
+                             ("pad", "u1")])
+assert BUILD_DESC_DTYPE.itemsize == 40
+
+
+def tx_build_batch(desc: np.ndarray, payload: np.ndarray, src_mac: bytes, flags: int = 1, out_stride: int = 1516,
+                   ip_id: int = 0):
+    """The Build* chain over a descriptor batch (ora_tx_build_batch): (frames [n, out_stride] with
+    untouched slot bytes 0, lens, results, new iphId)."""
+    desc = np.ascontiguousarray(desc, dtype=BUILD_DESC_DTYPE)
+    n = int(desc.shape[0])
+    pay = np.ascontiguousarray(payload, dtype=np.uint8)
+    frames = np.zeros((max(n, 1), out_stride), dtype=np.uint8)
+    lens = np.zeros(max(n, 1), dtype=np.uint16)
+    res = np.zeros(max(n, 1), dtype=np.uint8)
+    mac = np.frombuffer(bytes(src_mac), dtype=np.uint8).copy()
+    iph = ctypes.c_uint16(ip_id)
+    assert lib().ora_tx_build_batch(_p(desc), n, _p(pay), flags, _p(mac), _p(frames), out_stride, _p(lens), _p(res),
+                                    ctypes.byref(iph)) == 0
+    return frames[:n], lens[:n], res[:n], int(iph.value)
 
 
 def xxh3_64(data: bytes) -> int:

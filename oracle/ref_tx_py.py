@@ -184,3 +184,112 @@ def tx_frame(frame: bytearray, steps: int, dst_ip=0, dst_port=0, src_ip=0, src_p
     if steps & DPDK_FILL:
         r |= dpdk_tx_fill(frame)
     return r
+
+
+# ---- the Build* half of row f2 (locally originated packets), restated from the Go source -------
+#   BuildUdpPkt protocol/udp.go:52-91, BuildTcpPkt tcp.go:73-123, BuildIcmpPkt icmp.go:66-89,
+#   BuildIpv4Pkt ipv4.go:89-131 (iphId ipv4.go:33, `iphId++` before use), BuildEthFrm
+#   ethernet.go:58-82; drivers NetIf.Tx{Udp,Tcp,Icmp} -> TxIpv4 (engine/ipv4_engine.go:50-99,
+#   the LoChan copy at :72-79) -> TxEthernet (engine/ethernet_engine.go:34-50).
+B_OK, B_PAYLOAD_LEN, B_PROTO, B_SLOT = 0, 1, 2, 3
+MODE_ETH, MODE_LOOPBACK = 0, 1
+
+
+class BuildError(Exception):
+    pass
+
+
+def go_build_udp(payload: bytes, src_port: int, dst_port: int, src: bytes, dst: bytes, en: bool) -> bytearray:
+    if len(payload) > 1472:
+        raise BuildError("payload len must <= 1472")
+    udp_len = (len(payload) + 8) & 0xFFFF
+    pkt = bytearray()
+    pkt += src_port.to_bytes(2, "big") + dst_port.to_bytes(2, "big") + udp_len.to_bytes(2, "big") + b"\x00\x00"
+    pkt += payload
+    if en:
+        fake = bytes(src) + bytes(dst) + b"\x00\x11" + udp_len.to_bytes(2, "big")
+        _put16(pkt, 6, get_checksum(fake + bytes(pkt)))
+    else:
+        _put16(pkt, 6, 0)
+    return pkt
+
+
+def go_build_tcp(payload: bytes, src_port: int, dst_port: int, src: bytes, dst: bytes, seq: int, ack: int,
+                 flags: int, en: bool) -> bytearray:
+    if len(payload) > 1460:
+        raise BuildError("payload len must <= 1460")
+    pkt = bytearray()
+    pkt += src_port.to_bytes(2, "big") + dst_port.to_bytes(2, "big")
+    pkt += seq.to_bytes(4, "big") + ack.to_bytes(4, "big")
+    pkt += bytes([0x50, flags, 0x01, 0x00, 0x00, 0x00, 0x00, 0x00])
+    pkt += payload
+    if en:
+        total = 20 + len(payload)
+        fake = bytes(src) + bytes(dst) + b"\x00\x06" + (total & 0xFFFF).to_bytes(2, "big")
+        _put16(pkt, 16, get_checksum(fake + bytes(pkt)))
+    else:
+        _put16(pkt, 16, 0)
+    return pkt
+
+
+def go_build_icmp(payload: bytes, icmp_type: int, icmp_id: bytes, seq: int) -> bytearray:
+    if len(payload) > 1472:
+        raise BuildError("payload len must <= 1472")
+    pkt = bytearray([icmp_type, 0x00, 0x00, 0x00]) + bytearray(icmp_id) + bytearray(seq.to_bytes(2, "big"))
+    pkt += payload
+    _put16(pkt, 2, get_checksum(bytes(pkt)))  # CheckSumEnable is not consulted (icmp.go:84-87)
+    return pkt
+
+
+class IphId:
+    """protocol.iphId: the package-global IPv4 identification counter."""
+
+    def __init__(self, value: int = 0):
+        self.value = value & 0xFFFF
+
+
+def go_build_ipv4(payload: bytes, proto: int, src: bytes, dst: bytes, iph: IphId, en: bool) -> bytearray:
+    if len(payload) > 1480:
+        raise BuildError("payload len must <= 1480 bytes")
+    pkt = bytearray([0x45, 0x00]) + bytearray(((len(payload) + 20) & 0xFFFF).to_bytes(2, "big"))
+    iph.value = (iph.value + 1) & 0xFFFF
+    pkt += iph.value.to_bytes(2, "big") + b"\x00\x00" + bytes([0x80, proto, 0x00, 0x00]) + bytes(src) + bytes(dst)
+    _put16(pkt, 10, get_checksum(bytes(pkt)) if en else 0)
+    return pkt + bytearray(payload)
+
+
+def go_build_eth(payload: bytes, dst_mac: bytes, src_mac: bytes, eth_proto: int) -> bytearray:
+    if len(payload) > 1500:
+        raise BuildError("payload len must <= 1500 bytes")
+    frm = bytearray(dst_mac) + bytearray(src_mac) + bytearray(eth_proto.to_bytes(2, "big")) + bytearray(payload)
+    return frm + bytearray(max(0, 60 - len(frm)))
+
+
+def tx_build(desc: dict, payload: bytes, src_mac: bytes, iph: IphId, check_sum_enable=True):
+    """One halo_tx_build_desc_t through Tx* -> TxIpv4 -> TxEthernet / LoChan: (result, frame)."""
+    en = bool(check_sum_enable)
+    src = desc["src_ip"].to_bytes(4, "big")
+    dst = desc["dst_ip"].to_bytes(4, "big")
+    proto = desc["proto"]
+    try:
+        if proto == 0x11:
+            l4 = go_build_udp(payload, desc["src_port"], desc["dst_port"], src, dst, en)
+        elif proto == 0x06:
+            l4 = go_build_tcp(payload, desc["src_port"], desc["dst_port"], src, dst, desc["seq"], desc["ack"],
+                              desc["aux"], en)
+        elif proto == 0x01:
+            l4 = go_build_icmp(payload, desc["aux"], desc["src_port"].to_bytes(2, "big"), desc["dst_port"])
+        else:
+            return B_PROTO, b""
+    except BuildError:
+        return B_PAYLOAD_LEN, b""
+    ip = go_build_ipv4(bytes(l4), proto, src, dst, iph, en)
+    if desc["mode"] == MODE_LOOPBACK:
+        return B_OK, bytes(ip)
+    return B_OK, bytes(go_build_eth(bytes(ip), bytes(desc["dst_mac"]), src_mac, 0x0800))
+
+
+def tx_build_len(desc: dict) -> int:
+    """The frame length the Build* chain produces for a descriptor (no bytes needed)."""
+    l4 = (20 if desc["proto"] == 0x06 else 8) + desc["payload_len"]
+    return 20 + l4 if desc["mode"] == MODE_LOOPBACK else max(60, 34 + l4)

@@ -94,3 +94,41 @@ def assert_tx_equal(data, offsets_dw, lens, results, meta, exp, flag, entries=No
             bad.append((k, meta["frames"][e["frame"]]["name"], e["op"][0], got.tobytes().hex(),
                         want.tobytes().hex(), int(results[k]), e["result"][str(flag)]))
     assert not bad, f"{what}: {len(bad)} of {len(ents)} entries differ; first: {bad[:3]}"
+
+
+def build_golden(root):
+    """The §8f f2 Build* fixtures: (descriptor array, payload bytes, meta, expected frames blob)."""
+    import json
+    import os
+
+    from oracle.oracle import BUILD_DESC_DTYPE
+
+    g = os.path.join(root, "tests", "golden")
+    with open(os.path.join(g, "tx_build.json")) as fh:
+        meta = json.load(fh)
+    desc = np.zeros(len(meta["descs"]), dtype=BUILD_DESC_DTYPE)
+    for i, d in enumerate(meta["descs"]):
+        for k, v in d.items():
+            desc[i][k] = v
+    payload = np.fromfile(os.path.join(g, "tx_build_payload.bin"), dtype=np.uint8)
+    expect = np.fromfile(os.path.join(g, "tx_build_expect.bin"), dtype=np.uint8)
+    return desc, payload, meta, expect
+
+
+def assert_build_equal(frames, lens, res, ip_end, run, expect, what="", names=None):
+    """Built frames / lengths / results / final iphId == one fixture run (frames compared up to
+    each expected length)."""
+    want_lens = np.array(run["lens"], dtype=np.uint16)
+    want_res = np.array(run["results"], dtype=np.uint8)
+    bad_res = np.nonzero(np.asarray(res) != want_res)[0]
+    assert bad_res.size == 0, f"{what}: results differ at {bad_res[:8]} got {np.asarray(res)[bad_res[:8]]}"
+    bad_len = np.nonzero(np.asarray(lens) != want_lens)[0]
+    assert bad_len.size == 0, f"{what}: lengths differ at {bad_len[:8]}"
+    for i, (o, ln) in enumerate(zip(run["expect_offsets"], run["lens"])):
+        got = bytes(frames[i][:ln])
+        want = bytes(expect[o:o + ln])
+        if got != want:
+            k = next(j for j in range(ln) if got[j] != want[j])
+            raise AssertionError(f"{what}: frame {i} differs first at byte {k}: got {got[k:k+8].hex()} "
+                                 f"want {want[k:k+8].hex()}")
+    assert ip_end == run["ip_id_end"], (what, ip_end, run["ip_id_end"])

@@ -137,3 +137,43 @@ def test_dpdk_fill_known_answer(golden):
     assert got == kat and r == 0
     got, r = O.tx_frame(bytes(z), np.array([(0x08, 0, 0, 0, 0, 0, 0)], O.TX_OP_DTYPE)[0], 1)
     assert got == kat and r == 0
+
+
+# ---- the Build* half of row f2 -----------------------------------------------------------------
+def test_build_oracle_matches_fixtures():
+    """ora_tx_build_batch (C) == the Python restatement's fixtures, both runs (CheckSumEnable
+    true from iphId 0, false from 0xFFF0 across the wrap); the first frame is the canonical one."""
+    from tests.helpers import assert_build_equal, build_golden
+    from oracle import oracle as O
+
+    desc, payload, meta, expect = build_golden(ROOT)
+    mac = bytes.fromhex(meta["src_mac"])
+    for run in meta["runs"]:
+        frames, lens, res, end = O.tx_build_batch(desc, payload, mac, run["flags"], 1516, run["ip_id_start"])
+        assert_build_equal(frames, lens, res, end, run, expect, f"C oracle flags={run['flags']}")
+    assert set(meta["runs"][0]["results"]) == {0, 1, 2}
+
+
+def test_built_frames_parse_clean():
+    """Every Ethernet frame the Build* chain makes with CheckSumEnable passes the receive chain
+    (ParseEthFrm -> ParseIpv4Pkt -> ParseUdp/Tcp/IcmpPkt) with its fields intact: the transmit
+    and receive restatements agree on the same arithmetic."""
+    from tests.helpers import build_golden
+    from oracle import oracle as O
+
+    desc, payload, meta, expect = build_golden(ROOT)
+    run = meta["runs"][0]
+    netif = O.NetIf.make(mac="AA:AA:AA:AA:AA:AA", ip="192.168.100.100")
+    checked = 0
+    for i, d in enumerate(desc):
+        if run["results"][i] != 0 or d["mode"] != 0 or run["lens"][i] > 1514:
+            continue
+        o, ln = run["expect_offsets"][i], run["lens"][i]
+        r = O.rx_frame(bytes(expect[o:o + ln]), netif, 1)
+        assert r["status"] == 0, (i, int(r["status"]))
+        assert int(r["ip_proto"]) == int(d["proto"]) and int(r["src_ip"]) == int(d["src_ip"])
+        assert int(r["dst_ip"]) == int(d["dst_ip"])
+        if d["proto"] != 1:
+            assert (int(r["sport"]), int(r["dport"])) == (int(d["src_port"]), int(d["dst_port"]))
+        checked += 1
+    assert checked > 150
