@@ -92,6 +92,14 @@ TX_OP_DTYPE = np.dtype([("steps", "u1"), ("pad", "u1"), ("dst_port", "<u2"), ("d
 assert TX_OP_DTYPE.itemsize == 16
 TX_NAT_DST, TX_TTL, TX_NAT_SRC, TX_RECALC, TX_DPDK_FILL = 0x01, 0x02, 0x04, 0x08, 0x10
 TX_R_TTL_ALIVE, TX_R_SKIPPED, TX_R_OVERRUN = 0x01, 0x02, 0x04
+# halo_tx_build_desc_t (40 bytes): one locally originated packet for halo_tx_build_batch_device
+BUILD_DESC_DTYPE = np.dtype([("payload_off", "<u8"), ("payload_len", "<u2"), ("proto", "u1"), ("aux", "u1"),
+                             ("src_port", "<u2"), ("dst_port", "<u2"), ("src_ip", "<u4"), ("dst_ip", "<u4"),
+                             ("seq", "<u4"), ("ack", "<u4"), ("dst_mac", "u1", (6,)), ("mode", "u1"),
+                             ("pad", "u1")])
+assert BUILD_DESC_DTYPE.itemsize == 40
+TX_BUILD_ETH, TX_BUILD_LOOPBACK = 0, 1   # HALO_TX_BUILD_*
+TX_B_OK, TX_B_PAYLOAD_LEN, TX_B_PROTO, TX_B_SLOT = 0, 1, 2, 3
 FLOW_NAT_LAN, FLOW_NAT_WAN = 0, 1        # HALO_FLOW_*
 NAT_SYMMETRIC, NAT_FULL_CONE = 0, 1      # HALO_NAT_* (engine.NatTypeSymmetric / NatTypeFullCone)
 ROUTE_DTYPE = np.dtype([("dst_ip", "<u4"), ("network_mask", "<u4"), ("next_hop", "<u4"), ("netif", "<u4")])
@@ -217,6 +225,10 @@ _PROTOS = {
     "halo_rx_dispatch_compact": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_tx_fixup_batch_device": (ctypes.c_int, [
         _u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
+    "halo_tx_build_workspace": (ctypes.c_uint64, [ctypes.c_uint32]),
+    "halo_tx_build_batch_device": (ctypes.c_int, [
+        _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), ctypes.c_uint32, _u8p, ctypes.c_uint32,
+        _u8p, _u8p, _u8p, _u8p, ctypes.c_uint64, ctypes.c_void_p]),
     "halo_xxh3_64_batch_device": (ctypes.c_int, [_u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_rx_parse_flow_batch_device": (ctypes.c_int, [
         _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf), ctypes.c_uint32, _u8p, _u8p,

@@ -173,3 +173,51 @@ def tx_fixup_batch(frames, offsets_dw, lens, ops, *, check_sum_enable: bool = Tr
         HALO_RX_CSUM_ENABLE if check_sum_enable else 0, max_len_hint, _lib.ptr(result), _stream_handle(stream))
     _lib.check("halo_tx_fixup_batch_device", rc)
     return result
+
+
+# ---- transmit construction (the Build* half) ---------------------------------
+from ._lib import BUILD_DESC_DTYPE, TX_BUILD_ETH, TX_BUILD_LOOPBACK  # noqa: E402,F401
+
+
+class TxBuilder:
+    """Batched NetIf.TxUdp / TxTcp / TxIcmp -> TxIpv4 -> TxEthernet on the GPU
+    (halo_tx_build_batch_device). Owns the device workspace and the iphId counter
+    (protocol.iphId, protocol/ipv4.go:33), which advances by one per packet built, in order."""
+
+    def __init__(self, max_frames: int, device=None, ip_id: int = 0):
+        import torch
+
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        ws = int(_lib.lib.halo_tx_build_workspace(max_frames))
+        self.max_frames = max_frames
+        self.ws = torch.zeros(ws, dtype=torch.uint8, device=self.device)  # zeroed once; launches leave it so
+        self.ip_id = torch.tensor([ip_id & 0xFFFF], dtype=torch.int16, device=self.device)
+
+    def SetIpHeaderId(self, value: int) -> None:
+        """protocol.SetRandIpHeaderId's effect with a given value."""
+        self.ip_id.fill_(int(np.array(value & 0xFFFF, np.uint16).view(np.int16)))
+
+    @property
+    def iph_id(self) -> int:
+        return int(self.ip_id.cpu().numpy().view(np.uint16)[0])
+
+    def build(self, desc, payload, *, netif: NetIf, out_stride: int, frames=None, lens=None, result=None,
+              check_sum_enable: bool = True, max_payload_hint: int = 0, stream=None):
+        """desc: cuda uint8 tensor of n * 40 bytes (halo_tx_build_desc_t); payload: cuda uint8.
+        Returns (frames [n, out_stride] uint8, lens int16 [n], result uint8 [n]); asynchronous."""
+        import torch
+
+        n = desc.numel() // BUILD_DESC_DTYPE.itemsize
+        assert n <= self.max_frames
+        if frames is None:
+            frames = torch.zeros((n, out_stride), dtype=torch.uint8, device=desc.device)
+        if lens is None:
+            lens = torch.zeros(n, dtype=torch.int16, device=desc.device)
+        if result is None:
+            result = torch.zeros(n, dtype=torch.uint8, device=desc.device)
+        rc = _lib.lib.halo_tx_build_batch_device(
+            _lib.ptr(desc), n, _lib.ptr(payload), HALO_RX_CSUM_ENABLE if check_sum_enable else 0, netif,
+            max_payload_hint, _lib.ptr(frames), out_stride, _lib.ptr(lens), _lib.ptr(result), _lib.ptr(self.ip_id),
+            _lib.ptr(self.ws), self.ws.numel(), _stream_handle(stream))
+        _lib.check("halo_tx_build_batch_device", rc)
+        return frames, lens, result

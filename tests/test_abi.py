@@ -241,3 +241,42 @@ def test_host_registration_rules_before_any_hip_call():
     if not torch.cuda.is_available():
         assert L.halo_rx_host_register(base, 2 * P) == _lib.HALO_E_NODEV   # valid range, no device
         assert _lib.registered_count() == 0
+
+
+def test_tx_build_desc_layout_and_validation(tmp_path):
+    """halo_tx_build_desc_t matches BUILD_DESC_DTYPE (and the oracle's copy); the build entry
+    point validates before touching a device and has no CPU fallback."""
+    import torch
+
+    from halo_amd import _lib
+    from halo_amd._lib import BUILD_DESC_DTYPE
+    from oracle import oracle as O
+
+    assert O.BUILD_DESC_DTYPE == BUILD_DESC_DTYPE
+    fields = [f for f in BUILD_DESC_DTYPE.names if f != "dst_mac"] + ["dst_mac"]
+    src = tmp_path / "bdl.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "halo_rx.h"\nint main(void){\n'
+                   + "".join(f'printf("%zu\\n", offsetof(halo_tx_build_desc_t, {f}));\n' for f in fields)
+                   + 'printf("%zu\\n", sizeof(halo_tx_build_desc_t));\nreturn 0;}\n')
+    exe = tmp_path / "bdl"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals == [BUILD_DESC_DTYPE.fields[f][1] for f in fields] + [40]
+    L, n = _lib.lib, _lib.NetIf.make()
+    d = np.zeros(4, BUILD_DESC_DTYPE)
+    buf = np.zeros(4096, np.uint8)
+    ws = np.zeros(64, np.uint64)
+    ip = np.zeros(4, np.uint16)
+    lens = np.zeros(4, np.uint16)
+    wsb = int(L.halo_tx_build_workspace(4))
+    assert wsb == 16 and int(L.halo_tx_build_workspace(257)) == 24
+    args = lambda stride=64, flags=1, wsbytes=wsb: (d.ctypes.data, 4, buf.ctypes.data, flags, n, 0, buf.ctypes.data,  # noqa: E731
+                                                  stride, lens.ctypes.data, None, ip.ctypes.data, ws.ctypes.data,
+                                                  wsbytes, None)
+    assert L.halo_tx_build_batch_device(None, 0, None, 1, n, 0, None, 64, None, None, None, None, 0, None) == 0
+    assert L.halo_tx_build_batch_device(*args(stride=62)) == -1  # not a multiple of 4
+    assert L.halo_tx_build_batch_device(*args(stride=56)) == -1  # below the 60 B minimum frame
+    assert L.halo_tx_build_batch_device(*args(flags=2)) == -1    # only CSUM_ENABLE applies
+    assert L.halo_tx_build_batch_device(*args(wsbytes=8)) == -1  # workspace too small
+    if not torch.cuda.is_available():
+        assert L.halo_tx_build_batch_device(*args()) == _lib.HALO_E_NODEV
