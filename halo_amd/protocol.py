@@ -191,7 +191,7 @@ class TxBuilder:
         ws = int(_lib.lib.halo_tx_build_workspace(max_frames))
         self.max_frames = max_frames
         self.ws = torch.zeros(ws, dtype=torch.uint8, device=self.device)  # zeroed once; launches leave it so
-        self.ip_id = torch.tensor([ip_id & 0xFFFF], dtype=torch.int16, device=self.device)
+        self.ip_id = torch.from_numpy(np.array([ip_id & 0xFFFF], np.uint16).view(np.int16)).to(self.device)
 
     def SetIpHeaderId(self, value: int) -> None:
         """protocol.SetRandIpHeaderId's effect with a given value."""

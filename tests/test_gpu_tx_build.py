@@ -119,7 +119,9 @@ def test_build_slots_ids_and_two_launches(dev, oracle_lib):
         ids.append(f[r == TX_B_OK][:, 18].astype(np.int64) * 256 + f[r == TX_B_OK][:, 19])
         wf, wl, wr, we = oracle_lib.tx_build_batch(desc, payload, bytes.fromhex("020000000001"), 1, 64,
                                                    7 + launch * int((r == TX_B_OK).sum()))
-        assert np.array_equal(f[r == TX_B_OK], wf[r == TX_B_OK])
+        assert np.all(lens.cpu().numpy()[r == TX_B_OK] == 60)
+        assert np.array_equal(f[r == TX_B_OK][:, :60], wf[r == TX_B_OK][:, :60])
+        assert np.all(f[r == TX_B_OK][:, 60:] == 0xEE)  # slot bytes past the frame's last word untouched
     built = int((np.arange(n) % 7 != 3).sum())
     assert np.array_equal(ids[0], np.arange(8, 8 + built))
     assert np.array_equal(ids[1], np.arange(8 + built, 8 + 2 * built))
