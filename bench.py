@@ -316,6 +316,127 @@ def time_native(fn, *args, steps, warmup, d: Dist):
     return d.max(wall.value), region.value / steps
 
 
+def time_torch_loop(fn, steps: int, warmup: int, d: Dist):
+    """Launch fn() `steps` times back to back on torch's current stream (the stream the product
+    call is given) and time the region with one HIP event pair on that stream: (max-over-ranks
+    wall seconds, ms per launch)."""
+    import torch
+
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    d.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    d.barrier()
+    return d.max(wall), e0.elapsed_time(e1) / steps
+
+
+def tx_build_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
+    """§8f f2, the Build* half: NetIf.TxUdp -> TxIpv4 -> TxEthernet for a batch of descriptors
+    (halo_tx_build_batch_device): 1M 64 B UDP frames (22 B payloads, the headline's frame) and
+    256k 1514 B ones (1472 B payloads, the largest BuildUdpPkt accepts), CheckSumEnable on, the
+    iphId sequence carried across launches."""
+    import numpy as np
+    import torch
+
+    from halo_amd import protocol
+    from halo_amd._lib import BUILD_DESC_DTYPE, NetIf
+
+    res = {}
+    netif = NetIf.make(mac="02:00:00:00:00:01", ip="192.168.100.1")
+    for name, n, plen, stride in (("tx_build_udp_1M_64B", 1 << 20, 22, 64),
+                                  ("tx_build_udp_256k_1514B", 1 << 18, 1472, 1516)):
+        rng = np.random.default_rng(0x4255)
+        desc = np.zeros(n, BUILD_DESC_DTYPE)
+        desc["payload_off"] = np.arange(n, dtype=np.uint64) * plen
+        desc["payload_len"] = plen
+        desc["proto"] = 17
+        desc["src_port"] = rng.integers(1, 1 << 16, n)
+        desc["dst_port"] = rng.integers(1, 1 << 16, n)
+        desc["src_ip"] = netif.ip
+        desc["dst_ip"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+        desc["dst_mac"] = np.frombuffer(bytes.fromhex("aaaaaaaaaaaa"), np.uint8)
+        desc_d = torch.from_numpy(desc.view(np.uint8)).to(dev)
+        pay_d = torch.randint(0, 256, (n * plen,), dtype=torch.uint8, device=dev)
+        b = protocol.TxBuilder(n, device=dev, ip_id=1)
+        frames = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+        lens = torch.empty(n, dtype=torch.int16, device=dev)
+        rcode = torch.empty(n, dtype=torch.uint8, device=dev)
+        st = max(5, steps // 5) if plen > 64 else steps
+        w, k = time_torch_loop(lambda: b.build(desc_d, pay_d, netif=netif, out_stride=stride, frames=frames,
+                                               lens=lens, result=rcode, max_payload_hint=plen), st, warmup, d)
+        flen = 14 + 20 + 8 + plen
+        assert int((rcode != 0).sum()) == 0 and int((lens != flen).sum()) == 0
+        alg = n * (40 + plen + flen + 2 + 1)  # descriptor + payload in; frame + length + result out
+        res[name] = {"frames": n, "mpps": round(n * st / w / 1e6, 1), "gbit_s": round(n * flen * st * 8 / w / 1e9, 1),
+                     "kernel_ms": round(k, 5), "roofline": roofline(alg, k, load_traffic(name)),
+                     "alg_bytes_per_launch": alg,
+                     "what": "TxUdp -> BuildUdpPkt -> TxIpv4 (BuildIpv4Pkt, iphId) -> TxEthernet (BuildEthFrm)"}
+        if with_cpu:
+            from oracle import oracle as O
+
+            m = min(n, 1 << 16)
+            hd, hp = desc[:m].copy(), pay_d[:m * plen].cpu().numpy()
+            res[name]["cpu_baseline"] = cpu_rate(
+                lambda: O.tx_build_batch(hd, hp, bytes(netif.mac), 1, stride, 1), m, 2.0, "Mpps",
+                f"{m} descriptors of the same batch (oracle/halo_tx_oracle.c ora_tx_build_batch)")
+        del desc_d, pay_d, frames, lens, rcode, b
+        torch.cuda.empty_cache()
+    return res
+
+
+def lo_drain_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = False):
+    """§8a row a12: PacketHandle's LoChan drain over 1M TxIpv4 loopback copies (50 B IPv4/UDP
+    packets addressed to the NetIf itself), HALO_RX_L3_START, CheckSumEnable on."""
+    import numpy as np
+    import torch
+
+    from halo_amd import protocol
+    from halo_amd._lib import BUILD_DESC_DTYPE
+
+    n, plen = 1 << 20, 22
+    rng = np.random.default_rng(0x4C4F)
+    desc = np.zeros(n, BUILD_DESC_DTYPE)
+    desc["payload_off"] = np.arange(n, dtype=np.uint64) * plen
+    desc["payload_len"] = plen
+    desc["proto"] = 17
+    desc["src_port"] = rng.integers(1, 1 << 16, n)
+    desc["dst_port"] = rng.integers(1, 1 << 16, n)
+    desc["src_ip"] = desc["dst_ip"] = netif.ip
+    desc["mode"] = protocol.TX_BUILD_LOOPBACK
+    b = protocol.TxBuilder(n, device=dev)
+    pk, ln, _ = b.build(torch.from_numpy(desc.view(np.uint8)).to(dev),
+                        torch.randint(0, 256, (n * plen,), dtype=torch.uint8, device=dev), netif=netif,
+                        out_stride=64)  # 50 B packets in 64 B slots (out_stride >= 60)
+    offs = torch.arange(n, dtype=torch.int32, device=dev) * 16
+    out = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
+    w, k = time_torch_loop(lambda: protocol.parse_ipv4_packets_batch(pk.reshape(-1), offs, ln, netif=netif,
+                                                                     max_len_hint=64, out=out), steps, warmup, d)
+    recs = protocol.records(out)
+    assert np.all(recs["status"] == 0) and np.all(recs["flags"] & 4)
+    alg = n * (50 + 6 + RESULT_BYTES)
+    r = {"frames": n, "mpps": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 5),
+         "roofline": roofline(alg, k, load_traffic("lo_drain_1M_50B")), "alg_bytes_per_launch": alg,
+         "what": "LoChan drain: ParseIpv4Pkt -> own-address filter -> RxUdp verify (engine/engine.go:353-381)"}
+    if with_cpu:
+        from oracle import oracle as O
+
+        m = 1 << 18
+        host = pk.reshape(-1)[:m * 64].cpu().numpy()
+        hoffs = np.arange(m, dtype=np.uint32) * 16
+        hl = ln[:m].cpu().numpy().view(np.uint16)
+        r["cpu_baseline"] = cpu_rate(lambda: O.rx_batch(host, hl, O.NetIf.make(), 1 | 0x10, offsets_dw=hoffs), m, 2.0,
+                                     "Mpps", f"{m} packets of the batch (oracle/halo_rx_oracle.c, HALO_RX_L3_START)")
+    return r
+
+
 def flow_hash_secondary(batches, out_records, netif, steps, warmup, d: Dist, with_cpu: bool = False):
     """§8f f3 on the headline frames: parse each rotating batch once, then hash every record's NAT
     flow key (NatWanFlowHash, symmetric NAT) with the hashmap bucket for a 2^20-entry table."""
@@ -857,6 +978,9 @@ def main():
         sec["rx_flow_fused_config2_nat_wan"] = rx_flow_fused_secondary(
             batches, out, netif, args.steps, args.warmup, d, kern_ms, sec["flow_hash_config2_nat_wan"]["kernel_ms"])
         del batches
+        torch.cuda.empty_cache()
+        sec.update(tx_build_secondary(dev, args.steps, args.warmup, d, with_cpu=not args.no_cpu))
+        sec["lo_drain_1M_50B"] = lo_drain_secondary(dev, netif, args.steps, args.warmup, d, with_cpu=not args.no_cpu)
         torch.cuda.empty_cache()
         sec["xxh3_kcp_segments_1M"] = xxh3_secondary(dev, max(5, args.steps // 10), 2, d, with_cpu=not args.no_cpu)
         torch.cuda.empty_cache()

@@ -28,6 +28,7 @@ HALO_RX_CSUM_ENABLE = 0x1
 HALO_RX_JUMBO_EXT = 0x2
 HALO_RX_RECORD_COMPACT = 0x4
 HALO_RX_UNIFORM_LEN = 0x8
+HALO_RX_L3_START = 0x10  # LoChan packets: every buffer starts at its IPv4 header
 HALO_RX_VARIANT_SHIFT = 8
 # lanes per frame -> HALO_RX_VARIANT_* (0 = automatic, -1 = the size-class mix kernel)
 _VARIANT_CODE = {0: 0, 1: 1, 4: 2, 8: 3, 16: 4, -1: 5}
@@ -50,7 +51,7 @@ F_DST_IS_OWN = 0x04
 
 ACTION_NAMES = (
     "DROP_ETH", "IGNORE_MAC", "ARP", "IGNORE_TYPE", "DROP_IP", "BCAST_UDP", "DROP_BCAST_UDP",
-    "IGNORE_BCAST", "FORWARD", "LOCAL_ICMP", "LOCAL_UDP", "LOCAL_TCP", "DROP_L4",
+    "IGNORE_BCAST", "FORWARD", "LOCAL_ICMP", "LOCAL_UDP", "LOCAL_TCP", "DROP_L4", "LO_NOT_OWN",
 )
 ACTION = {name: code for code, name in enumerate(ACTION_NAMES)}
 HALO_RX_ACT_COUNT = len(ACTION_NAMES)
@@ -223,6 +224,7 @@ _PROTOS = {
     "halo_rx_host_registrations": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "halo_rx_dispatch": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_rx_dispatch_compact": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
+    "halo_rx_dispatch_loopback": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_tx_fixup_batch_device": (ctypes.c_int, [
         _u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_tx_build_workspace": (ctypes.c_uint64, [ctypes.c_uint32]),

@@ -207,6 +207,30 @@ extern "C" HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32
     return dispatch(results, n, netif, actions, action_hist);
 }
 
+extern "C" HALO_API int halo_rx_dispatch_loopback(const halo_rx_result_t* results, uint32_t n,
+                                                  const halo_rx_netif_t* netif, uint8_t* actions,
+                                                  uint32_t* action_hist) {
+    if (n && (!results || !netif || !actions)) return HALO_E_INVAL;
+    for (uint32_t i = 0; i < n; ++i) {
+        const halo_rx_result_t& r = results[i];
+        uint8_t a;
+        if (r.status >= HALO_RX_ETH_LEN && r.status <= HALO_RX_IP_TOTLEN_OVERRUN) {
+            a = HALO_RX_ACT_DROP_IP;                         // engine.go:362-365 (no Ethernet layer)
+        } else if (!(r.flags & HALO_RX_F_DST_IS_OWN)) {
+            a = HALO_RX_ACT_LO_NOT_OWN;                      // engine.go:366-368
+        } else if (r.status != HALO_RX_OK) {
+            a = HALO_RX_ACT_DROP_L4;                         // Rx{Icmp,Udp,Tcp} log and drop
+        } else {
+            a = r.ip_proto == halo::kIpIcmp ? HALO_RX_ACT_LOCAL_ICMP
+              : r.ip_proto == halo::kIpUdp  ? HALO_RX_ACT_LOCAL_UDP
+                                            : HALO_RX_ACT_LOCAL_TCP;  // engine.go:369-376
+        }
+        actions[i] = a;
+        if (action_hist) ++action_hist[a];
+    }
+    return HALO_OK;
+}
+
 extern "C" HALO_API int halo_rx_dispatch_compact(const halo_rx_record16_t* records, uint32_t n,
                                                  const halo_rx_netif_t* netif, uint8_t* actions,
                                                  uint32_t* action_hist) {
@@ -305,7 +329,8 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
     if (!bytes || !offsets || !lens || !out) return HALO_E_INVAL;
     if (flags & HALO_RX_RECORD_COMPACT) return HALO_E_INVAL;  // host path returns full records
     if (hipSetDevice(ctx->device) != hipSuccess) return HALO_E_NODEV;
-    const uint32_t cap = (flags & HALO_RX_JUMBO_EXT) ? halo::kEthMaxJumbo : halo::kEthMax;
+    const uint32_t cap = (flags & HALO_RX_L3_START) ? ((flags & HALO_RX_JUMBO_EXT) ? halo::kIpMaxJumbo : halo::kIpMax)
+                                                    : ((flags & HALO_RX_JUMBO_EXT) ? halo::kEthMaxJumbo : halo::kEthMax);
     int rc = HALO_OK;
     auto drain = [&](halo_rx_host_ctx::Slot& s) -> int {
         if (!s.busy) return HALO_OK;

@@ -49,14 +49,21 @@ __device__ __forceinline__ void store16(uint4* dst, uint4 v) {
 #endif
 }
 
-// Accumulate the L4-segment bytes [34, seg_end) held in dwords [d0, d0+4).
+// Byte offset of the IPv4 header in the buffer: 14 in an Ethernet frame, 0 for a LoChan packet
+// (HALO_RX_L3_START). Both are even, so every region stays on half-dword boundaries.
+template <bool L3>
+constexpr uint32_t kIpOff = L3 ? 0u : 14u;
+
+// Accumulate the L4-segment bytes [kIpOff + 20, seg_end) held in dwords [d0, d0+4).
+template <bool L3>
 __device__ __forceinline__ void acc_segment(const uint32_t (&w)[4], uint32_t d0, uint32_t seg_end, uint64_t& c) {
+    constexpr uint32_t kSeg = kIpOff<L3> + 20u;  // 34 (dword 8, high half) or 20 (dword 5)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t d = d0 + j;
         const int32_t rel = (int32_t)seg_end - (int32_t)(4u * d);  // segment bytes left in this dword
         uint32_t keep = rel >= 4 ? 0xFFFFFFFFu : (rel <= 0 ? 0u : ((1u << (rel * 8)) - 1u));
-        keep &= d >= 9 ? 0xFFFFFFFFu : (d == 8 ? 0xFFFF0000u : 0u);  // segment starts at byte 34
+        keep &= d >= (kSeg + 3u) / 4u ? 0xFFFFFFFFu : ((kSeg & 2u) && d == kSeg / 4u ? 0xFFFF0000u : 0u);
         c += (uint64_t)(w[j] & keep);
     }
 }
@@ -71,9 +78,21 @@ struct Verdict {
 
 #define HB(b) ((h[(b) >> 2] >> (((b)&3) * 8)) & 0xFFu)
 
-// Header checks, in reference order, up to (not including) the L4 checksum.
+// Frames failing ParseEthFrm's length check (or, for LoChan packets, ParseIpv4Pkt's) are never
+// read: the reference looks at no byte of them.
+template <bool L3>
+__device__ __forceinline__ bool len_readable(uint32_t L, uint32_t flags) {
+    const bool jumbo = (flags & HALO_RX_JUMBO_EXT) != 0;
+    if constexpr (L3) return L >= 20u && L <= (jumbo ? kIpMaxJumbo : kIpMax);
+    return L >= kEthMin && L <= (jumbo ? kEthMaxJumbo : kEthMax);
+}
+
+// Header checks, in reference order, up to (not including) the L4 checksum. h = buffer dwords
+// 0..11: an Ethernet frame (IPv4 header at byte 14) or, with L3, a LoChan packet (at byte 0).
+template <bool L3>
 __device__ __forceinline__ Verdict parse_header(const uint32_t (&h)[12], uint32_t L, bool present,
                                                 const RxParams& p) {
+    constexpr uint32_t O = kIpOff<L3>;
     Verdict v;
     v.status = HALO_RX_OK; v.flags = 0; v.ethertype = kEthUnknown; v.ip_proto = kIpUnknown;
     v.ip_total_len = 0; v.src_ip = 0; v.dst_ip = 0; v.sport = 0; v.dport = 0;
@@ -81,65 +100,75 @@ __device__ __forceinline__ Verdict parse_header(const uint32_t (&h)[12], uint32_
     v.seg_end = 0; v.l4_extra = 0; v.check_l4 = false;
     const bool jumbo = (p.flags & HALO_RX_JUMBO_EXT) != 0;
     const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
-    const uint32_t eth_max = jumbo ? kEthMaxJumbo : kEthMax;
     const uint32_t ip_max = jumbo ? kIpMaxJumbo : kIpMax;
     const uint32_t l4_max = jumbo ? kL4MaxJumbo : kL4Max;
 
-    // ---- ParseEthFrm (protocol/ethernet.go:29-55)
-    if (!present || L < kEthMin || L > eth_max) { v.status = HALO_RX_ETH_LEN; return v; }
-    const uint32_t et = bswap16(h[3] & 0xFFFFu);
-    if (et != kEthIeee8023 && et != kEthIpv4 && et != kEthArp && et != kEthIpv6) {
-        v.status = HALO_RX_ETH_TYPE; return v;
+    uint32_t iplen;
+    if constexpr (L3) {  // a LoChan packet: IPv4 only, no Ethernet layer (engine/engine.go:361)
+        v.ethertype = kEthIpv4;
+        iplen = L;
+    } else {
+        // ---- ParseEthFrm (protocol/ethernet.go:29-55)
+        const uint32_t eth_max = jumbo ? kEthMaxJumbo : kEthMax;
+        if (!present || L < kEthMin || L > eth_max) { v.status = HALO_RX_ETH_LEN; return v; }
+        const uint32_t et = bswap16(h[3] & 0xFFFFu);
+        if (et != kEthIeee8023 && et != kEthIpv4 && et != kEthArp && et != kEthIpv6) {
+            v.status = HALO_RX_ETH_TYPE; return v;
+        }
+        v.ethertype = et;
+        v.pay_off = 14; v.pay_len = L - 14;
+        // RxEthernet's filter (engine/ethernet_engine.go:22)
+        const uint32_t dm_lo = h[0], dm_hi = h[1] & 0xFFFFu;
+        if ((dm_lo == p.mac_lo && dm_hi == p.mac_hi) || (dm_lo == 0xFFFFFFFFu && dm_hi == 0xFFFFu))
+            v.flags |= HALO_RX_F_MAC_MATCH;
+        if (et != kEthIpv4) return v;
+        iplen = L - 14;
     }
-    v.ethertype = et;
-    v.pay_off = 14; v.pay_len = L - 14;
-    // RxEthernet's filter (engine/ethernet_engine.go:22)
-    const uint32_t dm_lo = h[0], dm_hi = h[1] & 0xFFFFu;
-    if ((dm_lo == p.mac_lo && dm_hi == p.mac_hi) || (dm_lo == 0xFFFFFFFFu && dm_hi == 0xFFFFu))
-        v.flags |= HALO_RX_F_MAC_MATCH;
-    if (et != kEthIpv4) return v;
 
-    // ---- ParseIpv4Pkt (protocol/ipv4.go:48-86) on pkt = frm[14:L]
-    const uint32_t iplen = L - 14;
-    if (iplen < 20 || iplen > ip_max) { v.status = HALO_RX_IP_LEN; return v; }
-    if (HB(14) != 0x45u) { v.status = HALO_RX_IP_VER; return v; }
-    if ((HB(20) != 0x40u && HB(20) != 0x00u) || HB(21) != 0x00u) { v.status = HALO_RX_IP_FRAG; return v; }
-    const uint32_t proto = HB(23);
+    // ---- ParseIpv4Pkt (protocol/ipv4.go:48-86) on pkt = frm[14:L] (or the LoChan packet)
+    if ((L3 && !present) || iplen < 20 || iplen > ip_max) { v.status = HALO_RX_IP_LEN; return v; }
+    if (HB(O + 0) != 0x45u) { v.status = HALO_RX_IP_VER; return v; }
+    if ((HB(O + 6) != 0x40u && HB(O + 6) != 0x00u) || HB(O + 7) != 0x00u) { v.status = HALO_RX_IP_FRAG; return v; }
+    const uint32_t proto = HB(O + 9);
     if (proto != kIpIcmp && proto != kIpTcp && proto != kIpUdp) { v.status = HALO_RX_IP_PROTO; return v; }
-    // pseudo-header src+dst (frame bytes 26..33), LE domain
-    const uint32_t sum_b = (h[6] >> 16) + hsum(h[7]) + (h[8] & 0xFFFFu);
+    // pseudo-header src+dst (IP bytes 12..19), LE domain; sum_a = the rest of the IP header
+    const uint32_t sum_b = L3 ? hsum(h[3]) + hsum(h[4]) : (h[6] >> 16) + hsum(h[7]) + (h[8] & 0xFFFFu);
     if (csum) {
-        const uint32_t sum_a = (h[3] >> 16) + hsum(h[4]) + hsum(h[5]) + (h[6] & 0xFFFFu);
+        const uint32_t sum_a = L3 ? hsum(h[0]) + hsum(h[1]) + hsum(h[2])
+                                  : (h[3] >> 16) + hsum(h[4]) + hsum(h[5]) + (h[6] & 0xFFFFu);
         if (fold16(sum_a + sum_b) != 0xFFFFu) { v.status = HALO_RX_IP_HDR_CKSUM; return v; }
     }
-    const uint32_t total_len = bswap16(h[4] & 0xFFFFu);
+    const uint32_t total_len = L3 ? bswap16(h[0] >> 16) : bswap16(h[4] & 0xFFFFu);
     // pkt[20:totalLen] (protocol/ipv4.go:84): Go panics below 20 and reads stale bytes or
     // panics past len(pkt); both are reported as build-defined statuses.
     if (total_len < 20) { v.status = HALO_RX_IP_TOTLEN_UNDERFLOW; return v; }
     if (total_len > iplen) { v.status = HALO_RX_IP_TOTLEN_OVERRUN; return v; }
     v.ip_proto = proto;
     v.ip_total_len = total_len;
-    v.src_ip = (HB(26) << 24) | (HB(27) << 16) | (HB(28) << 8) | HB(29);
-    v.dst_ip = (HB(30) << 24) | (HB(31) << 16) | (HB(32) << 8) | HB(33);
-    if (HB(33) == 255u) v.flags |= HALO_RX_F_IP_BCAST;
+    v.src_ip = (HB(O + 12) << 24) | (HB(O + 13) << 16) | (HB(O + 14) << 8) | HB(O + 15);
+    v.dst_ip = (HB(O + 16) << 24) | (HB(O + 17) << 16) | (HB(O + 18) << 8) | HB(O + 19);
+    if (HB(O + 19) == 255u) v.flags |= HALO_RX_F_IP_BCAST;
     if (v.dst_ip == p.own_ip) v.flags |= HALO_RX_F_DST_IS_OWN;
-    // NatGetSrcDstPort (protocol/ipv4.go:229-246) on the untrimmed packet (len >= 26 here)
-    if (proto == kIpIcmp) {
-        v.sport = v.dport = (HB(38) << 8) | HB(39);
+    // NatGetSrcDstPort (protocol/ipv4.go:229-246) on the untrimmed packet: (0, 0) below 26 B,
+    // which only a LoChan packet can be (an Ethernet frame's IPv4 part is >= 28 B)
+    if (L3 && iplen < 26) {
+        v.sport = v.dport = 0;
+    } else if (proto == kIpIcmp) {
+        v.sport = v.dport = (HB(O + 24) << 8) | HB(O + 25);
     } else {
-        v.sport = (HB(34) << 8) | HB(35);
-        v.dport = (HB(36) << 8) | HB(37);
+        v.sport = (HB(O + 20) << 8) | HB(O + 21);
+        v.dport = (HB(O + 22) << 8) | HB(O + 23);
     }
-    v.pay_off = 34; v.pay_len = total_len - 20;
+    v.pay_off = O + 20; v.pay_len = total_len - 20;
 
     // ---- L4 pre-checksum checks on pkt = ipPayload (len = totalLen - 20)
     const uint32_t l4len = total_len - 20;
-    const uint32_t seg_end = total_len + 14;
+    const uint32_t seg_end = total_len + O;
     if (proto == kIpUdp) {        // protocol/udp.go:21-49
         if (l4len < 8 || l4len > l4_max) { v.status = HALO_RX_L4_LEN; return v; }
         if (csum) {  // pseudo length = the UDP header's own length field (udp.go:30,38)
             v.check_l4 = true; v.seg_end = seg_end;
-            v.l4_extra = sum_b + 0x1100u + (h[9] >> 16);
+            v.l4_extra = sum_b + 0x1100u + (L3 ? h[6] & 0xFFFFu : h[9] >> 16);  // IP bytes 24..25
         }
     } else if (proto == kIpTcp) { // protocol/tcp.go:36-70
         if (l4len < 20 || l4len > l4_max) { v.status = HALO_RX_L4_LEN; return v; }
@@ -149,36 +178,43 @@ __device__ __forceinline__ Verdict parse_header(const uint32_t (&h)[12], uint32_
         }
     } else {                      // ICMP, protocol/icmp.go:33-63: checksum ALWAYS verified
         if (l4len < 8 || l4len > l4_max) { v.status = HALO_RX_L4_LEN; return v; }
-        const uint32_t type = HB(34);
+        const uint32_t type = HB(O + 20);
         if (type != kIcmpRequest && type != kIcmpReply && type != kIcmpTtl) { v.status = HALO_RX_ICMP_TYPE; return v; }
-        if (HB(35) != 0u) { v.status = HALO_RX_ICMP_CODE; return v; }
+        if (HB(O + 21) != 0u) { v.status = HALO_RX_ICMP_CODE; return v; }
         v.check_l4 = true; v.seg_end = seg_end; v.l4_extra = 0;
     }
     return v;
 }
 
 // L4 outputs once the whole chain succeeded.
+template <bool L3>
 __device__ __forceinline__ void finish_l4(const uint32_t (&h)[12], Verdict& v) {
+    constexpr uint32_t S = kIpOff<L3> + 20u;  // L4 segment start
     const uint32_t l4len = v.ip_total_len - 20;
     if (v.ip_proto == kIpUdp) {
-        v.pay_off = 42; v.pay_len = l4len - 8;                          // udp.go:47
+        v.pay_off = S + 8; v.pay_len = l4len - 8;                       // udp.go:47
     } else if (v.ip_proto == kIpTcp) {
-        v.l4_aux = HB(47);                                             // tcp.go:50
-        v.l4_seq = (HB(38) << 24) | (HB(39) << 16) | (HB(40) << 8) | HB(41);
-        v.l4_ack = (HB(42) << 24) | (HB(43) << 16) | (HB(44) << 8) | HB(45);
-        const uint32_t hl = HB(46) >> 4;                               // tcp.go:49 (words used as bytes)
-        v.pay_off = 34 + hl; v.pay_len = l4len - hl;                   // tcp.go:68
+        v.l4_aux = HB(S + 13);                                         // tcp.go:50
+        v.l4_seq = (HB(S + 4) << 24) | (HB(S + 5) << 16) | (HB(S + 6) << 8) | HB(S + 7);
+        v.l4_ack = (HB(S + 8) << 24) | (HB(S + 9) << 16) | (HB(S + 10) << 8) | HB(S + 11);
+        const uint32_t hl = HB(S + 12) >> 4;                           // tcp.go:49 (words used as bytes)
+        v.pay_off = S + hl; v.pay_len = l4len - hl;                    // tcp.go:68
     } else {
-        v.l4_aux = HB(34);                                             // icmp.go:38
-        v.l4_seq = (HB(38) << 24) | (HB(39) << 16) | (HB(40) << 8) | HB(41);
-        v.pay_off = 42; v.pay_len = l4len - 8;                          // icmp.go:62
+        v.l4_aux = HB(S);                                              // icmp.go:38
+        v.l4_seq = (HB(S + 4) << 24) | (HB(S + 5) << 16) | (HB(S + 6) << 8) | HB(S + 7);
+        v.pay_off = S + 8; v.pay_len = l4len - 8;                       // icmp.go:62
     }
 }
 #undef HB
 
+// LAYOUT 0: ragged (u32 dword offsets + u16 lengths); 1: strided with per-frame lengths;
+// 2: strided, one length; 3: ragged LoChan packets (HALO_RX_L3_START).
+template <int LAYOUT>
+constexpr bool kL3 = LAYOUT == 3;
+
 template <int LAYOUT>
 __device__ __forceinline__ void frame_at(const RxParams& p, uint64_t i, const uint8_t*& frame, uint32_t& L) {
-    if constexpr (LAYOUT == 0) {
+    if constexpr (LAYOUT == 0 || LAYOUT == 3) {
         frame = p.bytes + ((uint64_t)p.offsets_dw[i] << 2);
         L = p.lens[i];
     } else if constexpr (LAYOUT == 1) {
@@ -220,9 +256,7 @@ __device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool p
     st.frame = p.bytes;
     st.L = 0;
     if (present) frame_at<LAYOUT>(p, i, st.frame, st.L);
-    const uint32_t eth_max = (p.flags & HALO_RX_JUMBO_EXT) ? kEthMaxJumbo : kEthMax;
-    // frames failing the length check are never read (ParseEthFrm looks at no byte)
-    st.ndw = (present && st.L >= kEthMin && st.L <= eth_max) ? (st.L + 3) >> 2 : 0;
+    st.ndw = (present && len_readable<kL3<LAYOUT>>(st.L, p.flags)) ? (st.L + 3) >> 2 : 0;
 }
 
 // Round 0: four 16-byte chunks per lane issued back to back, bounded by the frame length (the
@@ -255,13 +289,13 @@ __device__ __forceinline__ void frame_header(const FrameState<G, R0>& st, uint32
 // FUSE (compile time, so the plain parse carries none of it): 1 = hash every record's NAT flow
 // key (halo_rx_parse_flow_batch_device), 2 = FindRoute of every record's dst
 // (halo_rx_parse_route_batch_device).
-template <int G, int FUSE = 0>
+template <int G, int FUSE = 0, bool L3 = false>
 __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool present, uint32_t gl,
                                             const uint32_t (&h)[12], Verdict& v, uint64_t c, Hist& hist,
                                             uint4* stage = nullptr) {
     const uint32_t c32 = group_sum<G>(fold64(c));
     if (v.status == HALO_RX_OK && v.check_l4 && fold16(c32 + v.l4_extra) != 0xFFFFu) v.status = HALO_RX_L4_CKSUM;
-    if (v.status == HALO_RX_OK && v.ip_proto != kIpUnknown) finish_l4(h, v);
+    if (v.status == HALO_RX_OK && v.ip_proto != kIpUnknown) finish_l4<L3>(h, v);
 
     if (present && gl < 2) {
         uint4 lo, hi;
@@ -320,7 +354,7 @@ __device__ __forceinline__ void frame_store(const RxParams& p, uint64_t i, bool 
 #ifndef HALO_RX_LATER_CHUNKS
 #define HALO_RX_LATER_CHUNKS 8
 #endif
-template <int G, int FUSE = 0, int U = HALO_RX_LATER_CHUNKS, int R0 = kRound0<G>>  // U: 16-byte chunks in flight per lane per later round
+template <int G, int FUSE = 0, int U = HALO_RX_LATER_CHUNKS, int R0 = kRound0<G>, bool L3 = false>  // U: 16-byte chunks in flight per lane per later round
 __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool present, uint32_t gl,
                                              uint32_t grp_base, FrameState<G, R0>& st, Hist& hist,
                                              uint4* stage = nullptr) {
@@ -328,23 +362,23 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
     constexpr int U0 = R0;            // chunks already loaded
     uint32_t h[12];
     frame_header(st, grp_base, h);
-    Verdict v = parse_header(h, st.L, present, p);
+    Verdict v = parse_header<L3>(h, st.L, present, p);
 
-    // L4 segment sum over [34, seg_end): round 0 from registers, then U chunks per round
+    // L4 segment sum over [kIpOff + 20, seg_end): round 0 from registers, then U chunks per round
     uint64_t c = 0;
     if (v.seg_end) {
 #pragma unroll
-        for (int u = 0; u < U0; ++u) acc_segment(st.buf[u], (u * G + gl) * 4, v.seg_end, c);
+        for (int u = 0; u < U0; ++u) acc_segment<L3>(st.buf[u], (u * G + gl) * 4, v.seg_end, c);
         const uint32_t seg_dw = (v.seg_end + 3) >> 2;
         for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
             uint32_t x[U][4];
 #pragma unroll
             for (int u = 0; u < U; ++u) load4(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc_segment(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
+            for (int u = 0; u < U; ++u) acc_segment<L3>(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
         }
     }
-    frame_store<G, FUSE>(p, i, present, gl, h, v, c, hist, stage);
+    frame_store<G, FUSE, L3>(p, i, present, gl, h, v, c, hist, stage);
 }
 
 // The whole chain for frame i on a group of G lanes.
@@ -354,7 +388,7 @@ __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, boo
     FrameState<G> st;
     frame_meta<LAYOUT>(p, i, present, st);
     frame_loads<G>(gl, st);
-    frame_finish<G, FUSE>(p, i, present, gl, grp_base, st, hist);
+    frame_finish<G, FUSE, HALO_RX_LATER_CHUNKS, kRound0<G>, kL3<LAYOUT>>(p, i, present, gl, grp_base, st, hist);
 }
 
 __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
@@ -418,7 +452,8 @@ rx_lane_kernel(const RxParams p) {
         FrameState<1> st;
         frame_meta<LAYOUT>(p, i, i < p.n, st);
         frame_loads<1>(0, st);
-        frame_finish<1, FUSE>(p, i, i < p.n, 0, lane, st, hist, &s_rec[w][compact ? lane : 2 * lane]);
+        frame_finish<1, FUSE, HALO_RX_LATER_CHUNKS, kRound0<1>, kL3<LAYOUT>>(p, i, i < p.n, 0, lane, st, hist,
+                                                                         &s_rec[w][compact ? lane : 2 * lane]);
         __builtin_amdgcn_wave_barrier();
         const uint32_t nrec = p.n - base < 64 ? p.n - base : 64;  // records of this wave
         if (compact) {
@@ -484,10 +519,10 @@ constexpr int kMixLater = !HALO_RX_MIX_LATER_SMALL ? HALO_RX_LATER_CHUNKS
 template <int G>
 constexpr int kMixRound0 = !HALO_RX_MIX_ROUND0 ? kRound0<G> : G == 4 ? 9 : G == 8 && HALO_RX_MIX_ROUND0 >= 2 ? 12 : kRound0<G>;
 
-template <int G, int FUSE>
+template <int G, int FUSE, bool L3>
 __device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, uint32_t e_end, uint32_t lane,
                                          const uint64_t* s_ptr, const uint32_t* s_idx, const uint16_t* s_len,
-                                         uint32_t eth_max, Hist& hist) {
+                                         uint32_t len_max, Hist& hist) {
     constexpr uint32_t FPW = 64 / G;
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp_base = lane & ~(uint32_t)(G - 1);
@@ -497,9 +532,9 @@ __device__ __forceinline__ void mix_pass(const RxParams& p, uint32_t e_begin, ui
         FrameState<G, kMixRound0<G>> st;
         st.frame = has ? reinterpret_cast<const uint8_t*>(s_ptr[e]) : p.bytes;
         st.L = has ? s_len[e] : 0u;
-        st.ndw = (has && st.L >= kEthMin && st.L <= eth_max) ? (st.L + 3) >> 2 : 0;
+        st.ndw = (has && st.L >= (L3 ? 20u : kEthMin) && st.L <= len_max) ? (st.L + 3) >> 2 : 0;
         frame_loads(gl, st);
-        frame_finish<G, FUSE, kMixLater<G>, kMixRound0<G>>(p, has ? s_idx[e] : 0u, has, gl, grp_base, st, hist);
+        frame_finish<G, FUSE, kMixLater<G>, kMixRound0<G>, L3>(p, has ? s_idx[e] : 0u, has, gl, grp_base, st, hist);
     }
 }
 
@@ -517,7 +552,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
     Hist hist{s_hist, 0};
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = threadIdx.x >> 6;
-    const uint32_t eth_max = (p.flags & HALO_RX_JUMBO_EXT) ? kEthMaxJumbo : kEthMax;
+    constexpr bool L3 = kL3<LAYOUT>;
+    const bool jumbo = (p.flags & HALO_RX_JUMBO_EXT) != 0;
+    const uint32_t len_max = L3 ? (jumbo ? kIpMaxJumbo : kIpMax) : (jumbo ? kEthMaxJumbo : kEthMax);
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t base = wave * kMixWindow; base < p.n; base += nwaves * kMixWindow) {
@@ -531,7 +568,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
             fl[k] = 0;
             if (i < p.n) frame_at<LAYOUT>(p, i, fp[k], fl[k]);
             cls[k] = i >= p.n ? 4u
-                   : (fl[k] <= 128 || fl[k] > eth_max) ? 0u
+                   : (fl[k] <= 128 || fl[k] > len_max) ? 0u
                    : fl[k] <= 1024 ? 1u : (HALO_RX_MIX_MAX_G < 16 || fl[k] <= 4096) ? 2u : 3u;
         }
         // counting sort by class: one ballot live at a time
@@ -561,11 +598,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
         }
         const uint32_t st0 = start[0], st1 = start[1], st2 = start[2], st3 = start[3], nall = start[4];
         __builtin_amdgcn_wave_barrier();
-        mix_pass<1, FUSE>(p, st0, st1, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
-        mix_pass<4, FUSE>(p, st1, st2, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
-        mix_pass<8, FUSE>(p, st2, st3, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+        mix_pass<1, FUSE, L3>(p, st0, st1, lane, s_ptr[w], s_idx[w], s_len[w], len_max, hist);
+        mix_pass<4, FUSE, L3>(p, st1, st2, lane, s_ptr[w], s_idx[w], s_len[w], len_max, hist);
+        mix_pass<8, FUSE, L3>(p, st2, st3, lane, s_ptr[w], s_idx[w], s_len[w], len_max, hist);
         if constexpr (HALO_RX_MIX_MAX_G >= 16)
-            mix_pass<16, FUSE>(p, st3, nall, lane, s_ptr[w], s_idx[w], s_len[w], eth_max, hist);
+            mix_pass<16, FUSE, L3>(p, st3, nall, lane, s_ptr[w], s_idx[w], s_len[w], len_max, hist);
         __builtin_amdgcn_wave_barrier();
     }
     flush_hist(p, hist);
@@ -630,6 +667,7 @@ int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, 
               : p.route_out ? launch_variant<0, 2>(p, v, s) : launch_variant<0, 0>(p, v, s);
             break;
         case 1: e = launch_variant<1>(p, v, s); break;
+        case 3: e = launch_variant<3>(p, v, s); break;  // LoChan packets: plain parse only
         default: e = launch_variant<2>(p, v, s); break;
     }
     return e == hipSuccess ? HALO_OK : HALO_E_HIP;
@@ -639,7 +677,7 @@ int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* 
                 halo_rx_result_t* d_out, uint32_t* d_hist) {
     if (!netif || !d_out) return HALO_E_INVAL;
     if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_RECORD_COMPACT | HALO_RX_UNIFORM_LEN |
-                  HALO_RX_VARIANT_MASK))
+                  HALO_RX_L3_START | HALO_RX_VARIANT_MASK))
         return HALO_E_INVAL;
     if (((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) > HALO_RX_VARIANT_MIX) return HALO_E_INVAL;
     if (reinterpret_cast<uintptr_t>(d_out) & 15u) return HALO_E_INVAL;
@@ -671,7 +709,8 @@ extern "C" HALO_API int halo_rx_parse_batch_device(const uint8_t* d_bytes, const
     p.bytes = d_bytes;
     p.offsets_dw = d_offsets_dw;
     p.lens = d_lens;
-    return halo::launch_parse(p, 0, max_len_hint, false, static_cast<hipStream_t>(stream));
+    return halo::launch_parse(p, (flags & HALO_RX_L3_START) ? 3 : 0, max_len_hint, false,
+                              static_cast<hipStream_t>(stream));
 }
 
 extern "C" HALO_API int halo_rx_parse_flow_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
@@ -686,6 +725,7 @@ extern "C" HALO_API int halo_rx_parse_flow_batch_device(const uint8_t* d_bytes, 
     halo::RxParams p{};
     int rc = halo::fill_common(p, n, flags, netif, d_out, d_status_hist);
     if (rc) return rc;
+    if (flags & HALO_RX_L3_START) return HALO_E_INVAL;  // LoChan packets: plain ragged parse only
     if (n == 0) return HALO_OK;
     if (!d_bytes || !d_offsets_dw || !d_lens) return HALO_E_INVAL;
     if ((rc = halo::check_device())) return rc;
@@ -711,6 +751,7 @@ extern "C" HALO_API int halo_rx_parse_route_batch_device(const uint8_t* d_bytes,
     halo::RxParams p{};
     int rc = halo::fill_common(p, n, flags, netif, d_out, d_status_hist);
     if (rc) return rc;
+    if (flags & HALO_RX_L3_START) return HALO_E_INVAL;  // LoChan packets: plain ragged parse only
     if (n == 0) return HALO_OK;
     if (!d_bytes || !d_offsets_dw || !d_lens) return HALO_E_INVAL;
     if ((rc = halo::check_device())) return rc;
@@ -733,6 +774,7 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
     halo::RxParams p{};
     int rc = halo::fill_common(p, n, flags, netif, d_out, d_status_hist);
     if (rc) return rc;
+    if (flags & HALO_RX_L3_START) return HALO_E_INVAL;  // LoChan packets: plain ragged parse only
     if (n == 0) return HALO_OK;
     if (!d_bytes || (stride & 3u) || (n > 1 && stride == 0)) return HALO_E_INVAL;
     if (!d_lens && n > 1 && len > stride) return HALO_E_INVAL;

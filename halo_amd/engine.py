@@ -8,10 +8,14 @@ and verifies the whole batch on the GPU through ``halo_rx_parse_batch_host`` (pi
 staging, double-buffered H2D -> kernel -> D2H), maps every record to the reference
 engine's decision with ``halo_rx_dispatch`` and invokes the registered UDP / TCP service
 handlers in frame order, with the same session and payload arguments as
-engine/udp_engine.go:16-20 and engine/tcp_engine.go:79-88.
+engine/udp_engine.go:16-20 and engine/tcp_engine.go:79-88. After each batch it drains the
+NetIf's ``LoChan`` (bare IPv4 packets: TxIpv4's loopback copies, Ipv4RouteForward's copies for
+another NetIf's address) the way PacketHandle does every 99 polls (engine/engine.go:353-381):
+one HALO_RX_L3_START batch parse, ``halo_rx_dispatch_loopback``, then the same handlers.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 from dataclasses import dataclass, field
 from typing import Callable, Optional
@@ -29,6 +33,15 @@ def dispatch(results: np.ndarray, netif: NetIfAbi) -> np.ndarray:
     actions = np.empty(results.shape[0], dtype=np.uint8)
     rc = _lib.lib.halo_rx_dispatch(_lib.ptr(results), results.shape[0], netif, _lib.ptr(actions), None)
     _lib.check("halo_rx_dispatch", rc)
+    return actions
+
+
+def dispatch_loopback(results: np.ndarray, netif: NetIfAbi) -> np.ndarray:
+    """PacketHandle's LoChan drain decision per record (halo_rx_dispatch_loopback)."""
+    results = np.ascontiguousarray(results).view(RESULT_DTYPE).reshape(-1)
+    actions = np.empty(results.shape[0], dtype=np.uint8)
+    rc = _lib.lib.halo_rx_dispatch_loopback(_lib.ptr(results), results.shape[0], netif, _lib.ptr(actions), None)
+    _lib.check("halo_rx_dispatch_loopback", rc)
     return actions
 
 
@@ -90,6 +103,7 @@ class NetIf:
     CheckSumEnable: bool = True  # protocol.CheckSumEnable for this interface's batches
     UdpServiceMap: dict = field(default_factory=dict)
     TcpServiceMap: dict = field(default_factory=dict)
+    LoChan: collections.deque = field(default_factory=collections.deque)  # NetIf.LoChan (engine/engine.go:106, cap 1024 :209)
     device: int = 0
 
     def __post_init__(self):
@@ -114,7 +128,8 @@ class NetIf:
             if f is None:
                 break
             frames.append(bytes(f))
-        if not frames:
+        if not frames:  # EthRxFunc returned nil every time: PacketHandle still drains LoChan
+            self.lo_drain()
             return np.empty(0, RESULT_DTYPE), np.empty(0, np.uint8)
         lens = np.fromiter((len(f) for f in frames), dtype=np.uint16, count=len(frames))
         offsets = np.zeros(len(frames), dtype=np.uint64)
@@ -124,10 +139,39 @@ class NetIf:
             self._batcher = HostBatcher(self.device)
         res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable))
         actions = dispatch(res, self.abi)
+        self._deliver(frames, res, actions)
+        self.lo_drain()
+        return res, actions
+
+    def lo_drain(self):
+        """PacketHandle's loopback drain (engine/engine.go:353-381) over everything queued in
+        LoChan: ParseIpv4Pkt, own-address filter, local RxIcmp / RxUdp / RxTcp — one GPU batch.
+        Returns (results, actions) for the packets drained."""
+        pkts = []
+        while self.LoChan:
+            pkts.append(bytes(self.LoChan.popleft()))
+        if not pkts:
+            return np.empty(0, RESULT_DTYPE), np.empty(0, np.uint8)
+        lens = np.fromiter((len(p) for p in pkts), dtype=np.uint16, count=len(pkts))
+        sizes = (lens.astype(np.uint64) + 3) & ~np.uint64(3)  # 4-byte aligned starts, like ring records
+        offsets = np.zeros(len(pkts), dtype=np.uint64)
+        np.cumsum(sizes[:-1], out=offsets[1:])
+        data = np.zeros(int(sizes.sum()) + 4, dtype=np.uint8)
+        for o, p in zip(offsets, pkts):
+            data[int(o):int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
+        if self._batcher is None:
+            self._batcher = HostBatcher(self.device)
+        res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable, l3_start=True))
+        actions = dispatch_loopback(res, self.abi)
+        self._deliver(pkts, res, actions)
+        return res, actions
+
+    def _deliver(self, bufs, res, actions):
+        """Invoke the UDP / TCP service handlers for the LOCAL_UDP / LOCAL_TCP records, in order."""
         np.add.at(self.action_counts, actions, 1)
         for i in np.nonzero((actions == ACTION["LOCAL_UDP"]) | (actions == ACTION["LOCAL_TCP"]))[0]:
             r = res[i]
-            payload = frames[i][int(r["payload_off"]):int(r["payload_off"]) + int(r["payload_len"])]
+            payload = bufs[i][int(r["payload_off"]):int(r["payload_off"]) + int(r["payload_len"])]
             if actions[i] == ACTION["LOCAL_UDP"]:
                 h = self.UdpServiceMap.get(int(r["dport"]))
                 if h is not None:
@@ -137,4 +181,3 @@ class NetIf:
                 if h is not None:
                     h(TcpSession(int(r["src_ip"]), int(r["sport"])), payload, int(r["l4_seq"]),
                       int(r["l4_ack"]), int(r["l4_aux"]))
-        return res, actions

@@ -63,11 +63,14 @@ ERROR_TEXT = {
 }
 
 
-def flags_word(check_sum_enable: bool = True, jumbo: bool = False, variant: int = 0, uniform_len: bool = False) -> int:
+def flags_word(check_sum_enable: bool = True, jumbo: bool = False, variant: int = 0, uniform_len: bool = False,
+               l3_start: bool = False) -> int:
     """The ABI ``flags`` word that replaces the ``CheckSumEnable`` package global (plus the
-    per-call kernel variant, lanes per frame with -1 = mix, and the uniform-length hint)."""
+    per-call kernel variant, lanes per frame with -1 = mix, the uniform-length hint and the
+    LoChan layout: buffers that start at their IPv4 header)."""
     return ((HALO_RX_CSUM_ENABLE if check_sum_enable else 0) | (HALO_RX_JUMBO_EXT if jumbo else 0)
-            | _lib.variant_flags(variant) | (_lib.HALO_RX_UNIFORM_LEN if uniform_len else 0))
+            | _lib.variant_flags(variant) | (_lib.HALO_RX_UNIFORM_LEN if uniform_len else 0)
+            | (_lib.HALO_RX_L3_START if l3_start else 0))
 
 
 def _stream_handle(stream):
@@ -85,14 +88,15 @@ def _check_out(out, n: int):
 
 def parse_frames_batch(frames, offsets_dw, lens, *, netif: NetIf, check_sum_enable: bool = True,
                        jumbo: bool = False, max_len_hint: int = 0, uniform_len: bool = False, variant: int = 0,
-                       out=None, hist=None, stream=None):
+                       out=None, hist=None, stream=None, l3_start: bool = False):
     """Parse + verify a ragged, device-resident batch (ParseEthFrm..ParseIcmpPkt per frame).
 
     frames: cuda uint8 tensor; offsets_dw: cuda int32 tensor (frame i at 4*offsets_dw[i]);
     lens: cuda int16 tensor (u16 lengths). Returns the cuda uint8 [n, 32] result tensor.
     ``hist`` (cuda int32[14]) is incremented per status. Asynchronous on ``stream``.
     ``uniform_len``: every frame is ``max_len_hint`` bytes; ``variant``: force lanes per frame
-    (1/4/8/16, -1 = mix) for this call — speed only, records are identical.
+    (1/4/8/16, -1 = mix) for this call — speed only, records are identical. ``l3_start``:
+    the buffers are LoChan packets starting at their IPv4 header (parse_ipv4_packets_batch).
     """
     import torch
 
@@ -102,10 +106,19 @@ def parse_frames_batch(frames, offsets_dw, lens, *, netif: NetIf, check_sum_enab
     _check_out(out, n)
     rc = _lib.lib.halo_rx_parse_batch_device(
         _lib.ptr(frames), _lib.ptr(offsets_dw), _lib.ptr(lens), n,
-        flags_word(check_sum_enable, jumbo, variant, uniform_len), netif, max_len_hint, _lib.ptr(out), _lib.ptr(hist),
+        flags_word(check_sum_enable, jumbo, variant, uniform_len, l3_start), netif, max_len_hint, _lib.ptr(out),
+        _lib.ptr(hist),
         _stream_handle(stream))
     _lib.check("halo_rx_parse_batch_device", rc)
     return out
+
+
+def parse_ipv4_packets_batch(packets, offsets_dw, lens, *, netif: NetIf, **kw):
+    """ParseIpv4Pkt + local L4 parse of a batch of LoChan packets (buffers that start at their
+    IPv4 header: engine/engine.go:353-381), HALO_RX_L3_START. Same arguments and record as
+    parse_frames_batch; map the records to the drain's decisions with
+    engine.dispatch_loopback."""
+    return parse_frames_batch(packets, offsets_dw, lens, netif=netif, l3_start=True, **kw)
 
 
 def parse_frames_strided(frames, stride: int, n: int, *, netif: NetIf, length: int = 0, lens=None,

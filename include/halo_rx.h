@@ -71,6 +71,19 @@ extern "C" {
                                     /* halo_rx_result_t (32 B); device entry points only     */
 #define HALO_RX_UNIFORM_LEN 0x8u    /* ragged batch whose frames all have length max_len_hint */
                                     /* (a speed hint: picks the uniform-length kernel table)  */
+/* Every buffer starts at its IPv4 header: the packets of a NetIf's LoChan, which
+ * PacketHandle drains every 99 polls through ParseIpv4Pkt -> own-address filter -> local
+ * Rx{Icmp,Udp,Tcp} (engine/engine.go:353-381; fed by TxIpv4's loopback copy,
+ * engine/ipv4_engine.go:72-79). The record is the one of the Ethernet chain minus its
+ * Ethernet layer: ParseIpv4Pkt's own length check (len<20 || len>1500, ipv4.go:49) is the
+ * first check and can fail (HALO_RX_IP_LEN); ethertype is 0x0800 (the channel carries IPv4
+ * only); MAC_MATCH is never set; payload_off is in packet coordinates (IPv4 payload at 20,
+ * UDP/ICMP payload at 28, TCP at 20 + headerLen) and 0/0 when ParseIpv4Pkt fails;
+ * NatGetSrcDstPort's ports are 0 for packets shorter than 26 B (ipv4.go:230). Map the records
+ * to the drain's decisions with halo_rx_dispatch_loopback. Ragged device and host entry
+ * points only (halo_rx_parse_batch_device / _host); not with the fused passes or strided
+ * layouts (HALO_E_INVAL).                                                                   */
+#define HALO_RX_L3_START 0x10u
 /* Per-call kernel variant (tuning and tests; results are identical for every value, only speed
  * changes): flags |= HALO_RX_VARIANT_x << HALO_RX_VARIANT_SHIFT. AUTO picks from max_len_hint /
  * the uniform length; LANE = one lane per frame; G4/G8/G16 = that many lanes per frame; MIX =
@@ -530,7 +543,9 @@ typedef enum halo_rx_action {
     HALO_RX_ACT_LOCAL_UDP = 10,    /* RxUdp OK -> UdpServiceMap                          */
     HALO_RX_ACT_LOCAL_TCP = 11,    /* RxTcp OK -> TcpServiceMap                          */
     HALO_RX_ACT_DROP_L4 = 12,      /* local L4 parse error: logged and dropped           */
-    HALO_RX_ACT_COUNT = 13
+    HALO_RX_ACT_LO_NOT_OWN = 13,   /* loopback drain: dst != NetIf.IpAddr, skipped       */
+                                   /* (engine/engine.go:367-369)                         */
+    HALO_RX_ACT_COUNT = 14
 } halo_rx_action_t;
 
 /* Host-side: maps n results to the action the reference engine takes (u8 per frame).
@@ -543,6 +558,14 @@ HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32_t n,
 HALO_API int halo_rx_dispatch_compact(const halo_rx_record16_t* records, uint32_t n,
                                       const halo_rx_netif_t* netif, uint8_t* actions,
                                       uint32_t* action_hist);
+/* PacketHandle's LoChan drain (engine/engine.go:353-381) over records parsed with
+ * HALO_RX_L3_START: ParseIpv4Pkt error -> DROP_IP (:362-365); dst != NetIf.IpAddr ->
+ * LO_NOT_OWN (:366-368); otherwise the local parse of ip_proto -> LOCAL_ICMP / LOCAL_UDP /
+ * LOCAL_TCP, or DROP_L4 when it failed (:369-376). No broadcast or NAT branch: the drain
+ * has none. */
+HALO_API int halo_rx_dispatch_loopback(const halo_rx_result_t* results, uint32_t n,
+                                       const halo_rx_netif_t* netif, uint8_t* actions,
+                                       uint32_t* action_hist);
 
 /* ---- synthetic traffic (bench + tests; SURVEY.md §8d generator) ----------------------
  * Every field of frame i is a pure function of (seed, i), so any shard of the global

@@ -16,6 +16,7 @@
  *   RxIpv4             engine/ipv4_engine.go:18-47
  *   RxUdp / RxUdpBroadcast engine/udp_engine.go:10-21, :35-44
  *   RxTcp              engine/tcp_engine.go:10-26   RxIcmp         engine/icmp_engine.go:12-23
+ *   PacketHandle's LoChan drain (HALO_RX_L3_START)   engine/engine.go:353-381
  *
  * Parity pinning: the reference is Go and no Go toolchain exists here or on the GPU box, so
  * the reference itself cannot run. GetCheckSum is pinned by the RFC 1071 §3 known answer and
@@ -212,15 +213,22 @@ ORA_API void ora_rx_frame(const uint8_t* frame, uint32_t len, uint32_t flags, co
     r->ip_proto = 0xff;
     const ora_cfg_t c = cfg_of(flags);
     slice_t frm = {frame, len}, eth_payload;
-    const uint8_t *dst_mac = NULL, *src_mac = NULL;
-    uint16_t eth_proto;
-    int st = parse_eth_frm(frm, &c, &eth_payload, &dst_mac, &src_mac, &eth_proto);
-    r->ethertype = eth_proto;
-    if (st) { r->status = (uint8_t)st; return; }
-    static const uint8_t bcast[6] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
-    if (memcmp(dst_mac, netif->mac, 6) == 0 || memcmp(dst_mac, bcast, 6) == 0) r->flags |= HALO_RX_F_MAC_MATCH;
-    set_payload(r, frame, eth_payload);
-    if (eth_proto != 0x0800) return;
+    int st;
+    if (flags & HALO_RX_L3_START) {
+        /* a LoChan packet (engine/engine.go:361): ParseIpv4Pkt straight on the buffer */
+        r->ethertype = 0x0800;
+        eth_payload = frm;
+    } else {
+        const uint8_t *dst_mac = NULL, *src_mac = NULL;
+        uint16_t eth_proto;
+        st = parse_eth_frm(frm, &c, &eth_payload, &dst_mac, &src_mac, &eth_proto);
+        r->ethertype = eth_proto;
+        if (st) { r->status = (uint8_t)st; return; }
+        static const uint8_t bcast[6] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+        if (memcmp(dst_mac, netif->mac, 6) == 0 || memcmp(dst_mac, bcast, 6) == 0) r->flags |= HALO_RX_F_MAC_MATCH;
+        set_payload(r, frame, eth_payload);
+        if (eth_proto != 0x0800) return;
+    }
 
     slice_t ip_payload;
     uint8_t proto;
@@ -300,6 +308,36 @@ ORA_API int ora_engine_rx(const uint8_t* frame, uint32_t len, uint32_t flags, co
                                                                                        : HALO_RX_ACT_LOCAL_TCP;
 }
 
+/* engine/engine.go:353-381: PacketHandle's LoChan drain for one packet (HALO_RX_L3_START). */
+ORA_API int ora_engine_lo(const uint8_t* pkt, uint32_t len, uint32_t flags, const halo_rx_netif_t* netif) {
+    const ora_cfg_t c = cfg_of(flags);
+    slice_t ipv4_pkt = {pkt, len}, ip_payload, l4;
+    uint8_t proto;
+    const uint8_t *src, *dst;
+    uint16_t total_len;
+    if (parse_ipv4_pkt(ipv4_pkt, &c, &ip_payload, &proto, &src, &dst, &total_len)) return HALO_RX_ACT_DROP_IP;
+    uint8_t own_ip[4] = {(uint8_t)(netif->ip >> 24), (uint8_t)(netif->ip >> 16), (uint8_t)(netif->ip >> 8),
+                         (uint8_t)netif->ip};
+    if (memcmp(dst, own_ip, 4) != 0) return HALO_RX_ACT_LO_NOT_OWN; /* :366-368 */
+    uint16_t sp, dp;
+    switch (proto) { /* :369-376 -> RxIcmp / RxUdp / RxTcp with the NetIf address as pseudo dst */
+        case 0x01: {
+            uint8_t t;
+            uint16_t id, sq;
+            return parse_icmp_pkt(ip_payload, &c, &l4, &t, &id, &sq) ? HALO_RX_ACT_DROP_L4 : HALO_RX_ACT_LOCAL_ICMP;
+        }
+        case 0x11:
+            return parse_udp_pkt(ip_payload, src, own_ip, &c, &l4, &sp, &dp) ? HALO_RX_ACT_DROP_L4
+                                                                              : HALO_RX_ACT_LOCAL_UDP;
+        default: {
+            uint32_t seq, ack;
+            uint8_t fl;
+            return parse_tcp_pkt(ip_payload, src, own_ip, &c, &l4, &sp, &dp, &seq, &ack, &fl) ? HALO_RX_ACT_DROP_L4
+                                                                                           : HALO_RX_ACT_LOCAL_TCP;
+        }
+    }
+}
+
 /* ---- batches (ragged dword offsets, or strided when offsets_dw == NULL) ---------------- */
 typedef struct {
     const uint8_t* bytes;
@@ -363,7 +401,9 @@ ORA_API void ora_engine_batch(const uint8_t* bytes, const uint32_t* offsets_dw, 
                               const halo_rx_netif_t* netif, uint8_t* actions) {
     for (uint64_t i = 0; i < n; ++i) {
         const uint8_t* f = offsets_dw ? bytes + ((uint64_t)offsets_dw[i] << 2) : bytes + i * stride;
-        actions[i] = (uint8_t)ora_engine_rx(f, lens ? lens[i] : len, flags, netif);
+        const uint32_t L = lens ? lens[i] : len;
+        actions[i] = (uint8_t)((flags & HALO_RX_L3_START) ? ora_engine_lo(f, L, flags, netif)
+                                                            : ora_engine_rx(f, L, flags, netif));
     }
 }
 

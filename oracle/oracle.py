@@ -48,6 +48,10 @@ def build(force: bool = False) -> str:
                                             "halo_route_oracle.c", "halo_ring_oracle.c")]
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, srcs)):
         subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
+    if os.path.exists("/root/reference/cgo/ring_buffer.h"):
+        # the reference's own C ring, compiled from where it lies (build container only; the
+        # GPU box has no /root/reference and uses the prebuilt oracle/_ref files if any)
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
     return LIB_PATH
 
 
@@ -69,6 +73,8 @@ def lib() -> ctypes.CDLL:
         L.ora_engine_rx.argtypes = [vp, u32, u32, ctypes.POINTER(NetIf)]
         L.ora_rx_batch.restype = ctypes.c_int
         L.ora_rx_batch.argtypes = [vp, vp, vp, u64, u32, u32, u32, ctypes.POINTER(NetIf), vp, vp, ctypes.c_int]
+        L.ora_engine_lo.restype = ctypes.c_int
+        L.ora_engine_lo.argtypes = [vp, u32, u32, ctypes.POINTER(NetIf)]
         L.ora_engine_batch.restype = None
         L.ora_engine_batch.argtypes = [vp, vp, vp, u64, u32, u32, u32, ctypes.POINTER(NetIf), vp]
         L.ora_synth_kind.restype = None
@@ -139,6 +145,12 @@ def rx_frame(frame: bytes, netif: NetIf, flags: int = 1) -> np.ndarray:
 def engine_rx(frame: bytes, netif: NetIf, flags: int = 1) -> int:
     b = np.frombuffer(bytes(frame) + b"\0", dtype=np.uint8)
     return lib().ora_engine_rx(_p(b), len(frame), flags, netif)
+
+
+def engine_lo(packet: bytes, netif: NetIf, flags: int = 1) -> int:
+    """PacketHandle's LoChan drain decision for one packet (ora_engine_lo)."""
+    b = np.frombuffer(bytes(packet) + b"\0", dtype=np.uint8)
+    return lib().ora_engine_lo(_p(b), len(packet), flags, netif)
 
 
 def rx_batch(data: np.ndarray, lens: np.ndarray, netif: NetIf, flags: int = 1, offsets_dw=None, stride: int = 0,

@@ -14,13 +14,14 @@ Go slices are Python bytes; a Go `error` is returned as a status name.
   parse_icmp_pkt      protocol/icmp.go:33-63
   nat_get_src_dst_port protocol/ipv4.go:229-246
   rx_ethernet/rx_ipv4 engine/ethernet_engine.go:13-31, engine/ipv4_engine.go:18-47
+  rx_lo_packet/engine_lo  PacketHandle's LoChan drain, engine/engine.go:353-381
 """
 from __future__ import annotations
 
 STATUS = ["OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_PROTO", "IP_HDR_CKSUM",
           "IP_TOTLEN_UNDERFLOW", "IP_TOTLEN_OVERRUN", "L4_LEN", "ICMP_TYPE", "ICMP_CODE", "L4_CKSUM"]
 ACTIONS = ["DROP_ETH", "IGNORE_MAC", "ARP", "IGNORE_TYPE", "DROP_IP", "BCAST_UDP", "DROP_BCAST_UDP",
-           "IGNORE_BCAST", "FORWARD", "LOCAL_ICMP", "LOCAL_UDP", "LOCAL_TCP", "DROP_L4"]
+           "IGNORE_BCAST", "FORWARD", "LOCAL_ICMP", "LOCAL_UDP", "LOCAL_TCP", "DROP_L4", "LO_NOT_OWN"]
 
 
 class Cfg:
@@ -206,6 +207,60 @@ def engine_rx(frame: bytes, mac: bytes, own_ip: int, nat_enable=False, check_sum
     if proto == 0x01:
         return "DROP_L4" if parse_icmp_pkt(ip_payload, c)[4] else "LOCAL_ICMP"
     if proto == 0x11:
+        return "DROP_L4" if parse_udp_pkt(ip_payload, src, own, c)[3] else "LOCAL_UDP"
+    return "DROP_L4" if parse_tcp_pkt(ip_payload, src, own, c)[6] else "LOCAL_TCP"
+
+
+def rx_lo_packet(pkt: bytes, own_ip: int, check_sum_enable=True, jumbo=False) -> dict:
+    """The record for one LoChan packet (HALO_RX_L3_START, include/halo_rx.h): the chain of
+    rx_frame without its Ethernet layer. engine/engine.go:361 hands the packet straight to
+    ParseIpv4Pkt; the channel carries IPv4 only, so the record's EtherType is 0x0800."""
+    c = Cfg(check_sum_enable, jumbo)
+    r = dict(status="OK", flags=0, ethertype=0x0800, ip_proto=0xFF, l4_aux=0, ip_total_len=0, src_ip=0, dst_ip=0,
+             sport=0, dport=0, payload_off=0, payload_len=0, l4_seq=0, l4_ack=0)
+    ip_payload, proto, src, dst, total_len, err = parse_ipv4_pkt(pkt, c)
+    if err:
+        r["status"] = err
+        return r
+    r.update(ip_proto=proto, ip_total_len=total_len, src_ip=ip_addr_to_u(src), dst_ip=ip_addr_to_u(dst))
+    if dst[3] == 255:
+        r["flags"] |= 2
+    if r["dst_ip"] == own_ip:
+        r["flags"] |= 4
+    r["sport"], r["dport"] = nat_get_src_dst_port(pkt)
+    r["payload_off"], r["payload_len"] = 20, len(ip_payload)
+    if proto == 0x11:
+        pay, _sp, _dp, err = parse_udp_pkt(ip_payload, src, dst, c)
+        off = 8
+    elif proto == 0x06:
+        pay, _sp, _dp, seq, ack, fl, err = parse_tcp_pkt(ip_payload, src, dst, c)
+        if not err:
+            r.update(l4_aux=fl, l4_seq=seq, l4_ack=ack)
+        off = None if err else ip_payload[12] >> 4
+    else:
+        pay, typ, icmp_id, icmp_seq, err = parse_icmp_pkt(ip_payload, c)
+        if not err:
+            r.update(l4_aux=typ, l4_seq=(be16(icmp_id) << 16) | icmp_seq)
+        off = 8
+    if err:
+        r["status"] = err
+        return r
+    r["payload_off"], r["payload_len"] = 20 + off, len(pay)
+    return r
+
+
+def engine_lo(pkt: bytes, own_ip: int, check_sum_enable=True, jumbo=False) -> str:
+    """What PacketHandle's LoChan drain does with one packet (engine/engine.go:360-377)."""
+    c = Cfg(check_sum_enable, jumbo)
+    ip_payload, proto, src, dst, _tl, err = parse_ipv4_pkt(pkt, c)
+    if err:
+        return "DROP_IP"  # logged, continue
+    own = own_ip.to_bytes(4, "big")
+    if dst != own:
+        return "LO_NOT_OWN"  # bytes.Equal(ipv4DstAddr, i.IpAddr) fails: continue
+    if proto == 0x01:  # i.RxIcmp
+        return "DROP_L4" if parse_icmp_pkt(ip_payload, c)[4] else "LOCAL_ICMP"
+    if proto == 0x11:  # i.RxUdp: pseudo dst = i.IpAddr (udp_engine.go:11)
         return "DROP_L4" if parse_udp_pkt(ip_payload, src, own, c)[3] else "LOCAL_UDP"
     return "DROP_L4" if parse_tcp_pkt(ip_payload, src, own, c)[6] else "LOCAL_TCP"
 

@@ -9,23 +9,51 @@ STATUS_NAMES = ["OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_
                 "IP_TOTLEN_UNDERFLOW", "IP_TOTLEN_OVERRUN", "L4_LEN", "ICMP_TYPE", "ICMP_CODE", "L4_CKSUM"]
 
 
-def golden_arrays(meta, blob):
-    """(data, offsets_dw, lens, names) for the golden frames (4-byte aligned, ragged)."""
-    fr = meta["frames"]
+def golden_arrays(meta, blob, key="frames"):
+    """(data, offsets_dw, lens, names) for the golden frames (4-byte aligned, ragged); key
+    "packets" for the LoChan fixtures (lo_golden)."""
+    fr = meta[key]
     offs = np.array([e["offset"] for e in fr], dtype=np.uint64)
     assert np.all(offs % 4 == 0)
     lens = np.array([e["len"] for e in fr], dtype=np.uint16)
     return blob, (offs // 4).astype(np.uint32), lens, [e["name"] for e in fr]
 
 
-def expected_records(meta, flags: int, dtype) -> np.ndarray:
-    fr = meta["frames"]
+def expected_records(meta, flags: int, dtype, key="frames") -> np.ndarray:
+    fr = meta[key]
     out = np.zeros(len(fr), dtype=dtype)
     for i, e in enumerate(fr):
         r = e["expect"][str(flags)]
         for f in FIELDS:
             out[i][f] = r[f]
     return out
+
+
+def lo_golden(root):
+    """The LoChan packet fixtures (tests/gen_golden_lo.py): (meta, blob); entries under "packets"."""
+    import json
+    import os
+
+    g = os.path.join(root, "tests", "golden")
+    with open(os.path.join(g, "lo_packets.json")) as fh:
+        meta = json.load(fh)
+    return meta, np.fromfile(os.path.join(g, "lo_packets.bin"), dtype=np.uint8)
+
+
+def strip_ethernet(data: np.ndarray, offsets_dw: np.ndarray, lens: np.ndarray):
+    """Frames -> their Ethernet payloads (what Ipv4RouteForward puts in LoChan,
+    engine/ipv4_engine.go:195-200), repacked at 4-byte-aligned starts: (data, offsets_dw, lens).
+    Frames shorter than 14 bytes become empty packets."""
+    plens = np.maximum(lens.astype(np.int64) - 14, 0)
+    sizes = (plens + 3) & ~3
+    offs = np.zeros(len(lens), dtype=np.int64)
+    if len(lens):
+        offs[1:] = np.cumsum(sizes)[:-1]
+    out = np.zeros(int(sizes.sum()) + 16, dtype=np.uint8)
+    for i in range(len(lens)):
+        src = int(offsets_dw[i]) * 4 + 14
+        out[offs[i]:offs[i] + plens[i]] = data[src:src + plens[i]]
+    return out, (offs // 4).astype(np.uint32), plens.astype(np.uint16)
 
 
 def assert_records_equal(got: np.ndarray, want: np.ndarray, names=None, what=""):

@@ -73,7 +73,7 @@ def test_argument_validation_without_gpu():
     assert L.halo_rx_parse_batch_device(None, None, None, 0, 1, n, 0, out.ctypes.data, None, None) == 0
     assert L.halo_rx_parse_batch_device(None, None, None, 0, 1, None, 0, out.ctypes.data, None, None) == -1
     assert L.halo_rx_parse_batch_device(None, None, None, 1, 1, n, 0, out.ctypes.data, None, None) == -1
-    assert L.halo_rx_parse_batch_device(buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 1, 0x10, n, 0,
+    assert L.halo_rx_parse_batch_device(buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 1, 0x20, n, 0,
                                         out.ctypes.data, None, None) == -1  # unknown flag bit
     assert L.halo_rx_parse_batch_device(buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 1, 1, n, 0,
                                         out.ctypes.data + 4, None, None) == -1  # misaligned output

@@ -20,7 +20,8 @@ step() {
 }
 for s in "$@"; do
   case $s in
-    test)  step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
+    test)  step pytest_gpu 1200 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
+    tlo)   step pytest_lo 600 python -u -m pytest tests/test_gpu_loopback.py tests/test_gpu_tx_build.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     ttx)   step pytest_tx 600 python -m pytest tests/test_gpu_tx.py -m gpu -q -rf -x ;;
     thash) step pytest_hash 600 python -m pytest tests/test_gpu_flow_hash.py -m gpu -q -rf -x ;;
     troute) step pytest_route 600 python -m pytest tests/test_gpu_route.py -m gpu -q -rf -x ;;
