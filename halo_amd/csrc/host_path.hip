@@ -301,7 +301,7 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
         ok = ok && hipMalloc((void**)&s.d_len, 2ull * chunk_frames) == hipSuccess;
         ok = ok && hipMalloc((void**)&s.d_res, sizeof(halo_rx_result_t) * chunk_frames) == hipSuccess;
         ok = ok && hipMalloc((void**)&s.d_hist, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
-        ok = ok && hipMemset(s.d_hist, 0, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
+        ok = ok && hipMemsetAsync(s.d_hist, 0, 4 * HALO_RX_STATUS_COUNT, s.stream) == hipSuccess;  // before its parses
     }
     if (!ok) {
         free_ctx(c);
@@ -405,8 +405,11 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
     if (rc == HALO_OK && status_hist) {
         for (auto& s : ctx->slot) {
             uint32_t h[HALO_RX_STATUS_COUNT];
-            if (hipMemcpy(h, s.d_hist, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemset(s.d_hist, 0, sizeof h) != hipSuccess)
+            // on the slot's own (non-blocking) stream: a null-stream hipMemset is not ordered
+            // before the next call's launches there, and could zero counts they already added
+            if (hipMemcpyAsync(h, s.d_hist, sizeof h, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+                hipMemsetAsync(s.d_hist, 0, sizeof h, s.stream) != hipSuccess ||
+                hipStreamSynchronize(s.stream) != hipSuccess)
                 return HALO_E_HIP;
             for (int j = 0; j < HALO_RX_STATUS_COUNT; ++j) status_hist[j] += h[j];
         }

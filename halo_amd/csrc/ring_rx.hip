@@ -751,7 +751,8 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     ok = ok && hipMalloc((void**)&r->d_len, 2ull * max_frames) == hipSuccess;
     ok = ok && hipMalloc((void**)&r->d_res, sizeof(halo_rx_result_t) * (uint64_t)max_frames) == hipSuccess;
     ok = ok && hipMalloc((void**)&r->d_hist, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
-    ok = ok && hipMemset(r->d_hist, 0, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
+    ok = ok && hipMemset(r->d_hist, 0, 4 * HALO_RX_STATUS_COUNT) == hipSuccess &&
+         hipDeviceSynchronize() == hipSuccess;  // complete before any non-blocking stream counts into it
     ok = ok && hipMalloc((void**)&r->d_info, sizeof(halo_rx_ring_scan_t)) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&r->h_info, sizeof(halo_rx_ring_scan_t), hipHostMallocDefault) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&r->h_off, 4ull * max_frames, hipHostMallocDefault) == hipSuccess;
@@ -872,8 +873,11 @@ extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, con
     }
     if (status_hist && done) {
         uint32_t h[HALO_RX_STATUS_COUNT];
-        if (hipMemcpy(h, r->d_hist, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMemset(r->d_hist, 0, sizeof h) != hipSuccess)
+        // on the stream the parses ran on: hipMemset / hipMemcpy go to the null stream, which a
+        // non-blocking stream does not wait for (a reset could land after the next poll's counts)
+        if (hipMemcpyAsync(h, r->d_hist, sizeof h, hipMemcpyDeviceToHost, r->s_comp) != hipSuccess ||
+            hipMemsetAsync(r->d_hist, 0, sizeof h, r->s_comp) != hipSuccess ||
+            hipStreamSynchronize(r->s_comp) != hipSuccess)
             return HALO_E_HIP;
         for (int j = 0; j < HALO_RX_STATUS_COUNT; ++j) status_hist[j] += h[j];
     }
