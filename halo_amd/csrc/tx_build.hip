@@ -9,19 +9,31 @@
 //    -> NetIf.TxEthernet                engine/ethernet_engine.go:34-50
 //       protocol.BuildEthFrm            protocol/ethernet.go:58-82 (zero pad to 60 B)
 //
-// Shape. Blocks take 256-descriptor tiles in order from a ticket counter. Per tile: the
-// descriptors are staged in LDS with coalesced 8-byte loads; each thread decides its frame
-// (Build* length limits, slot size) and a block scan plus a decoupled look-back over the tiles
-// before it gives every built frame its place in the iphId sequence (BuildIpv4Pkt increments the
-// process-global counter once per packet that reaches it, so frame k of the batch carries
-// base + k). Then G lanes per frame write it: lane j of the group produces 16-byte output chunks
-// j, j+G, ..., each dword = header bytes (kept in registers, from the descriptor) | payload bytes
-// (two aligned source loads merged with v_alignbyte: the payload may start at any byte) |
-// zero padding. The L4 checksum is summed over the output dwords as they are produced (little-
-// endian domain, as rx_parse.hip: the L4 segment starts at an even frame offset), reduced over
-// the group with DPP, and patched into the header chunks, which are stored last. HBM-bound: each
-// payload byte is read once and each frame byte written once.
+// iphId. BuildIpv4Pkt increments the process-global counter once per packet that reaches it, so
+// the k-th built frame of the batch carries base + k. A descriptor that Build* rejects is rare
+// (a caller error), so frame i is built with base + 1 + i - (rejected descriptors before it in
+// its own 64-descriptor tile) — everything its wave knows — and the rejections in earlier tiles
+// are settled afterwards: a one-block launch checks the per-tile rejection counts (writing the
+// new iphId) and, only when there were any, a third launch patches the identification and header
+// checksum of the frames behind them (RFC 1624). No atomics and no inter-block waiting anywhere:
+// a ticketed single pass with a decoupled look-back measured 175 us for 1M 64 B frames (its
+// ticket atomics serialise at ~25 ns each: 4096 tickets alone cost 100 us).
+//
+// Build. Each wave owns 64-descriptor tiles (grid-stride): lane i loads descriptor i, decides it
+// (Build* length limits, slot size), ranks the rejections with a ballot and writes its frame's
+// header dwords 0..15 (Ethernet layout, or the loopback packet's) to the wave's LDS region. Then
+// G lanes per frame (64 / G frames at a time) produce 16-byte output chunks j, j+G, ..., U per
+// memory round trip, each dword = header bytes | payload bytes (two aligned source loads merged
+// with v_alignbyte: the payload may start at any byte) | zero padding. The L4 checksum is summed
+// over the output dwords as they are produced (v_dot2_u32_u16 of each dword's halves: the
+// one's-complement sum in the little-endian domain, as rx_parse.hip; the L4 segment starts at an
+// even frame offset), reduced over the group with DPP, and patched into the header chunks, which
+// are stored last. Chunks wholly inside the payload skip every mask. The kernel is bound by its
+// vector instructions and register budget more than by HBM: tools/exp/probe_txb.hip moves the
+// same bytes in 32 us (64 B) / 161 us (1514 B) with no arithmetic.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "device_util.h"
 #include "halo_common.h"
@@ -29,8 +41,8 @@
 namespace halo {
 namespace {
 
-constexpr uint32_t kTile = 256;
-constexpr uint64_t kFlagAgg = 1ull << 32, kFlagPrefix = 2ull << 32;
+constexpr uint32_t kTile = 64;    // descriptors per tile = one wave's
+constexpr uint32_t kBlock = 256;  // threads per block of the build launch
 
 struct BuildParams {
     const halo_tx_build_desc_t* desc;
@@ -39,10 +51,11 @@ struct BuildParams {
     uint16_t* lens;
     uint8_t* result;
     uint16_t* ip_id;
-    uint32_t* ws;                 // [0] tile ticket, [1] blocks done; u64 tile status from byte 8
+    uint32_t* ws;                 // [0] rejections in the batch, [1 + t] rejections before / in tile t
     uint32_t n, n_tiles, flags, stride;
     uint32_t mac_lo, mac_hi;      // the NetIf's MAC (BuildEthFrm srcMac), little-endian packed
 };
+
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -79,14 +92,6 @@ __device__ __forceinline__ Frame decode(const uint32_t* d, const uint8_t* payloa
     f.hdr_end = f.base + 20u + f.l4hdr;
     f.flen = f.mode == HALO_TX_BUILD_LOOPBACK ? f.iplen : (f.iplen + 14u < 60u ? 60u : f.iplen + 14u);
     return f;
-}
-
-// HALO_TX_B_* of a descriptor, decided before Build* runs (the slot check is build-defined).
-__device__ __forceinline__ uint32_t verdict(const Frame& f, uint32_t stride) {
-    if (f.proto != kIpUdp && f.proto != kIpTcp && f.proto != kIpIcmp) return HALO_TX_B_PROTO;
-    if (f.plen > (f.proto == kIpTcp ? 1460u : 1472u)) return HALO_TX_B_PAYLOAD_LEN;  // udp.go:55 tcp.go:78 icmp.go:71
-    if (f.flen > stride) return HALO_TX_B_SLOT;
-    return HALO_TX_B_OK;
 }
 
 // Header dword k (0..13) of the Ethernet layout, payload bytes zero, L4 checksum field zero.
@@ -129,15 +134,13 @@ __device__ __forceinline__ uint32_t ipv4_cksum(const Frame& f, uint32_t id, bool
     return (~fold16(s)) & 0xFFFFu;
 }
 
-// Payload bytes of output dwords [4c, 4c+4): source bytes [16c - hdr_end, +16) of the payload,
-// never reading a dword that holds no payload byte (the caller masks what is not payload).
-__device__ __forceinline__ void payload_chunk(const Frame& f, uint32_t c, uint32_t (&w)[4]) {
+// Source dwords for output chunk c (payload bytes [16c - hdr_end, +16) of the frame): five
+// aligned dwords, never reading one that holds no payload byte (zeros instead). Issued early;
+// merge_chunk turns them into the chunk once they arrive.
+__device__ __forceinline__ void payload_raw(const Frame& f, uint32_t c, uint32_t (&s)[5]) {
     const int64_t rel = (int64_t)(16 * c) - (int64_t)f.hdr_end;  // payload offset of the chunk's first byte
-    const uint64_t a0 = f.pay + rel;                                // may lie before the payload
-    const uint64_t A = a0 & ~3ull;
-    const uint32_t sh = (uint32_t)(a0 & 3u);
+    const uint64_t A = (f.pay + rel) & ~3ull;                       // may lie before the payload
     const uint64_t lo = f.pay & ~3ull, hi = (f.pay + f.plen + 3) & ~3ull;  // readable dwords [lo, hi)
-    uint32_t s[5];
     typedef const __attribute__((address_space(1))) uint32_t gu32_t;
     gu32_t* q = (gu32_t*)A;
     if (A >= lo && A + 20 <= hi) {
@@ -152,57 +155,47 @@ __device__ __forceinline__ void payload_chunk(const Frame& f, uint32_t c, uint32
             s[i] = (x >= lo && x < hi) ? q[i] : 0u;
         }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(s[i + 1], s[i], sh);
 }
 
-// The frame of descriptor f, lane j of its G-lane group. Chunks 0..3 (bytes 0..63, which hold
-// every header byte and both checksum fields) are stored after the group's L4 sum is known.
-template <int G>
-__device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f, uint32_t id, uint32_t j,
+__device__ __forceinline__ bool chunk_has_payload(const Frame& f, uint32_t c, uint32_t ndw) {
+    return 4 * c < ndw && 16 * c + 16 > f.hdr_end && 16 * c < f.hdr_end + f.plen && f.plen;
+}
+
+// Sum of the four bytes pairs of a dword as 16-bit halves (one v_dot2_u32_u16): the one's-
+// complement sum in the little-endian domain accumulates per dword in u32 without overflow for
+// any frame here (<= 2 * 65535 per dword).
+__device__ __forceinline__ uint32_t hsum_acc(uint32_t w, uint32_t acc) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), one, acc, false);
+}
+
+// The frame of descriptor f on lane j of its G-lane group: chunks j, j+G, ... (U per memory
+// round trip, all loads of a round issued before any is used) merged, masked, summed and stored;
+// then the L4 checksum over the group and the header chunks 0..3 (which hold both checksum
+// fields), stored last.
+template <int G, int U>
+__device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f, const uint32_t* hdr, uint32_t j,
                                             uint8_t* out) {
     const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
-    const bool l3 = f.mode == HALO_TX_BUILD_LOOPBACK;
-    uint32_t e[18];
-    eth_header(f, id, ipv4_cksum(f, id, csum), p, e);
-    const uint32_t l4s = f.base + 20u, l4e = f.base + f.iplen, pay_end = f.hdr_end + f.plen;
+    const uint32_t l4s = f.base + 20u, pay_end = f.hdr_end + f.plen;  // the packet ends at pay_end
     const uint32_t ndw = (f.flen + 3u) >> 2;  // output dwords (the last one zero-filled past the frame)
-    // frame-layout header dword k (0..15): Ethernet as built, loopback = the same bytes from 14 on
-    auto hdr = [&](uint32_t k) -> uint32_t {
-        uint32_t v = 0;
-#pragma unroll
-        for (uint32_t m = 0; m < 14; ++m) {
-            const uint32_t ev = l3 ? ((e[m + 3] >> 16) | (e[m + 4] << 16)) : e[m];
-            v = (k == m) ? ev : v;
-        }
-        return v;
-    };
+    const uint32_t sh = (uint32_t)((f.pay - f.hdr_end) & 3u);  // source misalignment, every chunk
     constexpr int kDefer = G >= 4 ? 1 : 4;  // header chunks this lane keeps until the sum is known
     uint32_t keep[kDefer][4];
-    uint64_t sum = 0;
-    for (uint32_t c = j, r = 0; 4 * c < ndw; c += G, ++r) {
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        if (16 * c + 16 > f.hdr_end && 16 * c < pay_end && f.plen) payload_chunk(f, c, w);
+    uint32_t sum = 0;
+    // a chunk of frame bytes [16c, 16c+16): header bytes, payload, zero padding; its L4-segment
+    // bytes summed
+    auto edge = [&](uint32_t c, uint32_t (&w)[4]) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = 4 * c + i;
             w[i] &= byte_mask(k, f.hdr_end, pay_end);
-            if (k < 16) w[i] |= hdr(k) & byte_mask(k, 0, f.hdr_end);
-            sum += w[i] & byte_mask(k, l4s, l4e);
+            if (k < 16) w[i] |= hdr[k] & byte_mask(k, 0, f.hdr_end);
+            sum = hsum_acc(w[i] & byte_mask(k, l4s, pay_end), sum);
         }
-        if (c < 4) {
-            if constexpr (kDefer == 4) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (q == (int)c)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) keep[q][i] = w[i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) keep[0][i] = w[i];
-            }
-            continue;
-        }
+    };
+    auto store = [&](uint32_t c, const uint32_t (&w)[4]) {
         uint32_t* o = reinterpret_cast<uint32_t*>(out) + 4 * c;
         if (4 * c + 4 <= ndw) {
             *reinterpret_cast<uint4*>(o) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -211,13 +204,49 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
             for (int i = 0; i < 4; ++i)
                 if (4 * c + i < ndw) o[i] = w[i];
         }
+    };
+    for (uint32_t c0 = j; 4 * c0 < ndw; c0 += U * G) {
+        uint32_t raw[U][5];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            if (chunk_has_payload(f, c, ndw)) payload_raw(f, c, raw[u]);
+            else raw[u][0] = raw[u][1] = raw[u][2] = raw[u][3] = raw[u][4] = 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            if (4 * c >= ndw) break;
+            uint32_t w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(raw[u][i + 1], raw[u][i], sh);
+            if (c >= 4 && 16 * c >= f.hdr_end && 16 * c + 16 <= pay_end) {  // payload throughout
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sum = hsum_acc(w[i], sum);
+                store(c, w);
+                continue;
+            }
+            edge(c, w);
+            if (c < 4) {  // a header chunk: stored once the checksum is in
+                if constexpr (kDefer == 4) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (q == (int)c)
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) keep[q][i] = w[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) keep[0][i] = w[i];
+                }
+            } else {
+                store(c, w);
+            }
+        }
     }
     // L4 checksum: pseudo header (UDP / TCP) + the segment, one's-complement, LE domain
-    uint32_t part = fold64(sum);
-    part = group_sum<G>(part);
+    uint32_t part = group_sum<G>(fold16(sum));
     uint32_t ck_le = 0;  // the field's two bytes as a little-endian half-word
     uint32_t ck_at;      // frame byte offset of the L4 checksum field
-    const bool fill = csum || f.proto == kIpIcmp;
     if (f.proto == kIpUdp || f.proto == kIpTcp) {
         const uint32_t s = bswap32(f.src), t = bswap32(f.dst);
         part += hsum(s) + hsum(t) + (f.proto << 8) + bswap16(f.l4hdr + f.plen);
@@ -225,7 +254,7 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
     } else {
         ck_at = f.base + 22u;
     }
-    if (fill) ck_le = (~fold16(part)) & 0xFFFFu;
+    if (csum || f.proto == kIpIcmp) ck_le = (~fold16(part)) & 0xFFFFu;  // ICMP always (icmp.go:84-87)
     const uint32_t ck_dw = ck_at >> 2, ck_sh = (ck_at & 2u) * 8u;
 #pragma unroll
     for (int q = 0; q < kDefer; ++q) {
@@ -234,127 +263,170 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if (4 * c + i == ck_dw) keep[q][i] |= ck_le << ck_sh;
-        uint32_t* o = reinterpret_cast<uint32_t*>(out) + 4 * c;
-        if (4 * c + 4 <= ndw) {
-            *reinterpret_cast<uint4*>(o) = make_uint4(keep[q][0], keep[q][1], keep[q][2], keep[q][3]);
+        store(c, keep[q]);
+    }
+}
+
+// BuildUdpPkt / BuildTcpPkt / BuildIcmpPkt's length limits and the slot check (build-defined):
+// HALO_TX_B_* of a descriptor (its dwords 2 and 9) and its frame length.
+__device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t stride, uint32_t& flen) {
+    const uint32_t mode = (d9 >> 16) & 0xFFu;
+    const uint32_t plen = d2 & 0xFFFFu, proto = (d2 >> 16) & 0xFFu;
+    const uint32_t iplen = 20u + (proto == kIpTcp ? 20u : 8u) + plen;
+    flen = mode == HALO_TX_BUILD_LOOPBACK ? iplen : (iplen + 14u < 60u ? 60u : iplen + 14u);
+    if (proto != kIpUdp && proto != kIpTcp && proto != kIpIcmp) return HALO_TX_B_PROTO;
+    if (plen > (proto == kIpTcp ? 1460u : 1472u)) return HALO_TX_B_PAYLOAD_LEN;  // udp.go:55 tcp.go:78 icmp.go:71
+    if (flen > stride) return HALO_TX_B_SLOT;
+    return HALO_TX_B_OK;
+}
+
+// Launch 1: each wave owns tiles of 64 consecutive descriptors (grid-stride). Lane i loads
+// descriptor i of the tile and decides it; the wave's ballot ranks the rejections; then the
+// wave builds the tile's frames 64 / G at a time, G lanes per frame, each group taking its
+// descriptor's dwords from the lane that holds them (ds_bpermute). No LDS, no barrier.
+template <int G, int U>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) tx_build_kernel(const BuildParams p) {
+    __shared__ uint32_t s_desc[kBlock / 64][kTile * 10 + 1];  // per wave: its tile's descriptors
+    __shared__ uint32_t s_meta[kBlock / 64][kTile];
+    __shared__ uint32_t s_hdr[kBlock / 64][kTile * 16 + 1];  // per wave: frame-layout header dwords 0..15
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t nw = (gridDim.x * kBlock) >> 6;
+    const uint32_t base = *p.ip_id;
+    const uint32_t g = lane / G, j = lane % G;
+    for (uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 6; t < p.n_tiles; t += nw) {
+        const uint32_t first = t * kTile, i = first + lane;
+        uint32_t d[10];
+        if (i < p.n) {
+            const uint2* src = reinterpret_cast<const uint2*>(p.desc + i);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint2 v = src[k];
+                d[2 * k] = v.x;
+                d[2 * k + 1] = v.y;
+            }
         } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (4 * c + i < ndw) o[i] = keep[q][i];
+            for (int k = 0; k < 10; ++k) d[k] = 0u;
         }
-    }
-}
-
-__device__ __forceinline__ uint64_t status_load(const uint64_t* s) {
-    return __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void status_store(uint64_t* s, uint64_t v) {
-    __hip_atomic_store(s, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int G>
-__global__ void __launch_bounds__(256) tx_build_kernel(const BuildParams p) {
-    __shared__ uint32_t s_desc[kTile * 10];
-    __shared__ uint32_t s_meta[kTile];     // bit 31 built, bits 0..15 iphId
-    __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_tile, s_excl, s_base, s_last;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    uint64_t* status = reinterpret_cast<uint64_t*>(p.ws + 2);
-    if (tid == 0) s_base = *p.ip_id;  // read before any ticket: the last block rewrites it at the end
-    for (;;) {
-        if (tid == 0) s_tile = atomicAdd(&p.ws[0], 1u);
-        __syncthreads();
-        const uint32_t tile = s_tile;
-        if (tile >= p.n_tiles) break;
-        const uint32_t first = tile * kTile;
-        const uint32_t cnt = min(kTile, p.n - first);
-        // stage the tile's descriptors (40 B each) with coalesced 8-byte loads
-        const uint2* src = reinterpret_cast<const uint2*>(p.desc + first);
-        for (uint32_t q = tid; q < 5 * cnt; q += kTile) {
-            const uint2 v = src[q];
-            s_desc[2 * q] = v.x;
-            s_desc[2 * q + 1] = v.y;
-        }
-        __syncthreads();
-        // each thread's descriptor: build or not, and its rank among the tile's built frames
-        uint32_t code = HALO_TX_B_PROTO, flen = 0;
-        if (tid < cnt) {
-            const Frame f = decode(&s_desc[10 * tid], p.payload);
-            code = verdict(f, p.stride);
-            flen = f.flen;
-        }
-        const bool ok = tid < cnt && code == HALO_TX_B_OK;
-        const uint64_t bal = __ballot(ok);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        if (lane == 0) s_wave[wave] = __popcll(bal);
-        __syncthreads();
-        uint32_t before = 0, total = 0;
+        uint32_t flen = 0;
+        const uint32_t code = i < p.n ? verdict(d[2], d[9], p.stride, flen) : HALO_TX_B_PROTO;
+        const bool rej = i < p.n && code != HALO_TX_B_OK;
+        const uint64_t bal = __ballot(rej);
+        if (lane == 0) p.ws[1 + t] = (uint32_t)__popcll(bal);  // rejections in this tile
+        const uint32_t before =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        // iphId++ then use (ipv4.go:103-104); rejections in earlier tiles settled by launches 2/3
+        const uint32_t mine = (i < p.n && !rej) ? 0x80000000u | ((base + 1u + i - before) & 0xFFFFu) : 0u;
+        {  // this lane's descriptor's header (Ethernet layout, or the loopback bytes from 14 on)
+            const Frame f = decode(d, p.payload);
+            const uint32_t id = mine & 0xFFFFu;
+            uint32_t e[18];
+            eth_header(f, id, ipv4_cksum(f, id, (p.flags & HALO_RX_CSUM_ENABLE) != 0), p, e);
+            const bool l3 = f.mode == HALO_TX_BUILD_LOOPBACK;
 #pragma unroll
-        for (uint32_t w = 0; w < 4; ++w) {
-            before += w < wave ? s_wave[w] : 0u;
-            total += s_wave[w];
+            for (int k = 0; k < 16; ++k)
+                s_hdr[wv][16 * lane + k] = k >= 14 ? 0u : l3 ? ((e[k + 3] >> 16) | (e[k + 4] << 16)) : e[k];
         }
-        // decoupled look-back: the number of frames built in all tiles before this one
-        if (wave == 0) {
-            if (lane == 0) status_store(&status[tile], (tile == 0 ? kFlagPrefix : kFlagAgg) | total);
-            uint32_t excl = 0;
-            if (tile > 0) {
-                int64_t j = (int64_t)tile - 1;
-                for (;;) {
-                    const int64_t idx = j - (int64_t)lane;
-                    uint64_t v = idx >= 0 ? status_load(&status[idx]) : kFlagPrefix;
-                    const uint64_t pre = __ballot((v >> 32) == 2u);
-                    const uint32_t lim = pre ? (uint32_t)__builtin_ctzll(pre) : 63u;  // lanes 0..lim count
-                    const uint64_t zero = __ballot((v >> 32) == 0u);
-                    if (zero & ((lim == 63u) ? ~0ull : ((2ull << lim) - 1ull))) continue;  // not published yet
-                    uint32_t x = lane <= lim ? (uint32_t)v : 0u;
+        if constexpr (G == 1) {
+            __builtin_amdgcn_wave_barrier();
+            if (mine >> 31)
+                build_frame<G, U>(p, decode(d, p.payload), &s_hdr[wv][16 * lane], 0, p.frames + (uint64_t)i * p.stride);
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            // the wave's descriptors through its own LDS region (no block barrier), so that they
+            // are not live in registers across the build steps
 #pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, 64);
-                    excl += x;
-                    if (pre) break;
-                    j -= 64;
-                }
-                if (lane == 0) status_store(&status[tile], kFlagPrefix | (excl + total));
-            }
-            if (lane == 0) s_excl = excl;
-        }
-        __syncthreads();
-        const uint32_t id = (s_base + s_excl + before + rank + 1u) & 0xFFFFu;  // iphId++ then use
-        if (tid < cnt) {
-            s_meta[tid] = (ok ? 0x80000000u : 0u) | id;
-            p.lens[first + tid] = ok ? (uint16_t)flen : (uint16_t)0;
-            if (p.result) p.result[first + tid] = (uint8_t)code;
-        }
-        __syncthreads();
-        // build: G lanes per frame, 256 / G frames per round
-        constexpr uint32_t kPer = kTile / G;
-        const uint32_t g = tid / G, jl = tid % G;
+            for (int k = 0; k < 10; ++k) s_desc[wv][10 * lane + k] = d[k];
+            s_meta[wv][lane] = mine;
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-        for (uint32_t r = 0; r < (uint32_t)G; ++r) {
-            const uint32_t fi = r * kPer + g;
-            if (fi < cnt && (s_meta[fi] >> 31)) {  // uniform over the group
-                const Frame f = decode(&s_desc[10 * fi], p.payload);
-                build_frame<G>(p, f, s_meta[fi] & 0xFFFFu, jl, p.frames + (uint64_t)(first + fi) * p.stride);
+            for (uint32_t step = 0; step < (uint32_t)G; ++step) {
+                const uint32_t fl = step * (64u / G) + g;  // this group's frame, as a lane of the tile
+                const uint32_t meta = s_meta[wv][fl];
+                if (meta >> 31) {  // uniform over the group
+                    uint32_t dd[10];
+#pragma unroll
+                    for (int k = 0; k < 10; ++k) dd[k] = s_desc[wv][10 * fl + k];
+                    build_frame<G, U>(p, decode(dd, p.payload), &s_hdr[wv][16 * fl], j,
+                                      p.frames + (uint64_t)(first + fl) * p.stride);
+                }
             }
+            __builtin_amdgcn_wave_barrier();  // the region is rewritten for the next tile
         }
-        __syncthreads();  // LDS is reused by the next tile
+        if (i < p.n) {  // after the build: these stores do not hold up the payload loads
+            p.lens[i] = code == HALO_TX_B_OK ? (uint16_t)flen : (uint16_t)0;
+            if (p.result) p.result[i] = (uint8_t)code;
+        }
     }
-    // the last block out publishes the new iphId and leaves the workspace zeroed for the next launch
-    if (tid == 0) {
-        __threadfence();
-        s_last = atomicAdd(&p.ws[1], 1u) == gridDim.x - 1u;
+}
+
+// Launch 2 (one block): the rejections of the whole batch and before every tile; the new iphId.
+__global__ void __launch_bounds__(1024) tx_settle_kernel(const BuildParams p) {
+    __shared__ uint32_t s_part[1024 / 64];
+    __shared__ uint32_t s_carry;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    // the common case first: no rejection anywhere (every load of the pass in flight at once)
+    uint32_t any = 0;
+    for (uint32_t t = tid; t < p.n_tiles; t += 1024) any |= p.ws[1 + t];
+    if (tid == 0) s_carry = 0;
+    const int none = __syncthreads_or(any != 0) == 0;
+    if (none) {
+        if (tid == 0) {
+            p.ws[0] = 0;
+            *p.ip_id = (uint16_t)(*p.ip_id + p.n);  // one iphId++ per built packet
+        }
+        return;  // the tile counts are all 0 = the rejections before every tile
     }
-    __syncthreads();
-    if (s_last) {
-        __threadfence();
-        if (tid == 0) *p.ip_id = (uint16_t)(s_base + (uint32_t)status_load(&status[p.n_tiles - 1]));
+    for (uint32_t t0 = 0; t0 < p.n_tiles; t0 += 1024) {  // exclusive scan, 1024 tiles per pass
+        const uint32_t t = t0 + tid;
+        const uint32_t v = t < p.n_tiles ? p.ws[1 + t] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) s_part[wave] = x;
         __syncthreads();
-        for (uint32_t t = tid; t < p.n_tiles; t += kTile) status_store(&status[t], 0ull);
+        uint32_t off = s_carry;
+        for (uint32_t w = 0; w < wave; ++w) off += s_part[w];
+        if (t < p.n_tiles) p.ws[1 + t] = off + x - v;  // rejections before tile t
         __syncthreads();
         if (tid == 0) {
-            p.ws[0] = 0u;
-            p.ws[1] = 0u;
-            __threadfence();
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < 1024 / 64; ++w) tot += s_part[w];
+            s_carry += tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        p.ws[0] = s_carry;
+        *p.ip_id = (uint16_t)(*p.ip_id + p.n - s_carry);  // one iphId++ per built packet
+    }
+}
+
+// Launch 3 (only useful after a rejection): frames behind rejections in earlier tiles were
+// numbered too high by that many; patch their identification and, with checksums on, their
+// IPv4 header checksum (RFC 1624 incremental update of the value BuildIpv4Pkt computed).
+__global__ void __launch_bounds__(kBlock) tx_renumber_kernel(const BuildParams p) {
+    if (p.ws[0] == 0u) return;  // the common case: nothing was rejected
+    const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
+    for (uint32_t t = blockIdx.x; t < p.n_tiles; t += gridDim.x) {
+        const uint32_t back = p.ws[1 + t];
+        if (back == 0u || threadIdx.x >= kTile) continue;
+        const uint32_t i = t * kTile + threadIdx.x;
+        if (i >= p.n || p.lens[i] == 0) continue;
+        const uint32_t mode = (reinterpret_cast<const uint32_t*>(p.desc + i)[9] >> 16) & 0xFFu;
+        uint8_t* ip = p.frames + (uint64_t)i * p.stride + (mode == HALO_TX_BUILD_LOOPBACK ? 0u : 14u);
+        const uint32_t old_id = ((uint32_t)ip[4] << 8) | ip[5];
+        const uint32_t new_id = (old_id - back) & 0xFFFFu;
+        ip[4] = (uint8_t)(new_id >> 8);
+        ip[5] = (uint8_t)new_id;
+        if (csum) {  // HC' = ~(~HC + ~m + m')
+            const uint32_t hc = ((uint32_t)ip[10] << 8) | ip[11];
+            const uint32_t nc = (~fold16((~hc & 0xFFFFu) + (~old_id & 0xFFFFu) + new_id)) & 0xFFFFu;
+            ip[10] = (uint8_t)(nc >> 8);
+            ip[11] = (uint8_t)nc;
         }
     }
 }
@@ -363,7 +435,7 @@ __global__ void __launch_bounds__(256) tx_build_kernel(const BuildParams p) {
 }  // namespace halo
 
 extern "C" HALO_API uint64_t halo_tx_build_workspace(uint32_t n) {
-    return 8ull + 8ull * (((uint64_t)n + halo::kTile - 1) / halo::kTile);
+    return 4ull * (1ull + ((uint64_t)n + halo::kTile - 1) / halo::kTile);
 }
 
 extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d_desc, uint32_t n,
@@ -377,7 +449,7 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
     if (!d_desc || !d_payload || !d_frames || !d_out_lens || !d_ip_id || !d_workspace) return HALO_E_INVAL;
     if ((out_stride & 3u) || out_stride < 60u) return HALO_E_INVAL;
     if ((reinterpret_cast<uintptr_t>(d_desc) & 7u) || (reinterpret_cast<uintptr_t>(d_frames) & 3u) ||
-        (reinterpret_cast<uintptr_t>(d_workspace) & 7u) || (reinterpret_cast<uintptr_t>(d_ip_id) & 1u))
+        (reinterpret_cast<uintptr_t>(d_workspace) & 3u) || (reinterpret_cast<uintptr_t>(d_ip_id) & 1u))
         return HALO_E_INVAL;
     if (workspace_bytes < halo_tx_build_workspace(n)) return HALO_E_INVAL;
     int rc = halo::check_device();
@@ -397,12 +469,21 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
     p.mac_lo = (uint32_t)netif->mac[0] | ((uint32_t)netif->mac[1] << 8) | ((uint32_t)netif->mac[2] << 16) |
                ((uint32_t)netif->mac[3] << 24);
     p.mac_hi = (uint32_t)netif->mac[4] | ((uint32_t)netif->mac[5] << 8);
-    // blocks loop over tiles; 8 resident 256-thread blocks per CU on 256 CUs
-    const uint32_t grid = p.n_tiles < 2048u ? p.n_tiles : 2048u;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    // a wave per tile of 64 descriptors, grid-stride: up to 8 resident 4-wave blocks per CU
+    const uint32_t waves = p.n_tiles, blocks = (waves + 3) / 4;
+    const dim3 grid(blocks < 2048u ? blocks : 2048u), blk(halo::kBlock);
+    // lanes per frame and chunks per lane from the largest frame expected (a frame needs
+    // ceil(flen / 16) chunks; longer ones than G * U chunks take extra rounds)
     const uint32_t h = max_payload_hint ? max_payload_hint : 1472u;
-    if (h + 54u <= 128u) hipLaunchKernelGGL(halo::tx_build_kernel<1>, dim3(grid), dim3(256), 0, s, p);
-    else if (h + 54u <= 1024u) hipLaunchKernelGGL(halo::tx_build_kernel<4>, dim3(grid), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(halo::tx_build_kernel<8>, dim3(grid), dim3(256), 0, s, p);
+    const uint32_t chunks = (h + 42u + 15u) / 16u;  // UDP / ICMP headers; TCP frames 12 B longer
+    if (chunks <= 4) hipLaunchKernelGGL((halo::tx_build_kernel<1, 4>), grid, blk, 0, s, p);
+    else if (chunks <= 16) hipLaunchKernelGGL((halo::tx_build_kernel<4, 4>), grid, blk, 0, s, p);
+    else if (chunks <= 32) hipLaunchKernelGGL((halo::tx_build_kernel<8, 4>), grid, blk, 0, s, p);
+    else if (chunks <= 64) hipLaunchKernelGGL((halo::tx_build_kernel<16, 4>), grid, blk, 0, s, p);
+    else hipLaunchKernelGGL((halo::tx_build_kernel<32, 3>), grid, blk, 0, s, p);
+    hipLaunchKernelGGL(halo::tx_settle_kernel, dim3(1), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(halo::tx_renumber_kernel, dim3(p.n_tiles < 256u ? p.n_tiles : 256u), dim3(halo::kBlock), 0,
+                       s, p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }

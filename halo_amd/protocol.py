@@ -203,7 +203,7 @@ class TxBuilder:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         ws = int(_lib.lib.halo_tx_build_workspace(max_frames))
         self.max_frames = max_frames
-        self.ws = torch.zeros(ws, dtype=torch.uint8, device=self.device)  # zeroed once; launches leave it so
+        self.ws = torch.empty(ws, dtype=torch.uint8, device=self.device)  # scratch, no initialisation needed
         self.ip_id = torch.from_numpy(np.array([ip_id & 0xFFFF], np.uint16).view(np.int16)).to(self.device)
 
     def SetIpHeaderId(self, value: int) -> None:

@@ -427,8 +427,8 @@ typedef struct halo_tx_build_desc {
     uint8_t pad;
 } halo_tx_build_desc_t;    /* 40 B */
 
-/* Device workspace for n descriptors. Zero it once before its first use (hipMemset); every
- * launch leaves it zeroed again for the next one. One launch at a time per workspace. */
+/* Device scratch for n descriptors (bytes, 4-byte aligned; no initialisation needed). One
+ * launch at a time per workspace. */
 HALO_API uint64_t halo_tx_build_workspace(uint32_t n);
 /* Build n frames into fixed output slots: frame i at d_frames + i * out_stride (a multiple of
  * 4, at least 60), d_out_lens[i] = its length (0 when not built), d_result[i] (optional) =

@@ -269,7 +269,7 @@ def test_tx_build_desc_layout_and_validation(tmp_path):
     ip = np.zeros(4, np.uint16)
     lens = np.zeros(4, np.uint16)
     wsb = int(L.halo_tx_build_workspace(4))
-    assert wsb == 16 and int(L.halo_tx_build_workspace(257)) == 24
+    assert wsb == 8 and int(L.halo_tx_build_workspace(513)) == 40  # u32: rejections, then one per 64-descriptor tile
     args = lambda stride=64, flags=1, wsbytes=wsb: (d.ctypes.data, 4, buf.ctypes.data, flags, n, 0, buf.ctypes.data,  # noqa: E731
                                                   stride, lens.ctypes.data, None, ip.ctypes.data, ws.ctypes.data,
                                                   wsbytes, None)
@@ -277,6 +277,6 @@ def test_tx_build_desc_layout_and_validation(tmp_path):
     assert L.halo_tx_build_batch_device(*args(stride=62)) == -1  # not a multiple of 4
     assert L.halo_tx_build_batch_device(*args(stride=56)) == -1  # below the 60 B minimum frame
     assert L.halo_tx_build_batch_device(*args(flags=2)) == -1    # only CSUM_ENABLE applies
-    assert L.halo_tx_build_batch_device(*args(wsbytes=8)) == -1  # workspace too small
+    assert L.halo_tx_build_batch_device(*args(wsbytes=4)) == -1  # workspace too small
     if not torch.cuda.is_available():
         assert L.halo_tx_build_batch_device(*args()) == _lib.HALO_E_NODEV

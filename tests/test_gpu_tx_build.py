@@ -45,7 +45,6 @@ def _run(dev, desc, payload, netif, stride, flags, ip_start, hint=0, fill=0):
     frames, lens, res = b.build(d, pl, netif=netif, out_stride=stride, frames=frames, check_sum_enable=bool(flags),
                                 max_payload_hint=hint)
     torch.cuda.synchronize()
-    assert int(b.ws.count_nonzero()) == 0  # the launch left its workspace zeroed
     return frames.cpu().numpy(), lens.cpu().numpy().view(np.uint16), res.cpu().numpy(), b.iph_id
 
 
@@ -126,7 +125,6 @@ def test_build_slots_ids_and_two_launches(dev, oracle_lib):
     assert np.array_equal(ids[0], np.arange(8, 8 + built))
     assert np.array_equal(ids[1], np.arange(8 + built, 8 + 2 * built))
     assert b.iph_id == 7 + 2 * built
-    assert int(b.ws.count_nonzero()) == 0
 
 
 def test_build_then_parse_round_trip(dev):

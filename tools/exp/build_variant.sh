@@ -6,5 +6,5 @@ cd "$(dirname "$0")/../.."
 name=$1; shift
 C=halo_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fvisibility=hidden "$@" -Iinclude -I$C \
-  $C/rx_parse.hip $C/tx_fixup.hip $C/flow_hash.hip $C/route_lpm.hip $C/synth.hip $C/host_path.hip $C/ring_rx.hip \
+  $C/*.hip \
   -o tools/exp/libhalo_rx_$name.so
