@@ -100,6 +100,7 @@ BUILD_DESC_DTYPE = np.dtype([("payload_off", "<u8"), ("payload_len", "<u2"), ("p
                              ("pad", "u1")])
 assert BUILD_DESC_DTYPE.itemsize == 40
 TX_BUILD_ETH, TX_BUILD_LOOPBACK = 0, 1   # HALO_TX_BUILD_*
+DEEP_NAT_DTYPE = np.dtype([("lan_ip", "<u4"), ("lan_port", "<u2"), ("found", "u1"), ("pad", "u1")])  # halo_tx_deep_nat_t
 TX_B_OK, TX_B_PAYLOAD_LEN, TX_B_PROTO, TX_B_SLOT = 0, 1, 2, 3
 FLOW_NAT_LAN, FLOW_NAT_WAN = 0, 1        # HALO_FLOW_*
 NAT_SYMMETRIC, NAT_FULL_CONE = 0, 1      # HALO_NAT_* (engine.NatTypeSymmetric / NatTypeFullCone)
@@ -225,6 +226,8 @@ _PROTOS = {
     "halo_rx_dispatch": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_rx_dispatch_compact": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
     "halo_rx_dispatch_loopback": (ctypes.c_int, [_u8p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p]),
+    "halo_tx_icmp_deep_nat_batch_device": (ctypes.c_int, [
+        _u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p, _u8p, ctypes.c_void_p]),
     "halo_tx_fixup_batch_device": (ctypes.c_int, [
         _u8p, _u8p, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_tx_build_workspace": (ctypes.c_uint64, [ctypes.c_uint32]),

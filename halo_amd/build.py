@@ -11,7 +11,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "halo_amd", "csrc")
 OUT = os.path.join(ROOT, "halo_amd", "lib", "libhalo_rx.so")
-SOURCES = ["rx_parse.hip", "tx_fixup.hip", "tx_build.hip", "flow_hash.hip", "route_lpm.hip", "synth.hip", "host_path.hip",
+SOURCES = ["rx_parse.hip", "tx_fixup.hip", "tx_build.hip", "deep_nat.hip", "flow_hash.hip", "route_lpm.hip", "synth.hip", "host_path.hip",
            "ring_rx.hip"]
 # measurement tooling (bench.py's native step loop), linked against the product library
 BENCH_SRC = os.path.join(ROOT, "tools", "bench_loop.hip")

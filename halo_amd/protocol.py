@@ -234,3 +234,23 @@ class TxBuilder:
             _lib.ptr(self.ws), self.ws.numel(), _stream_handle(stream))
         _lib.check("halo_tx_build_batch_device", rc)
         return frames, lens, result
+
+
+# ---- IcmpTtlDeepNat (engine/icmp_engine.go:55-86) -----------------------------------------------
+from ._lib import DEEP_NAT_DTYPE  # noqa: E402,F401
+
+
+def icmp_ttl_deep_nat_batch(frames, offsets_dw, lens, *, nat=None, check_sum_enable: bool = True, quote=None,
+                            applied=None, stream=None):
+    """IcmpTtlDeepNat over a device-resident ragged batch (halo_tx_icmp_deep_nat_batch_device).
+
+    nat None: only the checks — ``quote`` (cuda uint8 [n, 32], halo_rx_result_t) receives per
+    frame the NatGetFlowByWan arguments (hash them with flow_hash kind NAT_WAN). nat: cuda uint8
+    tensor of n * 8 bytes (DEEP_NAT_DTYPE records: the lookups' LanHost and found) — frames
+    rewritten in place, ``applied`` (cuda uint8 [n]) = IcmpTtlDeepNat's bool. Asynchronous."""
+    n = int(lens.numel())
+    rc = _lib.lib.halo_tx_icmp_deep_nat_batch_device(
+        _lib.ptr(frames), _lib.ptr(offsets_dw), _lib.ptr(lens), n, _lib.ptr(nat),
+        HALO_RX_CSUM_ENABLE if check_sum_enable else 0, _lib.ptr(quote), _lib.ptr(applied), _stream_handle(stream))
+    _lib.check("halo_tx_icmp_deep_nat_batch_device", rc)
+    return quote, applied

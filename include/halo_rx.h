@@ -382,6 +382,35 @@ HALO_API int halo_tx_fixup_batch_device(uint8_t* d_bytes, const uint32_t* d_offs
                                         uint32_t max_len_hint, uint8_t* d_result,
                                         halo_stream_t stream);
 
+/* ---- IcmpTtlDeepNat (engine/icmp_engine.go:55-86) -------------------------------------------
+ * The forward path calls it on every received Ethernet payload of a NATing interface before its
+ * own DNAT (engine/ipv4_engine.go:111-130): when the packet is an ICMP time-exceeded message
+ * (ParseIpv4Pkt and ParseIcmpPkt pass, type ICMP_TTL) quoting at least 28 bytes of the original
+ * packet, it looks the quoted flow up with NatGetFlowByWan(quoted dst, its dst port, quoted src,
+ * its src port, quoted proto) and, when a flow exists, rewrites the quote's source to the flow's
+ * LAN host (NatChangeSrc on the quote, with its ReCalc* — TCP's needs 38 quoted bytes) and the
+ * message's destination to the LAN host with "port" 0 (NatChangeDst on the untrimmed Ethernet
+ * payload: its ICMP checksum covers Ethernet padding). The NAT table stays the caller's: call
+ * once with d_nat = NULL to get per frame a quote record — status HALO_RX_OK when the message
+ * qualifies, else the failing rx status, HALO_RX_IP_PROTO (not ICMP), HALO_RX_ICMP_TYPE (not
+ * ICMP_TTL) or HALO_RX_L4_LEN (quote < 28 B); ip_proto = the quoted protocol; src_ip / sport =
+ * the quoted destination and its port, dst_ip / dport = the quoted source and its port, so that
+ * halo_flow_hash_device(HALO_FLOW_NAT_WAN) of the records is NatGetFlowByWan's key — then again
+ * with the lookups' results in d_nat to rewrite the frames in place. d_applied[i] = 1 when frame
+ * i was rewritten (IcmpTtlDeepNat returned true). Frames are the ragged layout of the rx parse;
+ * `flags & HALO_RX_CSUM_ENABLE` is protocol.CheckSumEnable. A slow path: one wavefront per frame. */
+typedef struct halo_tx_deep_nat {
+    uint32_t lan_ip;   /* NatFlow.LanHostIpAddr (IpAddrToU form)       */
+    uint16_t lan_port; /* NatFlow.LanHostPort                          */
+    uint8_t found;     /* NatGetFlowByWan returned a flow               */
+    uint8_t pad;
+} halo_tx_deep_nat_t;  /* 8 B */
+HALO_API int halo_tx_icmp_deep_nat_batch_device(uint8_t* d_bytes, const uint32_t* d_offsets_dw,
+                                                const uint16_t* d_lens, uint32_t n,
+                                                const halo_tx_deep_nat_t* d_nat, uint32_t flags,
+                                                halo_rx_result_t* d_quote, uint8_t* d_applied,
+                                                halo_stream_t stream);
+
 /* ---- transmit direction: batch packet construction (the Build* half) --
  * The locally originated send chain, one frame per descriptor:
  *   NetIf.TxUdp / TxTcp / TxIcmp   engine/{udp,tcp,icmp}_engine.go:24-32 / :29-37 / :26-34

@@ -460,3 +460,65 @@ ORA_API int ora_tx_build_batch(const halo_tx_build_desc_t* desc, uint32_t n, con
     }
     return 0;
 }
+
+/* ================================================================================================
+ * IcmpTtlDeepNat (engine/icmp_engine.go:55-86): called by Ipv4RouteForward on the received
+ * frame's Ethernet payload before its own DNAT (engine/ipv4_engine.go:111-130). ParseIpv4Pkt ->
+ * ICMP only -> ParseIcmpPkt -> ICMP_TTL only -> quote (icmpPayload) of at least 28 bytes ->
+ * NatGetFlowByWan(quoted dst, its dst port, quoted src, its src port, quoted proto) -> when a
+ * flow exists: NatChangeSrc(icmpPayload, LanHost) and NatChangeDst(ethPayload, LanHost, 0).
+ * ParseIpv4Pkt and ParseIcmpPkt are the rx restatement's (ora_rx_frame with HALO_RX_L3_START on
+ * the Ethernet payload); the NAT table is the caller's: `found` / lan_ip / lan_port are what the
+ * lookup returned. */
+ORA_API void ora_rx_frame(const uint8_t* frame, uint32_t len, uint32_t flags, const halo_rx_netif_t* netif,
+                          halo_rx_result_t* r);
+
+/* The checks up to the lookup, as a record: status (OK, the failing rx status, IP_PROTO = not
+ * ICMP, ICMP_TYPE = not ICMP_TTL, L4_LEN = quote < 28 B), ip_proto = the quoted protocol and the
+ * lookup's arguments in received-packet orientation: src_ip/sport = the quoted packet's
+ * destination (the remote end), dst_ip/dport = its source (the WAN side) — so a NAT_WAN flow key
+ * of the record is NatGetFlowByWan's key. */
+ORA_API void ora_icmp_quote(const uint8_t* frame, uint32_t L, uint32_t flags, halo_rx_result_t* q) {
+    memset(q, 0, sizeof *q);
+    q->ethertype = 0x0800;
+    q->ip_proto = 0xff;
+    if (L < 14) { q->status = HALO_RX_ETH_LEN; return; }
+    const uint8_t* pkt = frame + 14;
+    halo_rx_netif_t nif;
+    memset(&nif, 0, sizeof nif);
+    halo_rx_result_t r;
+    ora_rx_frame(pkt, L - 14, (flags & HALO_RX_CSUM_ENABLE) | HALO_RX_L3_START, &nif, &r);
+    if (r.status >= HALO_RX_IP_LEN && r.status <= HALO_RX_IP_TOTLEN_OVERRUN) { q->status = r.status; return; }
+    if (r.ip_proto != 0x01) { q->status = HALO_RX_IP_PROTO; return; }
+    if (r.status != HALO_RX_OK) { q->status = r.status; return; }  /* ParseIcmpPkt failed */
+    if (r.l4_aux != 0x0b) { q->status = HALO_RX_ICMP_TYPE; return; }
+    const uint8_t* ic = pkt + 28;          /* icmpPayload = ipv4Payload[8:] */
+    const uint32_t ilen = r.payload_len;   /* totalLen - 28 */
+    if (ilen < 28) { q->status = HALO_RX_L4_LEN; return; }
+    q->ip_proto = ic[9];
+    q->src_ip = ((uint32_t)ic[16] << 24) | ((uint32_t)ic[17] << 16) | ((uint32_t)ic[18] << 8) | ic[19];
+    q->dst_ip = ((uint32_t)ic[12] << 24) | ((uint32_t)ic[13] << 16) | ((uint32_t)ic[14] << 8) | ic[15];
+    uint16_t wan_port = 0, remote_port = 0;  /* NatGetSrcDstPort(icmpPayload), ipv4.go:229-246 */
+    switch (ic[9]) {
+        case 0x01: wan_port = remote_port = be16(ic + 24); break;
+        case 0x06:
+        case 0x11: wan_port = be16(ic + 20); remote_port = be16(ic + 22); break;
+        default: break;
+    }
+    q->sport = remote_port;
+    q->dport = wan_port;
+}
+
+/* In place; returns isIcmpTtl. */
+ORA_API int ora_icmp_deep_nat(uint8_t* frame, uint32_t L, uint32_t flags, uint32_t lan_ip, uint16_t lan_port,
+                              int found) {
+    halo_rx_result_t q;
+    ora_icmp_quote(frame, L, flags, &q);
+    if (q.status != HALO_RX_OK || !found) return 0;
+    const int en = (flags & HALO_RX_CSUM_ENABLE) != 0;
+    uint8_t* pkt = frame + 14;
+    const uint32_t total_len = be16(pkt + 2);
+    nat_change(pkt + 28, total_len - 28, lan_ip, lan_port, 0, en); /* NatChangeSrc(icmpPayload, ...) */
+    nat_change(pkt, L - 14, lan_ip, 0, 1, en);                      /* NatChangeDst(ethPayload, ..., 0) */
+    return 1;
+}

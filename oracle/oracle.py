@@ -101,6 +101,10 @@ def lib() -> ctypes.CDLL:
         L.ora_route_find_batch.argtypes = [vp, vp, u32, vp]
         L.ora_tx_batch.restype = ctypes.c_int
         L.ora_tx_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, ctypes.c_int]
+        L.ora_icmp_quote.restype = None
+        L.ora_icmp_quote.argtypes = [vp, u32, u32, vp]
+        L.ora_icmp_deep_nat.restype = ctypes.c_int
+        L.ora_icmp_deep_nat.argtypes = [vp, u32, u32, u32, ctypes.c_uint16, ctypes.c_int]
         L.ora_tx_build_batch.restype = ctypes.c_int
         L.ora_tx_build_batch.argtypes = [vp, u32, vp, u32, vp, vp, u32, vp, vp, ctypes.POINTER(ctypes.c_uint16)]
         u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -250,6 +254,21 @@ def tx_build_batch(desc: np.ndarray, payload: np.ndarray, src_mac: bytes, flags:
     assert lib().ora_tx_build_batch(_p(desc), n, _p(pay), flags, _p(mac), _p(frames), out_stride, _p(lens), _p(res),
                                     ctypes.byref(iph)) == 0
     return frames[:n], lens[:n], res[:n], int(iph.value)
+
+
+def icmp_quote(frame: bytes, flags: int = 1) -> np.ndarray:
+    """IcmpTtlDeepNat's checks up to its NAT lookup, as a record (ora_icmp_quote)."""
+    b = np.frombuffer(bytes(frame) + b"\0", dtype=np.uint8)
+    out = np.zeros(1, dtype=RESULT_DTYPE)
+    lib().ora_icmp_quote(_p(b), len(frame), flags, _p(out))
+    return out[0]
+
+
+def icmp_deep_nat(frame: bytes, lan_ip: int, lan_port: int, found: bool, flags: int = 1):
+    """IcmpTtlDeepNat on a copy of the frame: (rewritten frame bytes, isIcmpTtl)."""
+    b = np.frombuffer(bytes(frame) + b"\0", dtype=np.uint8).copy()
+    ok = lib().ora_icmp_deep_nat(_p(b), len(frame), flags, lan_ip, lan_port, int(found))
+    return b[:len(frame)].tobytes(), bool(ok)
 
 
 def xxh3_64(data: bytes) -> int:

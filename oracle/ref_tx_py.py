@@ -293,3 +293,48 @@ def tx_build_len(desc: dict) -> int:
     """The frame length the Build* chain produces for a descriptor (no bytes needed)."""
     l4 = (20 if desc["proto"] == 0x06 else 8) + desc["payload_len"]
     return 20 + l4 if desc["mode"] == MODE_LOOPBACK else max(60, 34 + l4)
+
+
+# ---- IcmpTtlDeepNat (engine/icmp_engine.go:55-86): the NAT rewrite of the packet an ICMP
+#      time-exceeded message quotes, applied by Ipv4RouteForward before its own DNAT
+#      (engine/ipv4_engine.go:111-130). The NAT table lookup (NatGetFlowByWan) is the caller's.
+def icmp_quote(eth_payload: bytes, check_sum_enable=True):
+    """The checks of IcmpTtlDeepNat up to its flow lookup. Returns (status name, lookup args) with
+    lookup args = (proto, remote ip, remote port, wan ip, wan port) as NatGetFlowByWan takes them,
+    or None when the function returns early. Status: "OK", the rx status of ParseIpv4Pkt /
+    ParseIcmpPkt when they fail, "IP_PROTO" when the packet is not ICMP, "ICMP_TYPE" when the type
+    is not ICMP_TTL, "L4_LEN" when the quote is shorter than 28 bytes."""
+    from . import ref_py as R
+
+    c = R.Cfg(check_sum_enable, False)
+    ipv4_payload, proto, _src, _dst, _tl, err = R.parse_ipv4_pkt(bytes(eth_payload), c)
+    if err:
+        return err, None
+    if proto != 0x01:
+        return "IP_PROTO", None
+    icmp_payload, icmp_type, _id, _seq, err = R.parse_icmp_pkt(ipv4_payload, c)
+    if err:
+        return err, None
+    if icmp_type != 0x0B:
+        return "ICMP_TYPE", None
+    if len(icmp_payload) < 28:
+        return "L4_LEN", None
+    wan_port, remote_port = R.nat_get_src_dst_port(icmp_payload)
+    return "OK", (icmp_payload[9], R.ip_addr_to_u(icmp_payload[16:20]), remote_port,
+                  R.ip_addr_to_u(icmp_payload[12:16]), wan_port)
+
+
+def icmp_ttl_deep_nat(eth_payload: bytearray, lan_ip: int, lan_port: int, found: bool,
+                      check_sum_enable=True) -> bool:
+    """IcmpTtlDeepNat on eth_payload in place, natFlow = (lan_ip, lan_port) when found.
+    Returns isIcmpTtl."""
+    st, args = icmp_quote(bytes(eth_payload), check_sum_enable)
+    if st != "OK" or not found:
+        return False
+    total_len = (eth_payload[2] << 8) | eth_payload[3]
+    # icmpPayload = ipv4Payload[8:] = eth_payload[28:totalLen], a slice aliasing eth_payload
+    inner = bytearray(eth_payload[28:total_len])
+    nat_change_src(inner, lan_ip, lan_port, check_sum_enable)
+    eth_payload[28:total_len] = inner
+    nat_change_dst(eth_payload, lan_ip, 0, check_sum_enable)  # the whole (untrimmed) slice
+    return True
