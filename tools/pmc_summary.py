@@ -37,7 +37,7 @@ def alg_bytes():
     from tools.prof_kernels import WORKLOADS
 
     out = {}
-    for name, kw, n, _rot, _launches, slen, _flags, _hint in WORKLOADS:
+    for name, kw, n, _rot, _launches, slen, _flags, _hint in WORKLOADS:  # noqa: B007
         kw = dict(kw)
         kw.pop("strided", None)
         lay = synth.layout(n, **kw, ragged=not slen)
@@ -45,6 +45,14 @@ def alg_bytes():
         meta = 0 if slen else 6 * n
         if name.startswith("flow_hash"):  # record bytes 0..19 in; hash + bucket out
             out[name] = (20 * n, 12 * n)
+            continue
+        if name.startswith("lo_drain"):  # 50 B packets + offset/len in, 32 B record out
+            out[name] = (56 * n, 32 * n)
+            continue
+        if name.startswith("tx_build"):  # descriptor + payload in; frame + length + result out
+            plen = _hint
+            flen = max(60, 42 + plen)
+            out[name] = ((40 + plen) * n, (flen + 3) * n)
             continue
         if name.startswith("tx_"):  # + 16 B op in; 1 B result + 20 B of rewritten header out
             import bench
@@ -70,12 +78,16 @@ def main():
             order += [name] * launches
 
     def family(w):
-        return "flow_hash_kernel" if w.startswith("flow_hash") else ("tx_fixup" if w.startswith("tx_") else "rx_")
+        if w.startswith("flow_hash"):
+            return "flow_hash_kernel"
+        if w.startswith("tx_build"):
+            return "tx_build_kernel"
+        return "tx_fixup" if w.startswith("tx_") else "rx_"
 
     def attribute(rows, key="Dispatch_Id"):
         """dispatch id -> workload: each kernel family's dispatches in launch order."""
         amap = {}
-        for fam in ("rx_", "tx_fixup", "flow_hash_kernel"):
+        for fam in ("rx_", "tx_fixup", "flow_hash_kernel", "tx_build_kernel"):
             disp = sorted({int(r[key]) for r in rows if fam in r["Kernel_Name"]})
             ws = [w for w in order if family(w) == fam]
             # (the flow-hash workload's one preparatory parse comes after every rx workload's

@@ -18,15 +18,21 @@ sys.path.insert(0, ROOT)
 # name, synth kwargs, frames, rotating batches, launches, strided length (0 = ragged), flags, hint
 WORKLOADS = [
     ("config2", dict(length=64), 1 << 20, 8, 20, 0, 1, 64),
-    ("1500B_udp_1M", dict(length=1500), 1 << 20, 2, 10, 0, 1, 1500),
+    ("1500B_udp_1M", dict(length=1500), 1 << 20, 2, 10, 0, 1 | 0x8, 1500),  # HALO_RX_UNIFORM_LEN, as bench.py
+    ("config4_shard_16M_64B", dict(length=64), 16 << 20, 2, 6, 0, 1, 64),
     ("config3_imix_16M", dict(size_mode=1, proto_mode=3), 16 << 20, 1, 5, 0, 1, 1500),
     ("config5_jumbo_9000B_tcp_4M_ext", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, 3, 9000, 3, 0),
+    # PacketHandle's LoChan drain (§8a row a12): 1M x 50 B TxIpv4 loopback copies, HALO_RX_L3_START
+    ("lo_drain_1M_50B", dict(length=64), 1 << 20, 1, 20, 0, 1 | 0x10, 64),
     # forward / transmit rewrite (§8f row f2): bench.TX_BENCH_STEPS on the config 2 frames
     ("tx_config2", dict(length=64), 1 << 20, 8, 20, 0, 1, 64),
     # flow-key hashing (§8f row f3): NatWanFlowHash + bucket on the parsed config 2 records
     ("flow_hash_config2", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
     # halo's packet ring (§8f row f1): the record walk over 1M 64 B records (68 MB span)
     ("ring_scan_1M_64B", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
+    # transmit construction (§8f row f2, Build*): bench.tx_build_secondary's two workloads
+    ("tx_build_udp_1M_64B", dict(length=64), 1 << 20, 1, 20, 0, 1, 22),
+    ("tx_build_udp_256k_1514B", dict(length=64), 1 << 18, 1, 10, 0, 1, 1472),
 ]
 
 
@@ -77,6 +83,47 @@ def main():
             torch.cuda.synchronize()
             print(f"{name}: {launches} walks of {used} bytes", flush=True)
             del bs, out, span, ws
+            torch.cuda.empty_cache()
+            continue
+        if name.startswith("lo_drain"):
+            from halo_amd import protocol
+
+            fb = bs[0]["bytes"][:n * 64].view(n, 64)  # uniform 64 B frames, packed
+            pk = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+            pk[:, :50] = fb[:, 14:64]  # their IPv4 packets: what Ipv4RouteForward puts in a LoChan
+            offs = torch.arange(n, dtype=torch.int32, device=dev) * 16
+            fl = torch.full((n,), 50, dtype=torch.int16, device=dev)
+            torch.cuda.synchronize()
+            for i in range(launches):
+                protocol.parse_ipv4_packets_batch(pk.reshape(-1), offs, fl, netif=netif, max_len_hint=64, out=out)
+            torch.cuda.synchronize()
+            print(f"{name}: {launches} launches of {n}", flush=True)
+            del bs, out, pk
+            torch.cuda.empty_cache()
+            continue
+        if name.startswith("tx_build"):
+            import numpy as np
+
+            from halo_amd import protocol
+            from halo_amd._lib import BUILD_DESC_DTYPE
+
+            del bs
+            plen = hint
+            stride = 64 if plen <= 22 else 1516
+            desc = np.zeros(n, BUILD_DESC_DTYPE)
+            desc["payload_off"] = np.arange(n, dtype=np.uint64) * plen
+            desc["payload_len"], desc["proto"], desc["src_port"], desc["dst_port"] = plen, 17, 1234, 5678
+            desc["src_ip"], desc["dst_ip"] = netif.ip, 0x0A000001
+            desc_d = torch.from_numpy(desc.view(np.uint8)).to(dev)
+            pay = torch.randint(0, 256, (n * plen,), dtype=torch.uint8, device=dev)
+            b = protocol.TxBuilder(n, device=dev)
+            frames = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+            fl = torch.empty(n, dtype=torch.int16, device=dev)
+            for i in range(launches):
+                b.build(desc_d, pay, netif=netif, out_stride=stride, frames=frames, lens=fl, max_payload_hint=plen)
+            torch.cuda.synchronize()
+            print(f"{name}: {launches} launches of {n}", flush=True)
+            del out, frames, pay, desc_d, b
             torch.cuda.empty_cache()
             continue
         if name.startswith("flow_hash"):
