@@ -608,13 +608,197 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
     flush_hist(p, hist);
 }
 
+// ---- Byte-stream kernel (ragged batches of mixed sizes, DESIGN.md §4.3 "stream").
+// A wave takes a window of 64 consecutive frames, one per lane. Each lane reads its frame's
+// 48-byte header and runs the header checks (as the lane kernel). The L4 segment sums then come
+// from ONE coalesced pass over the window's bytes: the wave streams [min segment start, max
+// segment end) in 4 KB steps (64 contiguous bytes per lane), and a running prefix P of the
+// 16-bit halves of every dword gives each frame's sum as P(end) - P(start). Halves sums keep the
+// sum's value mod 0xFFFF and its zero-ness, which is all fold16 looks at; the u32 difference is
+// exact for any segment (< 2^32 whatever the prefix wraps to). So every byte of a window is
+// fetched once, in full 128-byte lines, whatever the sizes, and no lane waits on a longer
+// neighbour. The step's bytes and its prefix at each 16-byte sub-chunk go to LDS; a lane whose
+// segment starts or ends in the step reads its prefix back from there. A window whose frames are
+// not dense in memory (span > 2 x their segment bytes + 8 KB) sums each frame on its own lane.
+constexpr uint32_t kStreamStep = 4096;  // bytes per wave per step: 64 lanes x 64 B
+
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_allreduce(uint32_t x, Op op) {
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppHalfMirror, 0xF, 0xF, false));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kDppMirror, 0xF, 0xF, false));
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+    return op(op(r0, r1), op(r2, r3));
+}
+
+// Exclusive prefix sum of x over the wave (lane order) and the wave total: row scans over DPP
+// row_shr, row totals by v_readlane.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane, uint32_t& total) {
+    uint32_t v = x;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15), r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47), r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    total = r0 + r1 + r2 + r3;
+    const uint32_t row = lane >> 4;
+    const uint32_t off = row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r0 + r1 : r0 + r1 + r2;
+    return v + off - x;
+}
+
+// one dword's two 16-bit halves added to acc (v_dot2_u32_u16)
+__device__ __forceinline__ uint32_t halves_acc(uint32_t w, uint32_t acc) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 one = {1, 1};
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), one, acc, false);
+}
+
+// P at step byte r, counting nb (0..4) bytes of the dword holding r: the sub-chunk's base plus
+// the halves of its dwords below r's and of the low nb bytes of r's own.
+__device__ __forceinline__ uint32_t stream_prefix(const uint32_t* s_base, const uint4* s_x, uint32_t r, uint32_t nb) {
+    const uint32_t k = r >> 4, j = (r >> 2) & 3u;
+    const uint4 q = s_x[((k & 3u) << 6) | (k >> 2)];
+    const uint32_t part = nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
+    uint32_t acc = s_base[k];
+    acc = halves_acc(q.x & (j > 0 ? 0xFFFFFFFFu : part), acc);
+    acc = halves_acc(q.y & (j > 1 ? 0xFFFFFFFFu : j == 1 ? part : 0u), acc);
+    acc = halves_acc(q.z & (j > 2 ? 0xFFFFFFFFu : j == 2 ? part : 0u), acc);
+    return halves_acc(q.w & (j == 3 ? part : 0u), acc);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#ifndef HALO_RX_STREAM_WAVES
+#define HALO_RX_STREAM_WAVES 6
+#endif
+template <int LAYOUT, int FUSE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_RX_STREAM_WAVES)))
+rx_stream_kernel(const RxParams p) {
+    __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
+    __shared__ uint4 s_x[4][kStreamStep / 16];       // per wave: the step's bytes, sub-chunk u of lane l at [u][l]
+    __shared__ uint32_t s_base[4][kStreamStep / 16];  // per wave: P at each 16-byte sub-chunk, in stream order
+    if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    Hist hist{s_hist, 0};
+    constexpr bool L3 = kL3<LAYOUT>;
+    constexpr uint32_t kSeg = kIpOff<L3> + 20u;  // L4 segment start in the frame (34 or 20)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = threadIdx.x >> 6;
+    const bool compact = (p.flags & HALO_RX_RECORD_COMPACT) != 0;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t wbase = wave * 64; wbase < p.n; wbase += nwaves * 64) {
+        const uint32_t i = wbase + lane;
+        const bool present = i < p.n;
+        FrameState<1, 3> st;
+        frame_meta<LAYOUT>(p, i, present, st);
+        frame_loads(0u, st);
+        uint32_t h[12];
+        frame_header(st, lane, h);
+        Verdict v = parse_header<L3>(h, st.L, present, p);
+        const bool seg = v.seg_end != 0;
+        uint64_t c = 0;
+        const uint64_t segs = __ballot(seg);
+        if (segs) {
+            // positions relative to a base 2^30 below the first segment frame's 128-byte line
+            const uint32_t first = (uint32_t)__builtin_ctzll(segs);
+            const uint64_t fa = reinterpret_cast<uint64_t>(st.frame);
+            const uint64_t ref = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fa >> 32), first) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fa, first)) & ~127ull;
+            const uint64_t B = ref - (1ull << 30);
+            const uint64_t d64 = fa - B;
+            const bool far = seg && d64 >= (1ull << 31);
+            const uint32_t ps = (uint32_t)d64;
+            const uint32_t pa = ps + kSeg, pe = ps + v.seg_end;  // the segment is [pa, pe)
+            const uint32_t S = wave_allreduce(seg ? pa : 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+            const uint32_t E = wave_allreduce(seg ? pe : 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+            const uint32_t lo = wave_allreduce(seg ? ps : 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+            const uint32_t hi = wave_allreduce(seg ? ps + 4 * st.ndw : 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+            const uint32_t sum = wave_allreduce(seg ? v.seg_end - kSeg : 0u, [](uint32_t a, uint32_t b) { return a + b; });
+            const uint32_t S0 = S & ~127u;
+            const uint32_t span = E - S0;
+            if (!__ballot(far) && span <= 2 * sum + 8192u) {
+                uint32_t PA = 0, PB = 0;
+                const uint32_t ea = pe - 1;  // the segment's last byte
+                const uint32_t nsteps = (span + kStreamStep - 1) / kStreamStep;
+                uint32_t carry = 0;
+                for (uint32_t t = 0; t < nsteps; ++t) {
+                    const uint32_t s0 = S0 + t * kStreamStep;
+                    const uint32_t cp = s0 + 64 * lane;
+                    gu32* g = (gu32*)(B + cp);
+                    uint32_t x[4][4];
+                    if (cp >= lo && cp + 64 <= hi) {
+                        typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const u32x4 q = *(const __attribute__((address_space(1))) u32x4*)(g + 4 * u);
+                            x[u][0] = q.x; x[u][1] = q.y; x[u][2] = q.z; x[u][3] = q.w;
+                        }
+                    } else {  // window edges: only the dwords inside [lo, hi) are read
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                const uint32_t d = cp + 16 * u + 4 * k;
+                                x[u][k] = (d >= lo && d + 4 <= hi) ? g[4 * u + k] : 0u;
+                            }
+                    }
+                    uint32_t s[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        s[u] = halves_acc(x[u][3], halves_acc(x[u][2], halves_acc(x[u][1], halves_acc(x[u][0], 0u))));
+                    uint32_t total;
+                    const uint32_t b0 = carry + wave_excl_scan(s[0] + s[1] + s[2] + s[3], lane, total);
+                    reinterpret_cast<uint4*>(s_base[w])[lane] = make_uint4(b0, b0 + s[0], b0 + s[0] + s[1], b0 + s[0] + s[1] + s[2]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) s_x[w][u * 64 + lane] = make_uint4(x[u][0], x[u][1], x[u][2], x[u][3]);
+                    carry += total;
+                    wave_lds_sync();
+                    const uint32_t ra = pa - s0, rb = ea - s0;
+                    if (seg && ra < kStreamStep) PA = stream_prefix(s_base[w], s_x[w], ra, ra & 3u);
+                    if (seg && rb < kStreamStep) PB = stream_prefix(s_base[w], s_x[w], rb, (rb & 3u) + 1u);
+                    wave_lds_sync();
+                }
+                c = (uint32_t)(PB - PA);
+            } else if (seg) {  // not dense: this lane sums its own segment
+                const uint32_t seg_dw = (v.seg_end + 3) >> 2;
+                for (uint32_t d0 = (kSeg / 4) & ~3u; d0 < seg_dw; d0 += 4) {
+                    uint32_t x[4];
+                    load4(st.frame, d0, seg_dw, x);
+                    acc_segment<L3>(x, d0, v.seg_end, c);
+                }
+            }
+        }
+        uint4* stage = reinterpret_cast<uint4*>(s_x[w]);
+        frame_store<1, FUSE, L3>(p, i, present, 0, h, v, c, hist, &stage[compact ? lane : 2 * lane]);
+        wave_lds_sync();
+        const uint32_t nrec = p.n - wbase < 64 ? p.n - wbase : 64;
+        if (compact) {
+            if (lane < nrec) store16(reinterpret_cast<uint4*>(p.out) + wbase + lane, stage[lane]);
+        } else {
+            uint4* out4 = reinterpret_cast<uint4*>(p.out) + 2ull * wbase;
+            if (lane < 2 * nrec) store16(out4 + lane, stage[lane]);
+            if (64 + lane < 2 * nrec) store16(out4 + 64 + lane, stage[64 + lane]);
+        }
+        wave_lds_sync();
+    }
+    flush_hist(p, hist);
+}
+
 #ifndef HALO_RX_MAX_BLOCKS
 #define HALO_RX_MAX_BLOCKS (256ull * 8 * 8)  // 256 CUs x 8 resident blocks x 8 rounds
 #endif
 #ifndef HALO_RX_LANE_MAX_BLOCKS
 #define HALO_RX_LANE_MAX_BLOCKS HALO_RX_MAX_BLOCKS
 #endif
-constexpr int kVariantMix = -1;
+constexpr int kVariantMix = -1, kVariantStream = 2;
 
 uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS) {
     const uint64_t waves = (n + frames_per_wave - 1) / frames_per_wave;
@@ -628,6 +812,7 @@ hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     const dim3 block(256);
     switch (variant) {
         case 1: hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64, HALO_RX_LANE_MAX_BLOCKS)), block, 0, s, p); break;
+        case kVariantStream: hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
         case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT, FUSE>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
         case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT, FUSE>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
         case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT, FUSE>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
@@ -647,6 +832,7 @@ int pick_variant(uint32_t max_len, bool uniform, uint32_t flags) {
         case HALO_RX_VARIANT_G8: return 8;
         case HALO_RX_VARIANT_G16: return 16;
         case HALO_RX_VARIANT_MIX: return kVariantMix;
+        case HALO_RX_VARIANT_STREAM: return kVariantStream;
         default: break;
     }
     if (flags & HALO_RX_UNIFORM_LEN) uniform = max_len != 0;
@@ -679,7 +865,7 @@ int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* 
     if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_RECORD_COMPACT | HALO_RX_UNIFORM_LEN |
                   HALO_RX_L3_START | HALO_RX_VARIANT_MASK))
         return HALO_E_INVAL;
-    if (((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) > HALO_RX_VARIANT_MIX) return HALO_E_INVAL;
+    if (((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) > HALO_RX_VARIANT_STREAM) return HALO_E_INVAL;
     if (reinterpret_cast<uintptr_t>(d_out) & 15u) return HALO_E_INVAL;
     p.n = n;
     p.flags = flags;

@@ -88,7 +88,9 @@ extern "C" {
  * changes): flags |= HALO_RX_VARIANT_x << HALO_RX_VARIANT_SHIFT. AUTO picks from max_len_hint /
  * the uniform length; LANE = one lane per frame; G4/G8/G16 = that many lanes per frame; MIX =
  * the size-class kernel (each wave sorts 256 frames by size and runs lane-per-frame, 4-, 8- and
- * 16-lane passes). Device parse entry points only.                                          */
+ * 16-lane passes); STREAM = the byte-stream kernel (one frame header per lane, every L4
+ * segment summed from one coalesced pass over the window's bytes). Device parse entry points
+ * only.                                                                                     */
 #define HALO_RX_VARIANT_SHIFT 8
 #define HALO_RX_VARIANT_MASK 0x700u
 #define HALO_RX_VARIANT_AUTO 0u
@@ -97,6 +99,7 @@ extern "C" {
 #define HALO_RX_VARIANT_G8 3u
 #define HALO_RX_VARIANT_G16 4u
 #define HALO_RX_VARIANT_MIX 5u
+#define HALO_RX_VARIANT_STREAM 6u
 
 /* ---- per-frame status: the FIRST failing check in reference order, 0 = OK ---------- */
 typedef enum halo_rx_status {

@@ -79,7 +79,7 @@ def test_argument_validation_without_gpu():
                                         out.ctypes.data + 4, None, None) == -1  # misaligned output
     assert L.halo_rx_parse_strided_device(buf.ctypes.data, 6, None, 60, 2, 1, n, out.ctypes.data, None,
                                           None) == -1  # stride not a multiple of 4
-    for v in (6, 7):  # HALO_RX_VARIANT_* codes end at MIX = 5
+    for v in (7,):  # HALO_RX_VARIANT_* codes end at STREAM = 6
         assert L.halo_rx_parse_batch_device(buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 1,
                                             1 | (v << _lib.HALO_RX_VARIANT_SHIFT), n, 0, out.ctypes.data, None,
                                             None) == -1

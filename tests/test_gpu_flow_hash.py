@@ -115,7 +115,7 @@ def test_flow_hash_validation(dev):
     assert L.halo_flow_hash_device(r.data_ptr(), 2, 0, 0, h.data_ptr(), 0, h.data_ptr(), None) == _lib.HALO_E_INVAL
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4, 8, 16, -1])
+@pytest.mark.parametrize("variant", [0, 1, 4, 8, 16, -1, -2])
 def test_fused_parse_flow_hash(dev, oracle_lib, golden, variant):
     """halo_rx_parse_flow_batch_device: the same records as the plain parse (full and compact),
     and the flow hashes / buckets the oracle computes from those records — golden frames, a

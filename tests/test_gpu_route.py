@@ -108,7 +108,7 @@ def test_route_lookup_from_records(dev, oracle_lib):
     assert np.array_equal(rid.cpu().numpy().view(np.uint32), o.find_batch(recs["dst_ip"]))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4, 8, 16, -1])
+@pytest.mark.parametrize("variant", [0, 1, 4, 8, 16, -1, -2])
 def test_fused_parse_route(dev, oracle_lib, golden, variant):
     """halo_rx_parse_route_batch_device: records identical to the plain parse (full and compact)
     and route ids identical to the oracle's FindRoute of each record's dst — golden frames and

@@ -27,13 +27,13 @@ def main():
     netif = NetIf.make()
     d = bench.Dist()
     workloads = [
-        ("64B", dict(length=64), 1 << 20, 8, [1, -1]),
+        ("64B", dict(length=64), 1 << 20, 8, [1, -1, -2]),
         ("64B16M", dict(length=64), 16 << 20, 1, [1]),
-        ("128B", dict(length=128), 1 << 20, 8, [1, 4, -1]),
-        ("570B", dict(length=570), 1 << 20, 2, [4, 8, -1]),
-        ("1500B", dict(length=1500), 1 << 20, 2, [4, 8, -1]),
-        ("imix", dict(size_mode=1, proto_mode=3), 16 << 20, 1, [-1, 1, 4]),
-        ("jumbo9000", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, [8, 16, -1]),
+        ("128B", dict(length=128), 1 << 20, 8, [1, 4, -1, -2]),
+        ("570B", dict(length=570), 1 << 20, 2, [4, 8, -1, -2]),
+        ("1500B", dict(length=1500), 1 << 20, 2, [4, 8, -1, -2]),
+        ("imix", dict(size_mode=1, proto_mode=3), 16 << 20, 1, [-1, -2, 1, 4]),
+        ("jumbo9000", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, [8, 16, -1, -2]),
     ]
     if quick:
         workloads = workloads[:2] + workloads[3:5]
