@@ -660,7 +660,7 @@ __device__ __forceinline__ uint32_t halves_acc(uint32_t w, uint32_t acc) {
 // the halves of its dwords below r's and of the low nb bytes of r's own.
 __device__ __forceinline__ uint32_t stream_prefix(const uint32_t* s_base, const uint4* s_x, uint32_t r, uint32_t nb) {
     const uint32_t k = r >> 4, j = (r >> 2) & 3u;
-    const uint4 q = s_x[((k & 3u) << 6) | (k >> 2)];
+    const uint4 q = s_x[k];
     const uint32_t part = nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
     uint32_t acc = s_base[k];
     acc = halves_acc(q.x & (j > 0 ? 0xFFFFFFFFu : part), acc);
@@ -675,99 +675,225 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Stream origin alignment (bytes; the first step starts at the window's lowest byte rounded
+// down to it). Measured and removed (profiles/r02/stream/stream1-3.log): software-pipelining the
+// step loads (+16 VGPRs: 570 B 132 -> 156 us), issuing the next step's loads before this step's
+// lookups, and prefetching the next window's addresses / headers (neutral or slower).
+#ifndef HALO_RX_STREAM_ALIGN
+#define HALO_RX_STREAM_ALIGN 128
+#endif
+
+// This lane's 64 bytes of the step at s0 (sub-chunk u at s0 + 1024u + 16 lane, so each load
+// instruction reads 1 KB contiguous): always four 16-byte loads, no branch, so the load counter
+// stays exact across steps. Positions are 16-byte aligned in memory, and a 16-byte aligned block
+// never straddles a page, so a block holding any byte of the window's frames [lo, hi) is
+// readable; a sub-chunk wholly outside reads the nearest such block instead. Bytes outside the
+// frames are never inside a segment or header, and P differences cancel them.
+__device__ __forceinline__ void stream_load(uint64_t B, uint32_t s0, uint32_t lane, uint32_t lo, uint32_t hi,
+                                            uint32_t (&x)[4][4]) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(16)));
+    const uint32_t first = lo & ~15u, last = (hi - 1u) & ~15u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        uint32_t a = s0 + 1024u * u + 16 * lane;
+        a = a < first ? first : a > last ? last : a;
+        const u32x4 q = *(const __attribute__((address_space(1))) u32x4*)(B + a);
+        x[u][0] = q.x; x[u][1] = q.y; x[u][2] = q.z; x[u][3] = q.w;
+    }
+}
+
 #ifndef HALO_RX_STREAM_WAVES
 #define HALO_RX_STREAM_WAVES 6
 #endif
-template <int LAYOUT, int FUSE>
+#ifndef HALO_RX_STREAM_PIPE  // 1: the next step's loads issued before this step is summed
+#define HALO_RX_STREAM_PIPE 0
+#endif
+#ifndef HALO_RX_STREAM_HDR
+#define HALO_RX_STREAM_HDR 1
+#endif
+
+// One stream step's 64 bytes of this lane: their 16-byte sub-chunk prefixes (P at each sub-chunk
+// start; carry = P at the step start) and the bytes, to the wave's LDS.
+__device__ __forceinline__ void stream_sum(const uint32_t (&x)[4][4], uint32_t lane, uint32_t& carry,
+                                           uint32_t* s_base, uint4* s_x) {
+    uint32_t s[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        s[u] = halves_acc(x[u][3], halves_acc(x[u][2], halves_acc(x[u][1], halves_acc(x[u][0], 0u))));
+    uint32_t total;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // sub-chunk k = 64u + lane in stream order
+        s_base[u * 64 + lane] = carry + wave_excl_scan(s[u], lane, total);
+        carry += total;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s_x[u * 64 + lane] = make_uint4(x[u][0], x[u][1], x[u][2], x[u][3]);
+    wave_lds_sync();
+}
+
+// HDR (chosen per call: checksums on): the headers come out of the stream too. Each lane copies
+// its frame's 48 header bytes from the step buffer as the stream passes them, and its segment end
+// follows from the IPv4 total length (the parse's seg_end = O + totalLen) as soon as that field
+// has passed; the header checks run once after the stream. Every byte of a dense window is then
+// fetched from HBM exactly once. Without HDR (checksums off: only ICMP frames have a segment),
+// the lane reads its header first and the stream covers only the windows' segments.
+template <int LAYOUT, int FUSE, bool HDR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_RX_STREAM_WAVES)))
 rx_stream_kernel(const RxParams p) {
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
-    __shared__ uint4 s_x[4][kStreamStep / 16];       // per wave: the step's bytes, sub-chunk u of lane l at [u][l]
-    __shared__ uint32_t s_base[4][kStreamStep / 16];  // per wave: P at each 16-byte sub-chunk, in stream order
+    __shared__ uint4 s_x[4][kStreamStep / 16];       // per wave: the step's bytes (records at the end)
+    __shared__ uint32_t s_base[4][kStreamStep / 16];  // per wave: P at each 16-byte sub-chunk
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
     Hist hist{s_hist, 0};
     constexpr bool L3 = kL3<LAYOUT>;
-    constexpr uint32_t kSeg = kIpOff<L3> + 20u;  // L4 segment start in the frame (34 or 20)
+    constexpr uint32_t O = kIpOff<L3>;
+    constexpr uint32_t kSeg = O + 20u;        // L4 segment start in the frame (34 or 20)
+    constexpr uint32_t kTlDw = (O + 2u) / 4u;  // the header dword holding the IPv4 total length
+    constexpr uint32_t kNone = 0xFFFFFFFFu;    // a position no step holds
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = threadIdx.x >> 6;
     const bool compact = (p.flags & HALO_RX_RECORD_COMPACT) != 0;
+    const bool aligned = (reinterpret_cast<uint64_t>(p.bytes) & 3u) == 0;  // positions are dword-exact
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const auto umin = [](uint32_t a, uint32_t b) { return a < b ? a : b; };
+    const auto umax = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+    const auto uadd = [](uint32_t a, uint32_t b) { return a + b; };
     for (uint32_t wbase = wave * 64; wbase < p.n; wbase += nwaves * 64) {
         const uint32_t i = wbase + lane;
         const bool present = i < p.n;
         FrameState<1, 3> st;
         frame_meta<LAYOUT>(p, i, present, st);
-        frame_loads(0u, st);
         uint32_t h[12];
-        frame_header(st, lane, h);
-        Verdict v = parse_header<L3>(h, st.L, present, p);
-        const bool seg = v.seg_end != 0;
+        Verdict v;
         uint64_t c = 0;
-        const uint64_t segs = __ballot(seg);
-        if (segs) {
-            // positions relative to a base 2^30 below the first segment frame's 128-byte line
-            const uint32_t first = (uint32_t)__builtin_ctzll(segs);
-            const uint64_t fa = reinterpret_cast<uint64_t>(st.frame);
-            const uint64_t ref = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fa >> 32), first) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fa, first)) & ~127ull;
-            const uint64_t B = ref - (1ull << 30);
-            const uint64_t d64 = fa - B;
-            const bool far = seg && d64 >= (1ull << 31);
-            const uint32_t ps = (uint32_t)d64;
-            const uint32_t pa = ps + kSeg, pe = ps + v.seg_end;  // the segment is [pa, pe)
-            const uint32_t S = wave_allreduce(seg ? pa : 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
-            const uint32_t E = wave_allreduce(seg ? pe : 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
-            const uint32_t lo = wave_allreduce(seg ? ps : 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
-            const uint32_t hi = wave_allreduce(seg ? ps + 4 * st.ndw : 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
-            const uint32_t sum = wave_allreduce(seg ? v.seg_end - kSeg : 0u, [](uint32_t a, uint32_t b) { return a + b; });
-            const uint32_t S0 = S & ~127u;
-            const uint32_t span = E - S0;
-            if (!__ballot(far) && span <= 2 * sum + 8192u) {
-                uint32_t PA = 0, PB = 0;
-                const uint32_t ea = pe - 1;  // the segment's last byte
-                const uint32_t nsteps = (span + kStreamStep - 1) / kStreamStep;
-                uint32_t carry = 0;
-                for (uint32_t t = 0; t < nsteps; ++t) {
-                    const uint32_t s0 = S0 + t * kStreamStep;
-                    const uint32_t cp = s0 + 64 * lane;
-                    gu32* g = (gu32*)(B + cp);
-                    uint32_t x[4][4];
-                    if (cp >= lo && cp + 64 <= hi) {
-                        typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+        bool done = false;  // wave-uniform: the window went through the stream
+        if constexpr (HDR) {
+            const bool rd = st.ndw != 0;
+            const uint64_t rds = __ballot(rd);
+            if (rds && aligned) {
+                // positions relative to a base 2^30 below the first readable frame's 128-byte line
+                const uint32_t first = (uint32_t)__builtin_ctzll(rds);
+                const uint64_t fa = reinterpret_cast<uint64_t>(st.frame);
+                const uint64_t ref = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fa >> 32), first) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fa, first)) & ~127ull;
+                const uint64_t B = ref - (1ull << 30);
+                const uint64_t d64 = fa - B;
+                const uint32_t ps = (uint32_t)d64;
+                const uint32_t lo = wave_allreduce(rd ? ps : kNone, umin);
+                const uint32_t hi = wave_allreduce(rd ? ps + 4 * st.ndw : 0u, umax);
+                const uint32_t sum = wave_allreduce(rd ? st.L : 0u, uadd);
+                const uint32_t G0 = lo & ~(uint32_t)(HALO_RX_STREAM_ALIGN - 1);
+                const uint32_t span = hi - G0;
+                if (!__ballot(rd && d64 >= (1ull << 31)) && span <= 2 * sum + 8192u) {
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const u32x4 q = *(const __attribute__((address_space(1))) u32x4*)(g + 4 * u);
-                            x[u][0] = q.x; x[u][1] = q.y; x[u][2] = q.z; x[u][3] = q.w;
-                        }
-                    } else {  // window edges: only the dwords inside [lo, hi) are read
+                    for (int j = 0; j < 12; ++j) h[j] = 0;
+                    const uint32_t pa = ps + kSeg;
+                    uint32_t pb = kNone;  // the segment's last byte, once the total length has passed
+                    uint32_t PA = 0, PB = 0, carry = 0;
+                    const uint32_t nsteps = (span + kStreamStep - 1) / kStreamStep;
+#if HALO_RX_STREAM_PIPE
+                    uint32_t x[4][4];
+                    stream_load(B, G0, lane, lo, hi, x);
+#endif
+                    for (uint32_t t = 0; t < nsteps; ++t) {
+                        const uint32_t s0 = G0 + t * kStreamStep;
+#if HALO_RX_STREAM_PIPE
+                        uint32_t xn[4][4];  // the next step's bytes (past the window: a clamped re-read)
+                        stream_load(B, s0 + kStreamStep, lane, lo, hi, xn);
+                        stream_sum(x, lane, carry, s_base[w], s_x[w]);
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
 #pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                const uint32_t d = cp + 16 * u + 4 * k;
-                                x[u][k] = (d >= lo && d + 4 <= hi) ? g[4 * u + k] : 0u;
+                            for (int k = 0; k < 4; ++k) x[u][k] = xn[u][k];
+#else
+                        uint32_t x[4][4];
+                        stream_load(B, s0, lane, lo, hi, x);
+                        stream_sum(x, lane, carry, s_base[w], s_x[w]);
+#endif
+                        const uint32_t* xw = reinterpret_cast<const uint32_t*>(s_x[w]);
+                        const uint32_t r0 = ps - s0;  // header start in this step (wraps below it)
+                        if (__ballot(rd && (r0 < kStreamStep || r0 + 48u < 48u + kStreamStep))) {
+#pragma unroll
+                            for (int j = 0; j < 12; ++j) {
+                                const uint32_t r = r0 + 4u * j;
+                                const uint32_t wv = xw[(r >> 2) & (kStreamStep / 4 - 1)];
+                                if (rd && r < kStreamStep && (uint32_t)j < st.ndw) h[j] = wv;
                             }
+                            if (rd && pb == kNone && r0 + 4u * kTlDw < kStreamStep && kTlDw < st.ndw) {
+                                const uint32_t tl = L3 ? bswap16(h[0] >> 16) : bswap16(h[kTlDw] & 0xFFFFu);
+                                pb = (tl >= 20u && O + tl <= st.L) ? ps + O + tl - 1u : kNone - 1u;
+                            }
+                        }
+                        const uint32_t ra = pa - s0, rb = pb - s0;
+                        if (rd && ra < kStreamStep) PA = stream_prefix(s_base[w], s_x[w], ra, ra & 3u);
+                        if (rd && rb < kStreamStep) PB = stream_prefix(s_base[w], s_x[w], rb, (rb & 3u) + 1u);
+                        wave_lds_sync();
                     }
-                    uint32_t s[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        s[u] = halves_acc(x[u][3], halves_acc(x[u][2], halves_acc(x[u][1], halves_acc(x[u][0], 0u))));
-                    uint32_t total;
-                    const uint32_t b0 = carry + wave_excl_scan(s[0] + s[1] + s[2] + s[3], lane, total);
-                    reinterpret_cast<uint4*>(s_base[w])[lane] = make_uint4(b0, b0 + s[0], b0 + s[0] + s[1], b0 + s[0] + s[1] + s[2]);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) s_x[w][u * 64 + lane] = make_uint4(x[u][0], x[u][1], x[u][2], x[u][3]);
-                    carry += total;
-                    wave_lds_sync();
-                    const uint32_t ra = pa - s0, rb = ea - s0;
-                    if (seg && ra < kStreamStep) PA = stream_prefix(s_base[w], s_x[w], ra, ra & 3u);
-                    if (seg && rb < kStreamStep) PB = stream_prefix(s_base[w], s_x[w], rb, (rb & 3u) + 1u);
-                    wave_lds_sync();
+                    v = parse_header<L3>(h, st.L, present, p);
+                    if (v.seg_end) c = (uint32_t)(PB - PA);
+                    done = true;
                 }
-                c = (uint32_t)(PB - PA);
-            } else if (seg) {  // not dense: this lane sums its own segment
+            }
+        }
+        if (!done) {
+            frame_loads(0u, st);
+            frame_header(st, lane, h);
+            v = parse_header<L3>(h, st.L, present, p);
+            const bool seg = v.seg_end != 0;
+            const uint64_t segs = __ballot(seg);
+            bool streamed = false;
+            if (!HDR && segs && aligned) {
+                // positions relative to a base 2^30 below the first segment frame's 128-byte line
+                const uint32_t first = (uint32_t)__builtin_ctzll(segs);
+                const uint64_t fa = reinterpret_cast<uint64_t>(st.frame);
+                const uint64_t ref = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fa >> 32), first) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fa, first)) & ~127ull;
+                const uint64_t B = ref - (1ull << 30);
+                const uint64_t d64 = fa - B;
+                const uint32_t ps = (uint32_t)d64;
+                const uint32_t pa = ps + kSeg, pe = ps + v.seg_end;  // the segment is [pa, pe)
+                const uint32_t S = wave_allreduce(seg ? pa : kNone, umin);
+                const uint32_t E = wave_allreduce(seg ? pe : 0u, umax);
+                const uint32_t lo = wave_allreduce(seg ? ps : kNone, umin);
+                const uint32_t hi = wave_allreduce(seg ? ps + 4 * st.ndw : 0u, umax);
+                const uint32_t sum = wave_allreduce(seg ? v.seg_end - kSeg : 0u, uadd);
+                const uint32_t G0 = S & ~(uint32_t)(HALO_RX_STREAM_ALIGN - 1);
+                const uint32_t span = E - G0;
+                if (!__ballot(seg && d64 >= (1ull << 31)) && span <= 2 * sum + 8192u) {
+                    uint32_t PA = 0, PB = 0, carry = 0;
+                    const uint32_t ea = pe - 1;  // the segment's last byte
+                    const uint32_t nsteps = (span + kStreamStep - 1) / kStreamStep;
+#if HALO_RX_STREAM_PIPE
+                    uint32_t x[4][4];
+                    stream_load(B, G0, lane, lo, hi, x);
+#endif
+                    for (uint32_t t = 0; t < nsteps; ++t) {
+                        const uint32_t s0 = G0 + t * kStreamStep;
+#if HALO_RX_STREAM_PIPE
+                        uint32_t xn[4][4];  // the next step's bytes (past the window: a clamped re-read)
+                        stream_load(B, s0 + kStreamStep, lane, lo, hi, xn);
+                        stream_sum(x, lane, carry, s_base[w], s_x[w]);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) x[u][k] = xn[u][k];
+#else
+                        uint32_t x[4][4];
+                        stream_load(B, s0, lane, lo, hi, x);
+                        stream_sum(x, lane, carry, s_base[w], s_x[w]);
+#endif
+                        const uint32_t ra = pa - s0, rb = ea - s0;
+                        if (seg && ra < kStreamStep) PA = stream_prefix(s_base[w], s_x[w], ra, ra & 3u);
+                        if (seg && rb < kStreamStep) PB = stream_prefix(s_base[w], s_x[w], rb, (rb & 3u) + 1u);
+                        wave_lds_sync();
+                    }
+                    c = (uint32_t)(PB - PA);
+                    streamed = true;
+                }
+            }
+            if (seg && !streamed) {  // not dense (or unaligned data): this lane sums its own segment
                 const uint32_t seg_dw = (v.seg_end + 3) >> 2;
                 for (uint32_t d0 = (kSeg / 4) & ~3u; d0 < seg_dw; d0 += 4) {
                     uint32_t x[4];
@@ -812,7 +938,12 @@ hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     const dim3 block(256);
     switch (variant) {
         case 1: hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64, HALO_RX_LANE_MAX_BLOCKS)), block, 0, s, p); break;
-        case kVariantStream: hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64)), block, 0, s, p); break;
+        case kVariantStream:
+            if (HALO_RX_STREAM_HDR && (p.flags & HALO_RX_CSUM_ENABLE))
+                hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, true>), dim3(grid_for(p.n, 64)), block, 0, s, p);
+            else
+                hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, false>), dim3(grid_for(p.n, 64)), block, 0, s, p);
+            break;
         case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT, FUSE>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
         case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT, FUSE>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
         case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT, FUSE>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
@@ -821,11 +952,12 @@ hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Kernel variant (from the sweeps in profiles/r01/tune_*.log): a variant named in
-// the call's flags wins; a known uniform length (strided with one length, or a ragged batch flagged
-// HALO_RX_UNIFORM_LEN) picks the best lanes-per-frame; a ragged batch whose frames are all <= 64 B
-// goes lane per frame, and any other ragged batch goes to the size-class mix kernel.
-int pick_variant(uint32_t max_len, bool uniform, uint32_t flags) {
+// Kernel variant (from the sweeps in profiles/r01/tune_*.log and
+// profiles/r02/stream/): a variant named in the call's flags wins; frames all <= 64 B go lane
+// per frame; frames packed densely in memory (ragged layouts, or strided with little slack)
+// up to 1 KB, or of mixed sizes, take the byte-stream kernel; longer uniform frames take 8 or 16
+// lanes per frame; mixed sizes that are not dense take the size-class mix kernel.
+int pick_variant(uint32_t max_len, bool uniform, bool dense, uint32_t flags) {
     switch ((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) {
         case HALO_RX_VARIANT_LANE: return 1;
         case HALO_RX_VARIANT_G4: return 4;
@@ -837,15 +969,18 @@ int pick_variant(uint32_t max_len, bool uniform, uint32_t flags) {
     }
     if (flags & HALO_RX_UNIFORM_LEN) uniform = max_len != 0;
     if (max_len != 0 && max_len <= 64) return 1;
-    if (!uniform) return kVariantMix;
-    if (max_len <= 128) return 1;
-    if (max_len <= 1024) return 4;
+    if (!uniform) return dense ? kVariantStream : kVariantMix;
+    if (max_len <= 1024) return dense ? kVariantStream : max_len <= 128 ? 1 : 4;
     if (max_len <= 4096) return 8;
     return 16;
 }
 
 int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, hipStream_t s) {
-    const int v = pick_variant(max_len, uniform, p.flags);
+    // ragged batches are taken as packed back to back (the stream kernel checks each window and
+    // sums a sparse one frame by frame); strided frames of one length are dense when the stride
+    // wastes < 1/4; strided frames with their own lengths may be anything below the stride
+    const bool dense = layout == 0 || layout == 3 || (layout == 2 && p.stride <= max_len + max_len / 4 + 64);
+    const int v = pick_variant(max_len, uniform, dense, p.flags);
     hipError_t e;
     switch (layout) {
         case 0:  // ragged: the only layout with the fused passes

@@ -40,6 +40,9 @@ def main():
     if "--only" in sys.argv:
         keep = sys.argv[sys.argv.index("--only") + 1].split(",")
         workloads = [w for w in workloads if w[0] in keep]
+    if "--variants" in sys.argv:  # e.g. --variants=-2 (one kernel variant for every workload)
+        only = [int(x) for x in sys.argv[sys.argv.index("--variants") + 1].split(",")]
+        workloads = [(a, b, c, d, only) for a, b, c, d, _ in workloads]
     res = {}
     for name, kw, n, rot, gs in workloads:
         bs = bench.make_batches(dev, netif, n=n, rotate=rot, rank=0, **kw)
