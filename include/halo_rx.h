@@ -36,7 +36,9 @@
  *              long. u32 dword offsets address 16 GiB per call.
  *   - strided: frame i starts at bytes + i*stride (stride a multiple of 4), length
  *              lens[i] or, when lens == NULL, the uniform length `len`.
- *   The kernel never reads past the 4-byte word that holds a frame's last byte.
+ *   The kernels read no page that holds no frame byte: the per-frame kernels never read past
+ *   the 4-byte word holding a frame's last byte; the byte-stream kernel (HALO_RX_VARIANT_STREAM)
+ *   reads whole 16-byte-aligned blocks between a window's lowest and highest frame bytes.
  */
 #ifndef HALO_RX_H
 #define HALO_RX_H
