@@ -284,18 +284,31 @@ __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t s
 // descriptor i of the tile and decides it; the wave's ballot ranks the rejections; then the
 // wave builds the tile's frames 64 / G at a time, G lanes per frame, each group taking its
 // descriptor's dwords from the lane that holds them (ds_bpermute). No LDS, no barrier.
+#ifndef HALO_TXB_DESC_PREFETCH
+#define HALO_TXB_DESC_PREFETCH 0
+#endif
+#ifndef HALO_TXB_G1_WAVES
+#define HALO_TXB_G1_WAVES 6
+#endif
 template <int G, int U>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) tx_build_kernel(const BuildParams p) {
-    __shared__ uint32_t s_desc[kBlock / 64][kTile * 10 + 1];  // per wave: its tile's descriptors
-    __shared__ uint32_t s_meta[kBlock / 64][kTile];
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G == 1 ? HALO_TXB_G1_WAVES : 4)))
+tx_build_kernel(const BuildParams p) {
+#ifndef HALO_TXB_G1_LDS_TRIM
+#define HALO_TXB_G1_LDS_TRIM 1
+#endif
+    // the descriptor staging is only for G > 1 (a lane per frame keeps its own): 11 KB less LDS
+    // per block, so the lane-per-frame build fits eight blocks per CU
+    constexpr uint32_t kDescDw = (G > 1 || !HALO_TXB_G1_LDS_TRIM) ? kTile * 10 + 1 : 1;
+    constexpr uint32_t kMetaDw = (G > 1 || !HALO_TXB_G1_LDS_TRIM) ? kTile : 1;
+    __shared__ uint32_t s_desc[kBlock / 64][kDescDw];  // per wave: its tile's descriptors
+    __shared__ uint32_t s_meta[kBlock / 64][kMetaDw];
     __shared__ uint32_t s_hdr[kBlock / 64][kTile * 16 + 1];  // per wave: frame-layout header dwords 0..15
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t nw = (gridDim.x * kBlock) >> 6;
     const uint32_t base = *p.ip_id;
     const uint32_t g = lane / G, j = lane % G;
-    for (uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 6; t < p.n_tiles; t += nw) {
-        const uint32_t first = t * kTile, i = first + lane;
-        uint32_t d[10];
+    // descriptor i's ten dwords (zeros past the batch)
+    auto load_desc = [&](uint32_t i, uint32_t (&d)[10]) {
         if (i < p.n) {
             const uint2* src = reinterpret_cast<const uint2*>(p.desc + i);
 #pragma unroll
@@ -307,6 +320,22 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         } else {
 #pragma unroll
             for (int k = 0; k < 10; ++k) d[k] = 0u;
+        }
+    };
+    // G = 1: the next tile's descriptors load while this tile builds (one dependent round trip
+    // fewer per tile; +10 VGPRs)
+    constexpr bool kPf = G == 1 && HALO_TXB_DESC_PREFETCH;
+    uint32_t dn[10];
+    if constexpr (kPf) load_desc(((blockIdx.x * kBlock + threadIdx.x) >> 6) * kTile + lane, dn);
+    for (uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 6; t < p.n_tiles; t += nw) {
+        const uint32_t first = t * kTile, i = first + lane;
+        uint32_t d[10];
+        if constexpr (kPf) {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) d[k] = dn[k];
+            load_desc((t + nw) * kTile + lane, dn);
+        } else {
+            load_desc(i, d);
         }
         uint32_t flen = 0;
         const uint32_t code = i < p.n ? verdict(d[2], d[9], p.stride, flen) : HALO_TX_B_PROTO;
@@ -471,8 +500,11 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
     p.mac_hi = (uint32_t)netif->mac[4] | ((uint32_t)netif->mac[5] << 8);
     hipStream_t s = static_cast<hipStream_t>(stream);
     // a wave per tile of 64 descriptors, grid-stride: up to 8 resident 4-wave blocks per CU
+#ifndef HALO_TXB_MAX_BLOCKS
+#define HALO_TXB_MAX_BLOCKS 1536u  // 6 waves x 1024 SIMDs / 4 waves per block: one resident round
+#endif
     const uint32_t waves = p.n_tiles, blocks = (waves + 3) / 4;
-    const dim3 grid(blocks < 2048u ? blocks : 2048u), blk(halo::kBlock);
+    const dim3 grid(blocks < HALO_TXB_MAX_BLOCKS ? blocks : HALO_TXB_MAX_BLOCKS), blk(halo::kBlock);
     // lanes per frame and chunks per lane from the largest frame expected (a frame needs
     // ceil(flen / 16) chunks; longer ones than G * U chunks take extra rounds)
     const uint32_t h = max_payload_hint ? max_payload_hint : 1472u;
