@@ -267,6 +267,78 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
     }
 }
 
+// Bytes [0, n) of a dword as a mask, n clamped to 0..4.
+__device__ __forceinline__ uint32_t prefix_mask(int32_t n) {
+    const uint32_t c = (uint32_t)(n < 0 ? 0 : n > 4 ? 4 : n);
+    return (uint32_t)((1ull << (8 * c)) - 1ull);
+}
+
+// A lane's whole frame when it fits in 64 bytes (G = 1): the sixteen output dwords built in
+// registers with no per-dword branch. Payload dwords come from ten aligned source loads (output
+// dword k takes bytes from sources k and k + 1: the payload lies at frame bytes >= 28 in every
+// layout, so sources 7..16 cover it), each address clamped into the payload's readable dwords —
+// a clamped value lands only in bytes the masks drop. Header bytes [0, hdr_end) from the lane's
+// header dwords, payload [hdr_end, pay_end), zero padding after; the L4 segment summed with one
+// v_dot2 per dword; four 16-byte stores (single dwords only for a frame that ends mid-chunk).
+__device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f, const uint32_t* hdr, uint8_t* out,
+                                            const void* safe) {
+    const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
+    const uint32_t H = f.hdr_end, PE = f.hdr_end + f.plen, ndw = (f.flen + 3u) >> 2;
+    const uint64_t sv = f.pay - H;  // virtual address of frame byte 0 in payload space
+    const uint32_t sh = (uint32_t)(sv & 3u);
+    const uint64_t sb = sv - sh;
+    const uint64_t lo = f.pay & ~3ull, hi = (f.pay + f.plen + 3u) & ~3ull;  // readable dwords [lo, hi)
+    typedef const __attribute__((address_space(1))) uint32_t gu32_t;
+    uint32_t src[10];  // source dwords 7..16
+#pragma unroll
+    for (int m = 0; m < 10; ++m) {
+        uint64_t a = sb + 4u * (7u + m);
+        a = a < lo ? lo : a;
+        a = a + 4u > hi ? hi - 4u : a;
+        src[m] = *(gu32_t*)(f.plen ? a : reinterpret_cast<uint64_t>(safe));
+    }
+    uint32_t o[16];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) o[k] = hdr[k];  // bytes < 28 <= hdr_end: header only
+#pragma unroll
+    for (int k = 7; k < 16; ++k) {
+        const uint32_t pay = __builtin_amdgcn_alignbyte(src[k - 6 < 10 ? k - 6 : 9], src[k - 7], sh);
+        const uint32_t hm = prefix_mask((int32_t)H - 4 * k), pm = prefix_mask((int32_t)PE - 4 * k);
+        o[k] = (k < 14 ? hdr[k] & hm : 0u) | (pay & pm & ~hm);
+    }
+    // L4 segment [base + 20, pay_end): everything past it is already zero
+    const bool l3 = f.base == 0;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 5; k < 16; ++k) {
+        const uint32_t seg = k >= 9 ? 0xFFFFFFFFu : k == 8 ? (l3 ? 0xFFFFFFFFu : 0xFFFF0000u) : (l3 ? 0xFFFFFFFFu : 0u);
+        sum = hsum_acc(o[k] & seg, sum);
+    }
+    uint32_t part = fold16(sum), ck_at;
+    if (f.proto == kIpUdp || f.proto == kIpTcp) {
+        const uint32_t s = bswap32(f.src), t = bswap32(f.dst);
+        part += hsum(s) + hsum(t) + (f.proto << 8) + bswap16(f.l4hdr + f.plen);
+        ck_at = f.base + 20u + (f.proto == kIpUdp ? 6u : 16u);
+    } else {
+        ck_at = f.base + 22u;
+    }
+    const uint32_t ck_le = (csum || f.proto == kIpIcmp) ? (~fold16(part)) & 0xFFFFu : 0u;
+    const uint32_t ck_dw = ck_at >> 2, ck_v = ck_le << ((ck_at & 2u) * 8u);
+#pragma unroll
+    for (int k = 5; k < 13; ++k) o[k] |= (uint32_t)k == ck_dw ? ck_v : 0u;
+    uint32_t* ow = reinterpret_cast<uint32_t*>(out);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (4u * c + 4u <= ndw) {
+            *reinterpret_cast<uint4*>(ow + 4 * c) = make_uint4(o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (4u * c + i < ndw) ow[4 * c + i] = o[4 * c + i];
+        }
+    }
+}
+
 // BuildUdpPkt / BuildTcpPkt / BuildIcmpPkt's length limits and the slot check (build-defined):
 // HALO_TX_B_* of a descriptor (its dwords 2 and 9) and its frame length.
 __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t stride, uint32_t& flen) {
@@ -284,11 +356,14 @@ __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t s
 // descriptor i of the tile and decides it; the wave's ballot ranks the rejections; then the
 // wave builds the tile's frames 64 / G at a time, G lanes per frame, each group taking its
 // descriptor's dwords from the lane that holds them (ds_bpermute). No LDS, no barrier.
+#ifndef HALO_TXB_SMALL  // 1: frames <= 64 B on the branch-free lane path (build_small)
+#define HALO_TXB_SMALL 1
+#endif
 #ifndef HALO_TXB_DESC_PREFETCH
 #define HALO_TXB_DESC_PREFETCH 0
 #endif
 #ifndef HALO_TXB_G1_WAVES
-#define HALO_TXB_G1_WAVES 6
+#define HALO_TXB_G1_WAVES 4
 #endif
 template <int G, int U>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G == 1 ? HALO_TXB_G1_WAVES : 4)))
@@ -358,8 +433,12 @@ tx_build_kernel(const BuildParams p) {
         }
         if constexpr (G == 1) {
             __builtin_amdgcn_wave_barrier();
-            if (mine >> 31)
-                build_frame<G, U>(p, decode(d, p.payload), &s_hdr[wv][16 * lane], 0, p.frames + (uint64_t)i * p.stride);
+            if (mine >> 31) {
+                const Frame f = decode(d, p.payload);
+                uint8_t* o = p.frames + (uint64_t)i * p.stride;
+                if (HALO_TXB_SMALL && f.flen <= 64u) build_small(p, f, &s_hdr[wv][16 * lane], o, p.desc + i);
+                else build_frame<G, U>(p, f, &s_hdr[wv][16 * lane], 0, o);
+            }
             __builtin_amdgcn_wave_barrier();
         } else {
             // the wave's descriptors through its own LDS region (no block barrier), so that they
@@ -501,7 +580,7 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
     hipStream_t s = static_cast<hipStream_t>(stream);
     // a wave per tile of 64 descriptors, grid-stride: up to 8 resident 4-wave blocks per CU
 #ifndef HALO_TXB_MAX_BLOCKS
-#define HALO_TXB_MAX_BLOCKS 1536u  // 6 waves x 1024 SIMDs / 4 waves per block: one resident round
+#define HALO_TXB_MAX_BLOCKS (HALO_TXB_G1_WAVES * 256u)  // waves x 1024 SIMDs / 4 per block: one resident round
 #endif
     const uint32_t waves = p.n_tiles, blocks = (waves + 3) / 4;
     const dim3 grid(blocks < HALO_TXB_MAX_BLOCKS ? blocks : HALO_TXB_MAX_BLOCKS), blk(halo::kBlock);
