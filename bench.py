@@ -799,8 +799,8 @@ def e2e_host(dev, netif, steps: int):
         out.view(np.uint8)[:] = 0  # touched once: no page faults in the timed loop
         lens = own_pages(np.ascontiguousarray(lay["lens"]))
         for registered in (True, False):
-            # registered: frames, offsets, lengths and the record array all pinned in place (the
-            # offsets then become dword offsets on the GPU, no per-frame host loop)
+            # registered: frames, offsets, lengths and the record array all pinned in place (one
+            # DMA per chunk straight from the caller's frames; the host converts the offsets)
             pinned = (host, offs, lens, out) if registered else ()
             with contextlib.ExitStack() as regs:  # unregistered on exit, checked, even on error
                 for a in pinned:
