@@ -19,7 +19,10 @@
 // G = 64, ds_bpermute otherwise); every lane then runs the header checks redundantly (no
 // divergence, no second broadcast). Only the L4 segment sum needs a cross-lane reduction
 // (DPP butterflies). G = 1 (small frames): each lane owns a whole frame, reads its header with
-// its own three 16-byte loads and needs no cross-lane traffic at all.
+// its own three 16-byte loads and needs no cross-lane traffic at all. Mixed sizes packed in
+// memory (IMIX) take the byte-stream kernel (rx_stream_kernel below): a lane per frame for the
+// header, the whole wave for one coalesced pass over the window's bytes, and every L4 sum as a
+// difference of a running prefix.
 //
 // Checksum arithmetic (DESIGN.md "Checksum in the little-endian domain"): the frame is summed
 // as little-endian dwords. A one's-complement sum of byte-swapped 16-bit words is the byte
