@@ -422,26 +422,32 @@ tx_build_kernel(const BuildParams p) {
             __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
         // iphId++ then use (ipv4.go:103-104); rejections in earlier tiles settled by launches 2/3
         const uint32_t mine = (i < p.n && !rej) ? 0x80000000u | ((base + 1u + i - before) & 0xFFFFu) : 0u;
-        {  // this lane's descriptor's header (Ethernet layout, or the loopback bytes from 14 on)
+        uint32_t hv[16];  // this lane's descriptor's header (Ethernet layout, or the loopback bytes from 14 on)
+        {
             const Frame f = decode(d, p.payload);
             const uint32_t id = mine & 0xFFFFu;
             uint32_t e[18];
             eth_header(f, id, ipv4_cksum(f, id, (p.flags & HALO_RX_CSUM_ENABLE) != 0), p, e);
             const bool l3 = f.mode == HALO_TX_BUILD_LOOPBACK;
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                s_hdr[wv][16 * lane + k] = k >= 14 ? 0u : l3 ? ((e[k + 3] >> 16) | (e[k + 4] << 16)) : e[k];
+            for (int k = 0; k < 16; ++k) hv[k] = k >= 14 ? 0u : l3 ? ((e[k + 3] >> 16) | (e[k + 4] << 16)) : e[k];
         }
         if constexpr (G == 1) {
-            __builtin_amdgcn_wave_barrier();
+            // a frame of <= 64 B keeps its header in registers; longer ones read it from LDS
             if (mine >> 31) {
                 const Frame f = decode(d, p.payload);
                 uint8_t* o = p.frames + (uint64_t)i * p.stride;
-                if (HALO_TXB_SMALL && f.flen <= 64u) build_small(p, f, &s_hdr[wv][16 * lane], o, p.desc + i);
-                else build_frame<G, U>(p, f, &s_hdr[wv][16 * lane], 0, o);
+                if (HALO_TXB_SMALL && f.flen <= 64u) {
+                    build_small(p, f, hv, o, p.desc + i);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) s_hdr[wv][16 * lane + k] = hv[k];
+                    build_frame<G, U>(p, f, &s_hdr[wv][16 * lane], 0, o);
+                }
             }
-            __builtin_amdgcn_wave_barrier();
         } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) s_hdr[wv][16 * lane + k] = hv[k];
             // the wave's descriptors through its own LDS region (no block barrier), so that they
             // are not live in registers across the build steps
 #pragma unroll
