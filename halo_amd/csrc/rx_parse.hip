@@ -435,6 +435,11 @@ template <int LAYOUT, int FUSE>
 #ifndef HALO_RX_LANE_WAVES
 #define HALO_RX_LANE_WAVES 0
 #endif
+// Prefetching the next group's address/length in waves that loop: no gain at 1M (22.0 vs 22.1
+// us) and 3 % slower at 16M; with capped grids 2-11 % slower (profiles/r02/ab_lane_prefetch.log).
+#ifndef HALO_RX_LANE_PREFETCH
+#define HALO_RX_LANE_PREFETCH 0
+#endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80)))
 #if HALO_RX_LANE_WAVES
 __attribute__((amdgpu_waves_per_eu(HALO_RX_LANE_WAVES)))
@@ -450,11 +455,22 @@ rx_lane_kernel(const RxParams p) {
     const bool compact = (p.flags & HALO_RX_RECORD_COMPACT) != 0;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+#if HALO_RX_LANE_PREFETCH
+    // the next group's address and length load while this group is parsed (waves that loop)
+    FrameState<1> nx;
+    frame_meta<LAYOUT>(p, wave * 64 + lane, wave * 64 + lane < p.n, nx);
+#endif
     for (uint32_t base = wave * 64; base < p.n; base += nwaves * 64) {
         const uint32_t i = base + lane;
         FrameState<1> st;
+#if HALO_RX_LANE_PREFETCH
+        st.frame = nx.frame; st.L = nx.L; st.ndw = nx.ndw;
+        frame_loads<1>(0, st);
+        frame_meta<LAYOUT>(p, i + nwaves * 64, i + nwaves * 64 < p.n, nx);
+#else
         frame_meta<LAYOUT>(p, i, i < p.n, st);
         frame_loads<1>(0, st);
+#endif
         frame_finish<1, FUSE, HALO_RX_LATER_CHUNKS, kRound0<1>, kL3<LAYOUT>>(p, i, i < p.n, 0, lane, st, hist,
                                                                          &s_rec[w][compact ? lane : 2 * lane]);
         __builtin_amdgcn_wave_barrier();
