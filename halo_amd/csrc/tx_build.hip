@@ -599,7 +599,13 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
     else if (chunks <= 16) hipLaunchKernelGGL((halo::tx_build_kernel<4, 4>), grid, blk, 0, s, p);
     else if (chunks <= 32) hipLaunchKernelGGL((halo::tx_build_kernel<8, 4>), grid, blk, 0, s, p);
     else if (chunks <= 64) hipLaunchKernelGGL((halo::tx_build_kernel<16, 4>), grid, blk, 0, s, p);
-    else hipLaunchKernelGGL((halo::tx_build_kernel<32, 3>), grid, blk, 0, s, p);
+// lanes x chunks per round for frames > 64 chunks: 32 x 3 (227 us for 256k x 1514 B) against
+// 16 x 6 303, 16 x 3 242, 8 x 4 277, 64 x 2 305, 32 x 2 244 (profiles/r02/txb/ab_big_frame_G_U_sweep.log)
+#ifndef HALO_TXB_BIG_G
+#define HALO_TXB_BIG_G 32
+#define HALO_TXB_BIG_U 3
+#endif
+    else hipLaunchKernelGGL((halo::tx_build_kernel<HALO_TXB_BIG_G, HALO_TXB_BIG_U>), grid, blk, 0, s, p);
     hipLaunchKernelGGL(halo::tx_settle_kernel, dim3(1), dim3(1024), 0, s, p);
     hipLaunchKernelGGL(halo::tx_renumber_kernel, dim3(p.n_tiles < 256u ? p.n_tiles : 256u), dim3(halo::kBlock), 0,
                        s, p);
