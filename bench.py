@@ -798,10 +798,16 @@ def e2e_host(dev, netif, steps: int):
         out = _lib.host_array(n, _lib.RESULT_DTYPE)
         out.view(np.uint8)[:] = 0  # touched once: no page faults in the timed loop
         lens = own_pages(np.ascontiguousarray(lay["lens"]))
-        for registered in (True, False):
-            # registered: frames, offsets, lengths and the record array all pinned in place (one
-            # DMA per chunk straight from the caller's frames; the host converts the offsets)
+        modes = [("_registered", True, True,
+                  "zero-copy: frames and record array registered; the kernel reads the frames in place "
+                  "over PCIe and writes the records straight into the caller's array"),
+                 ("_registered_dma", True, False,
+                  "registered, zero-copy off: one DMA per chunk from the caller's frames, records DMA'd back"),
+                 ("_pageable", False, False, "pageable: runtime-staged DMA per chunk, records DMA'd back")]
+        for suffix, registered, zero_copy, path in modes:
             pinned = (host, offs, lens, out) if registered else ()
+            hb.set_zero_copy(zero_copy)
+            out.view(np.uint8)[:] = 0
             with contextlib.ExitStack() as regs:  # unregistered on exit, checked, even on error
                 for a in pinned:
                     regs.enter_context(_lib.registered(a))
@@ -812,9 +818,9 @@ def e2e_host(dev, netif, steps: int):
                     hb.parse(host, offs, lens, netif, 1, out=out)
                 el = (time.perf_counter() - t0) / steps
             fb = int(lay["lens"].astype(np.int64).sum())
-            res[name + ("_registered" if registered else "_pageable")] = {
+            res[name + suffix] = {
                 "frames": n, "mpps": round(n / el / 1e6, 1), "gbit_s": round(fb * 8 / el / 1e9, 1),
-                "ms_per_batch": round(el * 1e3, 3), "ok": int((out["status"] == 0).sum()) == n}
+                "ms_per_batch": round(el * 1e3, 3), "ok": int((out["status"] == 0).sum()) == n, "path": path}
         hb.close()
         del fr
         torch.cuda.empty_cache()

@@ -217,6 +217,7 @@ _PROTOS = {
     "halo_rx_host_ctx_create": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "halo_rx_host_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "halo_rx_host_ctx_set_zero_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "halo_rx_parse_batch_host": (ctypes.c_int, [
         ctypes.c_void_p, _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf),
         _u8p, _u8p]),

@@ -75,5 +75,8 @@ enum HostRegKind : int { kRegUser = 1, kRegRing = 2 };
 uint64_t host_page_size();
 int host_reg_add(void* base, uint64_t bytes, HostRegKind kind);  // bytes: a page multiple
 int host_reg_remove(void* base, HostRegKind kind);
+// The device's address for host range [p, p + bytes) if it lies inside one live registration,
+// else nullptr.
+void* host_reg_device_view(const void* p, uint64_t bytes);
 
 }  // namespace halo

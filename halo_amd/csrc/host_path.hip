@@ -44,6 +44,7 @@ namespace {
 struct Reg {
     uint64_t bytes;
     HostRegKind kind;
+    uint8_t* dev;  // the range as the device addresses it (hipHostGetDevicePointer)
 };
 std::mutex g_reg_mu;
 std::map<uintptr_t, Reg> g_regs;  // base -> range (page-aligned, whole pages)
@@ -101,8 +102,24 @@ int host_reg_add(void* base, uint64_t bytes, HostRegKind kind) {
         (void)hipGetLastError();
         return HALO_E_HIP;
     }
-    g_regs.emplace(b, Reg{bytes, kind});
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = nullptr;  // no device view: the range is still usable as a DMA source
+    }
+    g_regs.emplace(b, Reg{bytes, kind, static_cast<uint8_t*>(dev)});
     return HALO_OK;
+}
+
+void* host_reg_device_view(const void* p, uint64_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if (!p || a + bytes < a) return nullptr;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_regs.upper_bound(a);  // the first registration starting after a
+    if (it == g_regs.begin()) return nullptr;
+    --it;
+    if (!it->second.dev || a + bytes > it->first + it->second.bytes) return nullptr;
+    return it->second.dev + (a - it->first);
 }
 
 int host_reg_remove(void* base, HostRegKind kind) {
@@ -242,6 +259,7 @@ struct halo_rx_host_ctx {
     int device;
     uint32_t chunk_frames;
     uint64_t chunk_bytes;
+    bool zero_copy = true;  // registered frames are parsed where they lie (no H2D of frame bytes)
     struct Slot {
         hipStream_t stream = nullptr;
         uint8_t* h_bytes = nullptr;   // pinned staging
@@ -342,6 +360,54 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
     while (next < n && rc == HALO_OK) {
         auto& s = ctx->slot[k & 1];
         if ((rc = drain(s))) break;
+        // Zero-copy mode: frames 4-byte aligned relative to each other inside one live
+        // registration (a registered ring segment or packed batch) are read by the kernel in
+        // place over PCIe, and the records are written straight into `out` when it is registered
+        // too: no staging, no DMA of frame bytes (tools/exp/zc_probe.py: the kernel reads host
+        // memory at the link rate, where the DMA-then-parse pipeline lost a third of it).
+        if (ctx->zero_copy) {
+            const uint32_t cnt = (uint32_t)((n - next) < ctx->chunk_frames ? (n - next) : ctx->chunk_frames);
+            const uint64_t* o = offsets + next;
+            const uint16_t* l = lens + next;
+            uint64_t lo = ~0ull, hi = 0, mis = 0;
+            for (uint32_t j = 0; j < cnt; ++j) {  // span and relative alignment (vectorisable)
+                const uint64_t e = o[j] + l[j];
+                lo = o[j] < lo ? o[j] : lo;
+                hi = e > hi ? e : hi;
+                mis |= o[j] - o[0];
+            }
+            const uint64_t span = hi > lo ? hi - lo : 1;
+            const uint8_t* view = (mis & 3u) || span > (16ull << 30)
+                                      ? nullptr
+                                      : static_cast<const uint8_t*>(halo::host_reg_device_view(bytes + lo, span));
+            if (view && !(reinterpret_cast<uintptr_t>(view) & 3u)) {
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    s.h_off[j] = (uint32_t)((o[j] - lo) >> 2);
+                    s.h_len[j] = l[j];
+                }
+                auto* out_view = static_cast<halo_rx_result_t*>(
+                    halo::host_reg_device_view(out + next, sizeof(halo_rx_result_t) * cnt));
+                if (reinterpret_cast<uintptr_t>(out_view) & 15u) out_view = nullptr;
+                hipError_t e = hipMemcpyAsync(s.d_off, s.h_off, 4ull * cnt, hipMemcpyHostToDevice, s.stream);
+                if (e == hipSuccess) e = hipMemcpyAsync(s.d_len, s.h_len, 2ull * cnt, hipMemcpyHostToDevice, s.stream);
+                if (e != hipSuccess) { rc = HALO_E_HIP; break; }
+                rc = halo_rx_parse_batch_device(view, s.d_off, s.d_len, cnt, flags, netif, 0,
+                                                out_view ? out_view : s.d_res, status_hist ? s.d_hist : nullptr,
+                                                s.stream);
+                if (rc) break;
+                if (!out_view && hipMemcpyAsync(out + next, s.d_res, sizeof(halo_rx_result_t) * cnt,
+                                                hipMemcpyDeviceToHost, s.stream) != hipSuccess) {
+                    rc = HALO_E_HIP;
+                    break;
+                }
+                s.busy = true;
+                s.first = next;
+                s.count = cnt;
+                next += cnt;
+                ++k;
+                continue;
+            }
+        }
         // Direct mode: frames in order, 4-byte aligned relative to the first, spanning at most
         // chunk_bytes (a drained ring segment, or a packed batch): one DMA of the caller's span
         // (pinned if registered with halo_rx_host_register), no CPU copy of frame bytes.
@@ -415,6 +481,12 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
         }
     }
     return rc;
+}
+
+extern "C" HALO_API int halo_rx_host_ctx_set_zero_copy(halo_rx_host_ctx_t* ctx, int enable) {
+    if (!ctx) return HALO_E_INVAL;
+    ctx->zero_copy = enable != 0;
+    return HALO_OK;
 }
 
 extern "C" HALO_API int halo_rx_host_register(const void* ptr, uint64_t bytes) {

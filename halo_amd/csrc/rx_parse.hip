@@ -440,20 +440,47 @@ template <int LAYOUT, int FUSE>
 #ifndef HALO_RX_LANE_PREFETCH
 #define HALO_RX_LANE_PREFETCH 0
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80)))
+// Threads per block of the lane kernel (64, 128 or 256) and 16-byte chunks per lane in its later
+// load rounds (frames > 64 B only). One-wave blocks with 4.5 KB of LDS padding (22 blocks =
+// 5.5 waves per SIMD resident, against 6 by registers) beat 256-thread blocks at every size
+// measured: 1M x 64 B 22.2 -> 21.5 us, 16M x 64 B 321 -> 313 us, 128 B 49.8 -> 49.3 us
+// (profiles/r02/lane_ab/: fewer frame bytes in flight per CU stream faster
+// from HBM; occupancy 8 (LATER 4: 60 VGPRs) was 2-8 % slower, 4 waves 2-9 % slower).
+#ifndef HALO_RX_LANE_BLOCK
+#define HALO_RX_LANE_BLOCK 64
+#endif
+#ifndef HALO_RX_LANE_LATER
+#define HALO_RX_LANE_LATER HALO_RX_LATER_CHUNKS
+#endif
+// A/B knobs: dynamic LDS bytes per lane-kernel block (caps resident blocks per CU, i.e. the
+// frame bytes in flight), and XCD-contiguous block order (blocks b, b+8, ... share an XCD; with
+// the remap each XCD's blocks take one contiguous range of the batch).
+#ifndef HALO_RX_LANE_LDS_PAD
+#define HALO_RX_LANE_LDS_PAD 4608
+#endif
+#ifndef HALO_RX_LANE_XCD
+#define HALO_RX_LANE_XCD 0
+#endif
+__global__ void __launch_bounds__(HALO_RX_LANE_BLOCK) __attribute__((amdgpu_num_sgpr(80)))
 #if HALO_RX_LANE_WAVES
 __attribute__((amdgpu_waves_per_eu(HALO_RX_LANE_WAVES)))
 #endif
 rx_lane_kernel(const RxParams p) {
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
-    __shared__ uint4 s_rec[4][128];  // per wave: 64 records of 32 B
+    __shared__ uint4 s_rec[HALO_RX_LANE_BLOCK / 64][128];  // per wave: 64 records of 32 B
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
     Hist hist{s_hist, 0};
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = threadIdx.x >> 6;
     const bool compact = (p.flags & HALO_RX_RECORD_COMPACT) != 0;
+#if HALO_RX_LANE_XCD
+    const uint32_t nb = gridDim.x, per = nb >> 3, rem = nb & 7u, xcd = blockIdx.x & 7u;
+    const uint32_t lblock = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (blockIdx.x >> 3);
+    const uint32_t wave = (lblock * blockDim.x + threadIdx.x) >> 6;
+#else
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+#endif
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
 #if HALO_RX_LANE_PREFETCH
     // the next group's address and length load while this group is parsed (waves that loop)
@@ -471,7 +498,7 @@ rx_lane_kernel(const RxParams p) {
         frame_meta<LAYOUT>(p, i, i < p.n, st);
         frame_loads<1>(0, st);
 #endif
-        frame_finish<1, FUSE, HALO_RX_LATER_CHUNKS, kRound0<1>, kL3<LAYOUT>>(p, i, i < p.n, 0, lane, st, hist,
+        frame_finish<1, FUSE, HALO_RX_LANE_LATER, kRound0<1>, kL3<LAYOUT>>(p, i, i < p.n, 0, lane, st, hist,
                                                                          &s_rec[w][compact ? lane : 2 * lane]);
         __builtin_amdgcn_wave_barrier();
         const uint32_t nrec = p.n - base < 64 ? p.n - base : 64;  // records of this wave
@@ -491,8 +518,15 @@ rx_lane_kernel(const RxParams p) {
 #ifndef HALO_RX_GROUP_WAVES
 #define HALO_RX_GROUP_WAVES 5
 #endif
+// A/B knobs: threads per block and dynamic LDS padding per block (caps resident blocks per CU).
+#ifndef HALO_RX_GROUP_BLOCK
+#define HALO_RX_GROUP_BLOCK 256
+#endif
+#ifndef HALO_RX_GROUP_LDS_PAD
+#define HALO_RX_GROUP_LDS_PAD 0
+#endif
 template <int G, int LAYOUT, int FUSE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_RX_GROUP_WAVES)))
+__global__ void __launch_bounds__(HALO_RX_GROUP_BLOCK) __attribute__((amdgpu_waves_per_eu(HALO_RX_GROUP_WAVES)))
 rx_group_kernel(const RxParams p) {
     static_assert(G == 4 || G == 8 || G == 16, "G must be 4, 8 or 16");
     group_kernel_body<G, LAYOUT, FUSE>(p);
@@ -721,6 +755,13 @@ __device__ __forceinline__ void stream_load(uint64_t B, uint32_t s0, uint32_t la
     }
 }
 
+// A/B knobs: threads per block and dynamic LDS padding per block.
+#ifndef HALO_RX_STREAM_BLOCK
+#define HALO_RX_STREAM_BLOCK 256
+#endif
+#ifndef HALO_RX_STREAM_LDS_PAD
+#define HALO_RX_STREAM_LDS_PAD 0
+#endif
 #ifndef HALO_RX_STREAM_WAVES
 #define HALO_RX_STREAM_WAVES 6
 #endif
@@ -757,11 +798,12 @@ __device__ __forceinline__ void stream_sum(const uint32_t (&x)[4][4], uint32_t l
 // fetched from HBM exactly once. Without HDR (checksums off: only ICMP frames have a segment),
 // the lane reads its header first and the stream covers only the windows' segments.
 template <int LAYOUT, int FUSE, bool HDR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_RX_STREAM_WAVES)))
+__global__ void __launch_bounds__(HALO_RX_STREAM_BLOCK) __attribute__((amdgpu_waves_per_eu(HALO_RX_STREAM_WAVES)))
 rx_stream_kernel(const RxParams p) {
+    constexpr int kW = HALO_RX_STREAM_BLOCK / 64;
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
-    __shared__ uint4 s_x[4][kStreamStep / 16];       // per wave: the step's bytes (records at the end)
-    __shared__ uint32_t s_base[4][kStreamStep / 16];  // per wave: P at each 16-byte sub-chunk
+    __shared__ uint4 s_x[kW][kStreamStep / 16];       // per wave: the step's bytes (records at the end)
+    __shared__ uint32_t s_base[kW][kStreamStep / 16];  // per wave: P at each 16-byte sub-chunk
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
     Hist hist{s_hist, 0};
@@ -945,9 +987,10 @@ rx_stream_kernel(const RxParams p) {
 #endif
 constexpr int kVariantMix = -1, kVariantStream = 2;
 
-uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS) {
+uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS,
+                  uint32_t waves_per_block = 4) {
     const uint64_t waves = (n + frames_per_wave - 1) / frames_per_wave;
-    uint64_t blocks = (waves + 3) / 4;
+    uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     const uint64_t kMaxBlocks = max_blocks;
     return (uint32_t)(blocks > kMaxBlocks ? kMaxBlocks : blocks);
 }
@@ -956,16 +999,33 @@ template <int LAYOUT, int FUSE = 0>
 hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     const dim3 block(256);
     switch (variant) {
-        case 1: hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64, HALO_RX_LANE_MAX_BLOCKS)), block, 0, s, p); break;
-        case kVariantStream:
-            if (HALO_RX_STREAM_HDR && (p.flags & HALO_RX_CSUM_ENABLE))
-                hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, true>), dim3(grid_for(p.n, 64)), block, 0, s, p);
-            else
-                hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, false>), dim3(grid_for(p.n, 64)), block, 0, s, p);
+        case 1: {
+            constexpr uint32_t wpb = HALO_RX_LANE_BLOCK / 64;
+            hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64, HALO_RX_LANE_MAX_BLOCKS * 4 / wpb, wpb)),
+                               dim3(HALO_RX_LANE_BLOCK), HALO_RX_LANE_LDS_PAD, s, p);
             break;
-        case 4: hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT, FUSE>), dim3(grid_for(p.n, 16)), block, 0, s, p); break;
-        case 8: hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT, FUSE>), dim3(grid_for(p.n, 8)), block, 0, s, p); break;
-        case 16: hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT, FUSE>), dim3(grid_for(p.n, 4)), block, 0, s, p); break;
+        }
+        case kVariantStream: {
+            constexpr uint32_t wpb = HALO_RX_STREAM_BLOCK / 64;
+            const dim3 g(grid_for(p.n, 64, HALO_RX_MAX_BLOCKS * 4 / wpb, wpb)), b(HALO_RX_STREAM_BLOCK);
+            if (HALO_RX_STREAM_HDR && (p.flags & HALO_RX_CSUM_ENABLE))
+                hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, true>), g, b, HALO_RX_STREAM_LDS_PAD, s, p);
+            else
+                hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, false>), g, b, HALO_RX_STREAM_LDS_PAD, s, p);
+            break;
+        }
+        case 4: case 8: case 16: {
+            constexpr uint32_t wpb = HALO_RX_GROUP_BLOCK / 64;
+            const dim3 b(HALO_RX_GROUP_BLOCK);
+            const uint64_t cap = HALO_RX_MAX_BLOCKS * 4 / wpb;
+            if (variant == 4)
+                hipLaunchKernelGGL((rx_group_kernel<4, LAYOUT, FUSE>), dim3(grid_for(p.n, 16, cap, wpb)), b, HALO_RX_GROUP_LDS_PAD, s, p);
+            else if (variant == 8)
+                hipLaunchKernelGGL((rx_group_kernel<8, LAYOUT, FUSE>), dim3(grid_for(p.n, 8, cap, wpb)), b, HALO_RX_GROUP_LDS_PAD, s, p);
+            else
+                hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT, FUSE>), dim3(grid_for(p.n, 4, cap, wpb)), b, HALO_RX_GROUP_LDS_PAD, s, p);
+            break;
+        }
         default: hipLaunchKernelGGL((rx_mix_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, kMixWindow)), block, 0, s, p); break;
     }
     return hipGetLastError();

@@ -66,6 +66,10 @@ class HostBatcher:
                    _lib.lib.halo_rx_host_ctx_create(device, chunk_frames, chunk_bytes, ctypes.byref(h)))
         self._ctx = h
 
+    def set_zero_copy(self, enable: bool):
+        """Registered batches parsed in place over PCIe (default) or DMA'd in chunks."""
+        _lib.check("halo_rx_host_ctx_set_zero_copy", _lib.lib.halo_rx_host_ctx_set_zero_copy(self._ctx, int(enable)))
+
     def close(self):
         if self._ctx:
             _lib.lib.halo_rx_host_ctx_destroy(self._ctx)

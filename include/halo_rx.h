@@ -230,10 +230,16 @@ HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* by
                                       const uint64_t* offsets, const uint16_t* lens, uint32_t n,
                                       uint32_t flags, const halo_rx_netif_t* netif,
                                       halo_rx_result_t* out, uint32_t* status_hist);
-/* Frames whose offsets are ascending and 4-byte aligned relative to each other (a drained ring
- * segment, a packed batch) are sent with one DMA per chunk straight from `bytes`; registering
- * that memory (e.g. the ring's hugepages) makes the DMA run at full PCIe rate. Other batches
- * are repacked into pinned staging by the CPU.
+/* Frames whose offsets are 4-byte aligned relative to each other and that lie inside one live
+ * registration (halo_rx_host_register, or a ring attached with HALO_RING_REGISTER) are parsed
+ * in place: the kernel reads them over PCIe, no staging copy (zero-copy mode, the default), and
+ * writes the records straight into `out` when `out` is registered as well. Otherwise frames
+ * whose offsets are ascending and relatively aligned (a drained ring segment, a packed batch)
+ * are sent with one DMA per chunk straight from `bytes`, and other batches are repacked into
+ * pinned staging by the CPU. halo_rx_host_ctx_set_zero_copy(ctx, 0) keeps registered batches
+ * on the DMA path. Registered memory must stay registered until the call returns.         */
+HALO_API int halo_rx_host_ctx_set_zero_copy(halo_rx_host_ctx_t* ctx, int enable);
+/*
  * Registration pins whole pages, so the library enforces: `ptr` page-aligned and `bytes` a
  * multiple of the page size (hugepages, mmap regions; halo_amd._lib.host_array in Python), and
  * no page shared with a live registration (this call's or a ring's) — otherwise HALO_E_INVAL,

@@ -493,12 +493,74 @@ def test_host_path_direct_dma_registered(dev, oracle_lib):
     hb = HostBatcher(0, chunk_frames=3000, chunk_bytes=1 << 20)
     import contextlib
 
+    out = _lib.host_array(len(lay["lens"]), _lib.RESULT_DTYPE)
     try:
-        for registered in (False, True):
+        # registered frames: zero-copy (parsed in place over PCIe) and, forced, the DMA path;
+        # records into a registered array (written by the kernel over PCIe) or a pageable one
+        for registered, zero_copy, out_reg in [(False, True, False), (True, False, False), (True, True, False),
+                                               (True, True, True), (False, True, True)]:
+            hb.set_zero_copy(zero_copy)
             hist = np.zeros(14, np.uint32)
-            with _lib.registered(data) if registered else contextlib.nullcontext():
-                got = hb.parse(data, offs, lay["lens"], NetIf.make(), 1, hist)
-            assert_records_equal(got, want, None, f"host direct registered={registered}")
+            out.view(np.uint8)[:] = 0xEE
+            with contextlib.ExitStack() as regs:
+                if registered:
+                    regs.enter_context(_lib.registered(data))
+                if out_reg:
+                    regs.enter_context(_lib.registered(out))
+                got = hb.parse(data, offs, lay["lens"], NetIf.make(), 1, hist, out=out if out_reg else None)
+            assert_records_equal(got, want, None,
+                                 f"host direct registered={registered} zero_copy={zero_copy} out_registered={out_reg}")
+            assert np.array_equal(hist, whist)
+    finally:
+        hb.close()
+    assert _lib.registered_count() == 0, _lib.registrations()
+
+
+def test_host_path_zero_copy_any_order(dev, oracle_lib):
+    """Zero-copy takes frames in any order inside one registration (span = min..max of the
+    chunk); a chunk whose offsets are not 4-byte aligned relative to each other, or whose span
+    starts off a dword, is refused and goes the DMA / repack way. Records identical to the
+    oracle in every case."""
+    from halo_amd import _lib, synth
+    from halo_amd._lib import NetIf
+    from halo_amd.engine import HostBatcher
+
+    n = 20_000
+    lay = synth.layout(n, size_mode=1, proto_mode=3, mutate_shift=4, first_index=123_456)
+    data = oracle_lib.synth_batch(synth.SEED, 123_456, lay["lens"], lay["kinds"], oracle_lib.NetIf.make(),
+                                  offsets_dw=lay["offsets_dw"], fill=0x5A)
+    perm = np.random.default_rng(7).permutation(n)
+    lens = np.ascontiguousarray(lay["lens"][perm])
+    base_offs = lay["offsets_dw"][perm].astype(np.uint64) * 4
+    want, whist = oracle_lib.rx_batch(data, lens, oracle_lib.NetIf.make(), 1,
+                                      offsets_dw=np.ascontiguousarray(lay["offsets_dw"][perm]))
+    size = data.shape[0]
+    reg = _lib.host_array(2 * size + 4096, np.uint8)
+    hb = HostBatcher(0, chunk_frames=4096, chunk_bytes=1 << 20)
+    try:
+        cases = []
+        # shuffled, aligned: zero-copy; shifted by one byte: relative alignment kept, span off a dword
+        for shift in (0, 1):
+            cases.append((f"shuffled shift={shift}", shift, base_offs + shift, None))
+        # one frame per chunk relocated to a 2 mod 4 offset: that chunk is repacked by the CPU
+        offs = base_offs.copy()
+        moved = np.arange(0, n, 4096)
+        cases.append(("one misaligned frame per chunk", 0, offs, moved))
+        for label, shift, offs, moved in cases:
+            reg[:] = 0
+            reg[shift:shift + size] = data
+            offs = offs.copy()
+            if moved is not None:
+                pos = size + 2
+                for i in moved:
+                    o, L = int(offs[i]), int(lens[i])
+                    reg[pos:pos + L] = reg[o:o + L]
+                    offs[i] = pos
+                    pos += L + 4
+            hist = np.zeros(14, np.uint32)
+            with _lib.registered(reg):
+                got = hb.parse(reg, offs, lens, NetIf.make(), 1, hist)
+            assert_records_equal(got, want, None, f"zero-copy {label}")
             assert np.array_equal(hist, whist)
     finally:
         hb.close()

@@ -43,6 +43,9 @@ def main():
     if "--variants" in sys.argv:  # e.g. --variants=-2 (one kernel variant for every workload)
         only = [int(x) for x in sys.argv[sys.argv.index("--variants") + 1].split(",")]
         workloads = [(a, b, c, d, only) for a, b, c, d, _ in workloads]
+    if "--spec" in sys.argv:  # e.g. --spec imix:-2,1500B:8 (workloads and one variant each)
+        spec = dict(x.split(":") for x in sys.argv[sys.argv.index("--spec") + 1].split(","))
+        workloads = [(a, b, c, d, [int(spec[a])]) for a, b, c, d, _ in workloads if a in spec]
     res = {}
     for name, kw, n, rot, gs in workloads:
         bs = bench.make_batches(dev, netif, n=n, rotate=rot, rank=0, **kw)
