@@ -355,8 +355,15 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
 #undef SET_BE16
 #undef SET_LE16
 
+// A/B knobs: threads per block and dynamic LDS padding per block (caps resident blocks per CU).
+#ifndef HALO_TX_BLOCK
+#define HALO_TX_BLOCK 256
+#endif
+#ifndef HALO_TX_LDS_PAD
+#define HALO_TX_LDS_PAD 0
+#endif
 template <int G>
-__global__ void __launch_bounds__(256) tx_fixup_kernel(const TxParams p) {
+__global__ void __launch_bounds__(HALO_TX_BLOCK) tx_fixup_kernel(const TxParams p) {
     constexpr uint32_t FPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
@@ -370,9 +377,10 @@ __global__ void __launch_bounds__(256) tx_fixup_kernel(const TxParams p) {
 }
 
 uint32_t tx_grid(uint64_t n, uint32_t frames_per_wave) {
+    constexpr uint64_t wpb = HALO_TX_BLOCK / 64;
     const uint64_t waves = (n + frames_per_wave - 1) / frames_per_wave;
-    const uint64_t blocks = (waves + 3) / 4;
-    const uint64_t kMaxBlocks = 256ull * 8 * 8;
+    const uint64_t blocks = (waves + wpb - 1) / wpb;
+    const uint64_t kMaxBlocks = 256ull * 8 * 8 * 4 / wpb;
     return (uint32_t)(blocks > kMaxBlocks ? kMaxBlocks : blocks);
 }
 
@@ -392,12 +400,12 @@ extern "C" HALO_API int halo_tx_fixup_batch_device(uint8_t* d_bytes, const uint3
     if (rc) return rc;
     halo::TxParams p{d_bytes, d_offsets_dw, d_lens, d_ops, n, flags, d_result};
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 block(256);
+    const dim3 block(HALO_TX_BLOCK);
     // lanes per frame from the longest frame (0: unknown -> widest); any G handles any length
     const uint32_t h = max_len_hint ? max_len_hint : 65535u;
-    if (h <= 128) hipLaunchKernelGGL(halo::tx_fixup_kernel<1>, dim3(halo::tx_grid(n, 64)), block, 0, s, p);
-    else if (h <= 1024) hipLaunchKernelGGL(halo::tx_fixup_kernel<4>, dim3(halo::tx_grid(n, 16)), block, 0, s, p);
-    else if (h <= 4096) hipLaunchKernelGGL(halo::tx_fixup_kernel<8>, dim3(halo::tx_grid(n, 8)), block, 0, s, p);
-    else hipLaunchKernelGGL(halo::tx_fixup_kernel<16>, dim3(halo::tx_grid(n, 4)), block, 0, s, p);
+    if (h <= 128) hipLaunchKernelGGL(halo::tx_fixup_kernel<1>, dim3(halo::tx_grid(n, 64)), block, HALO_TX_LDS_PAD, s, p);
+    else if (h <= 1024) hipLaunchKernelGGL(halo::tx_fixup_kernel<4>, dim3(halo::tx_grid(n, 16)), block, HALO_TX_LDS_PAD, s, p);
+    else if (h <= 4096) hipLaunchKernelGGL(halo::tx_fixup_kernel<8>, dim3(halo::tx_grid(n, 8)), block, HALO_TX_LDS_PAD, s, p);
+    else hipLaunchKernelGGL(halo::tx_fixup_kernel<16>, dim3(halo::tx_grid(n, 4)), block, HALO_TX_LDS_PAD, s, p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
