@@ -78,5 +78,7 @@ int host_reg_remove(void* base, HostRegKind kind);
 // The device's address for host range [p, p + bytes) if it lies inside one live registration,
 // else nullptr.
 void* host_reg_device_view(const void* p, uint64_t bytes);
+// The live registration holding host address p: base, size and device address.
+bool host_reg_find(const void* p, uintptr_t* base, uint64_t* bytes, uint8_t** dev);
 
 }  // namespace halo

@@ -10,6 +10,8 @@
 #include <map>
 #include <mutex>
 #include <new>
+#include <utility>
+#include <vector>
 
 #include "halo_common.h"
 
@@ -109,6 +111,19 @@ int host_reg_add(void* base, uint64_t bytes, HostRegKind kind) {
     }
     g_regs.emplace(b, Reg{bytes, kind, static_cast<uint8_t*>(dev)});
     return HALO_OK;
+}
+
+bool host_reg_find(const void* p, uintptr_t* base, uint64_t* bytes, uint8_t** dev) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_regs.upper_bound(a);
+    if (it == g_regs.begin()) return false;
+    --it;
+    if (a >= it->first + it->second.bytes) return false;
+    *base = it->first;
+    *bytes = it->second.bytes;
+    *dev = it->second.dev;
+    return true;
 }
 
 void* host_reg_device_view(const void* p, uint64_t bytes) {
@@ -258,6 +273,7 @@ extern "C" HALO_API int halo_rx_dispatch_compact(const halo_rx_record16_t* recor
 struct halo_rx_host_ctx {
     int device;
     uint32_t chunk_frames;
+    uint32_t zc_frames;  // chunk of the zero-copy path with GPU-converted metadata (no host staging)
     uint64_t chunk_bytes;
     bool zero_copy = true;  // registered frames are parsed where they lie (no H2D of frame bytes)
     struct Slot {
@@ -270,6 +286,10 @@ struct halo_rx_host_ctx {
         uint16_t* d_len = nullptr;
         halo_rx_result_t* d_res = nullptr;
         uint32_t* d_hist = nullptr;
+        uint32_t* d_hist_try = nullptr;  // zero-copy chunks with GPU-converted metadata count here first
+        uint32_t* d_flag = nullptr;      // set by zc_meta_kernel when a frame lies outside the registration
+        uint32_t* h_flag = nullptr;      // pinned copy of d_flag
+        bool zc_meta = false;            // the chunk in flight converted its metadata on the GPU
         // chunk currently in flight in this slot
         bool busy = false;
         uint64_t first = 0;
@@ -289,8 +309,38 @@ void free_ctx(halo_rx_host_ctx* c) {
         if (s.d_len) (void)hipFree(s.d_len);
         if (s.d_res) (void)hipFree(s.d_res);
         if (s.d_hist) (void)hipFree(s.d_hist);
+        if (s.d_hist_try) (void)hipFree(s.d_hist_try);
+        if (s.d_flag) (void)hipFree(s.d_flag);
+        if (s.h_flag) (void)hipHostFree(s.h_flag);
     }
     delete c;
+}
+
+// Zero-copy metadata: the caller's own u64 byte offsets and u16 lengths (registered host memory,
+// read over PCIe) become the kernel's u32 dword offsets into the frames' registration. A frame not
+// wholly inside that registration, or not 4-byte aligned in it, gets length 0 (never read) and
+// raises the flag: the host then re-parses that chunk on the DMA path (and its status counts
+// never reach the histogram: zc_hist_commit drops them).
+__global__ void __launch_bounds__(256) zc_meta_kernel(const uint64_t* __restrict__ offs,
+                                                      const uint16_t* __restrict__ lens, uint32_t n,
+                                                      uint64_t delta, uint64_t reg_bytes, uint32_t* d_off,
+                                                      uint16_t* d_len, uint32_t* flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t rel = offs[i] + delta;  // byte offset in the registration (mod 2^64)
+    const uint32_t L = lens[i];
+    const bool ok = rel < reg_bytes && L <= reg_bytes - rel && (rel & 3u) == 0;
+    d_off[i] = ok ? (uint32_t)(rel >> 2) : 0u;
+    d_len[i] = ok ? (uint16_t)L : (uint16_t)0;
+    if (!ok) atomicOr(flag, 1u);
+}
+
+// Adds the chunk's status counts to the slot's histogram unless the chunk is to be re-parsed.
+__global__ void zc_hist_commit(const uint32_t* flag, uint32_t* try_hist, uint32_t* hist) {
+    const uint32_t t = threadIdx.x;
+    if (t >= HALO_RX_STATUS_COUNT) return;
+    if (*flag == 0) hist[t] += try_hist[t];
+    try_hist[t] = 0;
 }
 }  // namespace
 
@@ -307,6 +357,10 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
     if (!c) return HALO_E_NOMEM;
     c->device = device;
     c->chunk_frames = chunk_frames;
+    // zero-copy chunks with GPU-converted metadata stage nothing on the host, so they can be
+    // larger: fewer chunk boundaries (1M x 64 B: 1.87 ms in 256k-frame chunks, 1.60 ms in one;
+    // profiles/r02/r2o/host_zc_sweep.log); the device metadata and record buffers are sized for them
+    c->zc_frames = chunk_frames <= (1u << 30) ? chunk_frames * 4u : chunk_frames;
     c->chunk_bytes = chunk_bytes;
     bool ok = true;
     for (auto& s : c->slot) {
@@ -315,11 +369,17 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
         ok = ok && hipHostMalloc((void**)&s.h_off, 4ull * chunk_frames, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipHostMalloc((void**)&s.h_len, 2ull * chunk_frames, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipMalloc((void**)&s.d_bytes, chunk_bytes) == hipSuccess;
-        ok = ok && hipMalloc((void**)&s.d_off, 4ull * chunk_frames) == hipSuccess;
-        ok = ok && hipMalloc((void**)&s.d_len, 2ull * chunk_frames) == hipSuccess;
-        ok = ok && hipMalloc((void**)&s.d_res, sizeof(halo_rx_result_t) * chunk_frames) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_off, 4ull * c->zc_frames) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_len, 2ull * c->zc_frames) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_res, sizeof(halo_rx_result_t) * c->zc_frames) == hipSuccess;
         ok = ok && hipMalloc((void**)&s.d_hist, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
         ok = ok && hipMemsetAsync(s.d_hist, 0, 4 * HALO_RX_STATUS_COUNT, s.stream) == hipSuccess;  // before its parses
+        ok = ok && hipMalloc((void**)&s.d_hist_try, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
+        ok = ok && hipMemsetAsync(s.d_hist_try, 0, 4 * HALO_RX_STATUS_COUNT, s.stream) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.d_flag, 4) == hipSuccess;
+        ok = ok && hipMemsetAsync(s.d_flag, 0, 4, s.stream) == hipSuccess;
+        ok = ok && hipHostMalloc((void**)&s.h_flag, 4, hipHostMallocDefault) == hipSuccess;
+        if (ok) *s.h_flag = 0;
     }
     if (!ok) {
         free_ctx(c);
@@ -350,10 +410,15 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
     const uint32_t cap = (flags & HALO_RX_L3_START) ? ((flags & HALO_RX_JUMBO_EXT) ? halo::kIpMaxJumbo : halo::kIpMax)
                                                     : ((flags & HALO_RX_JUMBO_EXT) ? halo::kEthMaxJumbo : halo::kEthMax);
     int rc = HALO_OK;
+    std::vector<std::pair<uint64_t, uint32_t>> redo;  // zero-copy chunks to re-parse on the DMA path
     auto drain = [&](halo_rx_host_ctx::Slot& s) -> int {
         if (!s.busy) return HALO_OK;
         s.busy = false;
-        return hipStreamSynchronize(s.stream) == hipSuccess ? HALO_OK : HALO_E_HIP;
+        if (hipStreamSynchronize(s.stream) != hipSuccess) return HALO_E_HIP;
+        if (s.zc_meta && *s.h_flag) redo.emplace_back(s.first, s.count);
+        s.zc_meta = false;
+        *s.h_flag = 0;
+        return HALO_OK;
     };
     uint64_t next = 0;
     uint32_t k = 0;
@@ -366,9 +431,51 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
         // too: no staging, no DMA of frame bytes (tools/exp/zc_probe.py: the kernel reads host
         // memory at the link rate, where the DMA-then-parse pipeline lost a third of it).
         if (ctx->zero_copy) {
-            const uint32_t cnt = (uint32_t)((n - next) < ctx->chunk_frames ? (n - next) : ctx->chunk_frames);
+            uint32_t cnt = (uint32_t)((n - next) < ctx->zc_frames ? (n - next) : ctx->zc_frames);
             const uint64_t* o = offsets + next;
             const uint16_t* l = lens + next;
+            // (a) offsets and lengths registered too: the GPU converts them (no host pass over the
+            // metadata, which cost ~1.4 ms per 1M frames on the host: profiles/r02/host_zc_sweep.log)
+            const auto* d_o = static_cast<const uint64_t*>(halo::host_reg_device_view(o, 8ull * cnt));
+            const auto* d_l = d_o ? static_cast<const uint16_t*>(halo::host_reg_device_view(l, 2ull * cnt)) : nullptr;
+            uintptr_t rb = 0;
+            uint64_t rbytes = 0;
+            uint8_t* rdev = nullptr;
+            if (d_l && !(reinterpret_cast<uintptr_t>(d_o) & 7u) && !(reinterpret_cast<uintptr_t>(d_l) & 1u) &&
+                halo::host_reg_find(bytes + o[0], &rb, &rbytes, &rdev) && rdev && rbytes <= (16ull << 30) &&
+                !(reinterpret_cast<uintptr_t>(rdev) & 3u)) {
+                const uint64_t delta = reinterpret_cast<uintptr_t>(bytes) - rb;  // frame at rdev + o + delta
+                auto* out_view = static_cast<halo_rx_result_t*>(
+                    halo::host_reg_device_view(out + next, sizeof(halo_rx_result_t) * cnt));
+                if (reinterpret_cast<uintptr_t>(out_view) & 15u) out_view = nullptr;
+                hipLaunchKernelGGL(zc_meta_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s.stream, d_o, d_l, cnt,
+                                   delta, rbytes, s.d_off, s.d_len, s.d_flag);
+                if (hipGetLastError() != hipSuccess) { rc = HALO_E_HIP; break; }
+                rc = halo_rx_parse_batch_device(rdev, s.d_off, s.d_len, cnt, flags, netif, 0,
+                                                out_view ? out_view : s.d_res,
+                                                status_hist ? s.d_hist_try : nullptr, s.stream);
+                if (rc) break;
+                if (status_hist) {
+                    hipLaunchKernelGGL(zc_hist_commit, dim3(1), dim3(64), 0, s.stream, s.d_flag, s.d_hist_try, s.d_hist);
+                    if (hipGetLastError() != hipSuccess) { rc = HALO_E_HIP; break; }
+                }
+                hipError_t e = hipSuccess;
+                if (!out_view)
+                    e = hipMemcpyAsync(out + next, s.d_res, sizeof(halo_rx_result_t) * cnt, hipMemcpyDeviceToHost,
+                                       s.stream);
+                if (e == hipSuccess) e = hipMemcpyAsync(s.h_flag, s.d_flag, 4, hipMemcpyDeviceToHost, s.stream);
+                if (e == hipSuccess) e = hipMemsetAsync(s.d_flag, 0, 4, s.stream);
+                if (e != hipSuccess) { rc = HALO_E_HIP; break; }
+                s.zc_meta = true;
+                s.busy = true;
+                s.first = next;
+                s.count = cnt;
+                next += cnt;
+                ++k;
+                continue;
+            }
+            // (b) metadata converted by the host, into the slot's pinned staging
+            if (cnt > ctx->chunk_frames) cnt = ctx->chunk_frames;
             uint64_t lo = ~0ull, hi = 0, mis = 0;
             for (uint32_t j = 0; j < cnt; ++j) {  // span and relative alignment (vectorisable)
                 const uint64_t e = o[j] + l[j];
@@ -479,6 +586,15 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
                 return HALO_E_HIP;
             for (int j = 0; j < HALO_RX_STATUS_COUNT; ++j) status_hist[j] += h[j];
         }
+    }
+    if (rc == HALO_OK && !redo.empty()) {  // frames outside the registration: those chunks again, by DMA
+        ctx->zero_copy = false;
+        for (const auto& r : redo) {
+            rc = halo_rx_parse_batch_host(ctx, bytes, offsets + r.first, lens + r.first, r.second, flags, netif,
+                                          out + r.first, status_hist);
+            if (rc) break;
+        }
+        ctx->zero_copy = true;
     }
     return rc;
 }

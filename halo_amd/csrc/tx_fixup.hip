@@ -355,15 +355,20 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
 #undef SET_BE16
 #undef SET_LE16
 
-// A/B knobs: threads per block and dynamic LDS padding per block (caps resident blocks per CU).
-#ifndef HALO_TX_BLOCK
-#define HALO_TX_BLOCK 256
+// Lane-per-frame (G = 1) launch shape: one-wave blocks with 8 KB of dynamic LDS padding each,
+// so 20 blocks = 5 waves per SIMD are resident instead of 6 (by registers): fewer frame bytes in
+// flight per CU, 35.6 -> 33.6 us per 1M x 64 B (profiles/r02/ab_tx_block.log; 4 and 5.5 waves and
+// plain one-wave blocks measured between). G > 1 keeps 256-thread blocks (not measured).
+#ifndef HALO_TX_G1_BLOCK
+#define HALO_TX_G1_BLOCK 64
 #endif
-#ifndef HALO_TX_LDS_PAD
-#define HALO_TX_LDS_PAD 0
+#ifndef HALO_TX_G1_LDS_PAD
+#define HALO_TX_G1_LDS_PAD 8192
 #endif
 template <int G>
-__global__ void __launch_bounds__(HALO_TX_BLOCK) tx_fixup_kernel(const TxParams p) {
+constexpr uint32_t kTxBlock = G == 1 ? HALO_TX_G1_BLOCK : 256;
+template <int G>
+__global__ void __launch_bounds__(kTxBlock<G>) tx_fixup_kernel(const TxParams p) {
     constexpr uint32_t FPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
@@ -376,8 +381,7 @@ __global__ void __launch_bounds__(HALO_TX_BLOCK) tx_fixup_kernel(const TxParams 
     }
 }
 
-uint32_t tx_grid(uint64_t n, uint32_t frames_per_wave) {
-    constexpr uint64_t wpb = HALO_TX_BLOCK / 64;
+uint32_t tx_grid(uint64_t n, uint32_t frames_per_wave, uint64_t wpb) {
     const uint64_t waves = (n + frames_per_wave - 1) / frames_per_wave;
     const uint64_t blocks = (waves + wpb - 1) / wpb;
     const uint64_t kMaxBlocks = 256ull * 8 * 8 * 4 / wpb;
@@ -400,12 +404,12 @@ extern "C" HALO_API int halo_tx_fixup_batch_device(uint8_t* d_bytes, const uint3
     if (rc) return rc;
     halo::TxParams p{d_bytes, d_offsets_dw, d_lens, d_ops, n, flags, d_result};
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    const dim3 block(HALO_TX_BLOCK);
+    const dim3 block(256), block1(HALO_TX_G1_BLOCK);
     // lanes per frame from the longest frame (0: unknown -> widest); any G handles any length
     const uint32_t h = max_len_hint ? max_len_hint : 65535u;
-    if (h <= 128) hipLaunchKernelGGL(halo::tx_fixup_kernel<1>, dim3(halo::tx_grid(n, 64)), block, HALO_TX_LDS_PAD, s, p);
-    else if (h <= 1024) hipLaunchKernelGGL(halo::tx_fixup_kernel<4>, dim3(halo::tx_grid(n, 16)), block, HALO_TX_LDS_PAD, s, p);
-    else if (h <= 4096) hipLaunchKernelGGL(halo::tx_fixup_kernel<8>, dim3(halo::tx_grid(n, 8)), block, HALO_TX_LDS_PAD, s, p);
-    else hipLaunchKernelGGL(halo::tx_fixup_kernel<16>, dim3(halo::tx_grid(n, 4)), block, HALO_TX_LDS_PAD, s, p);
+    if (h <= 128) hipLaunchKernelGGL(halo::tx_fixup_kernel<1>, dim3(halo::tx_grid(n, 64, HALO_TX_G1_BLOCK / 64)), block1, HALO_TX_G1_LDS_PAD, s, p);
+    else if (h <= 1024) hipLaunchKernelGGL(halo::tx_fixup_kernel<4>, dim3(halo::tx_grid(n, 16, 4)), block, 0, s, p);
+    else if (h <= 4096) hipLaunchKernelGGL(halo::tx_fixup_kernel<8>, dim3(halo::tx_grid(n, 8, 4)), block, 0, s, p);
+    else hipLaunchKernelGGL(halo::tx_fixup_kernel<16>, dim3(halo::tx_grid(n, 4, 4)), block, 0, s, p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }

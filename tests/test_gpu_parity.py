@@ -567,6 +567,53 @@ def test_host_path_zero_copy_any_order(dev, oracle_lib):
     assert _lib.registered_count() == 0, _lib.registrations()
 
 
+def test_host_path_zero_copy_gpu_metadata(dev, oracle_lib):
+    """Frames, offsets and lengths all registered: the GPU converts the caller's u64 offsets
+    itself (zc_meta_kernel) and parses in place; with a frame outside the frames' registration
+    that chunk is flagged and re-parsed on the DMA path, its first counts dropped from the
+    histogram. Records and histograms identical to the oracle in every case."""
+    import contextlib
+
+    from halo_amd import _lib, synth
+    from halo_amd._lib import NetIf
+    from halo_amd.engine import HostBatcher
+
+    n = 30_000
+    lay = synth.layout(n, size_mode=1, proto_mode=3, mutate_shift=3, first_index=777_000)
+    data = oracle_lib.synth_batch(synth.SEED, 777_000, lay["lens"], lay["kinds"], oracle_lib.NetIf.make(),
+                                  offsets_dw=lay["offsets_dw"], fill=0x33)
+    want, whist = oracle_lib.rx_batch(data, lay["lens"], oracle_lib.NetIf.make(), 1, offsets_dw=lay["offsets_dw"])
+    frames = _lib.host_array(data.shape, np.uint8)
+    frames[...] = data
+    offs = _lib.host_array(n, np.uint64)
+    lens = _lib.host_array(n, np.uint16)
+    lens[...] = lay["lens"]
+    out = _lib.host_array(n, _lib.RESULT_DTYPE)
+    # a copy of frame 5000 and 21000 in pageable memory, outside every registration
+    outside = {i: np.array(data[int(lay["offsets_dw"][i]) * 4:int(lay["offsets_dw"][i]) * 4 + int(lay["lens"][i])])
+               for i in (5000, 21000)}
+    hb = HostBatcher(0, chunk_frames=4096, chunk_bytes=1 << 20)
+    try:
+        for label, out_reg, move in [("all registered", True, False), ("records pageable", False, False),
+                                     ("two frames outside", True, True)]:
+            offs[...] = lay["offsets_dw"].astype(np.uint64) * 4
+            if move:
+                base = frames.ctypes.data
+                for i, buf in outside.items():
+                    offs[i] = np.uint64((buf.ctypes.data - base) % (1 << 64))
+            out.view(np.uint8)[:] = 0xEE
+            hist = np.zeros(14, np.uint32)
+            with contextlib.ExitStack() as regs:
+                for arr in (frames, offs, lens) + ((out,) if out_reg else ()):
+                    regs.enter_context(_lib.registered(arr))
+                got = hb.parse(frames, offs, lens, NetIf.make(), 1, hist, out=out if out_reg else None)
+            assert_records_equal(got, want, None, f"zero-copy GPU metadata: {label}")
+            assert np.array_equal(hist, whist), label
+    finally:
+        hb.close()
+    assert _lib.registered_count() == 0, _lib.registrations()
+
+
 def test_netif_packet_handle_batch(dev, golden, oracle_lib):
     """Batched PacketHandle: same actions as the reference engine, handlers get payloads."""
     from halo_amd import ACTION_NAMES
