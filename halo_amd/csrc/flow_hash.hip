@@ -177,6 +177,15 @@ __device__ __forceinline__ void stripe_acc(uint64_t& acc, uint64_t in, uint64_t 
     acc += swap_pair(in) + (uint64_t)(uint32_t)k * (k >> 32);
 }
 
+#ifndef HALO_XXH3_X3
+#define HALO_XXH3_X3 1
+#endif
+#ifndef HALO_XXH3_BATCH
+#define HALO_XXH3_BATCH 4
+#endif
+#ifndef HALO_XXH3_LONG_BLOCK
+#define HALO_XXH3_LONG_BLOCK 256
+#endif
 // hashLong (xxh3.go:132-178) on a group of 8 lanes; lane j = accumulator j. Result in every lane.
 // Stripe words are read as aligned dwords (three when the string is not 4-byte aligned) four
 // stripes at a time, so a lane has up to 12 loads in flight.
@@ -188,21 +197,35 @@ __device__ uint64_t hash_long8(const uint8_t* d, uint32_t len, uint32_t j, const
     const uintptr_t base = reinterpret_cast<uintptr_t>(d);
     const uint32_t sh = (uint32_t)(base & 3u);  // uniform per group
     gdw* q0 = (gdw*)(base & ~(uintptr_t)3) + 2 * j;
+    // Input word j of stripe `stripe`: three dwords in one load instruction (global_load_dwordx3)
+    // whatever the alignment. The third is read even when the string is dword-aligned: every
+    // stripe of this loop ends at least one byte before the string does, so that dword still
+    // holds a string byte (never a page the string is not on).
+#if HALO_XXH3_X3
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+    typedef const __attribute__((address_space(1))) u32x3 gdw3;
+    auto word = [&](uint32_t stripe) -> uint64_t {
+        const u32x3 v = *(gdw3*)(q0 + 16 * stripe);
+        return join64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
+    };
+#else
     auto word = [&](uint32_t stripe) -> uint64_t {  // input word j of stripe `stripe`
         gdw* r = q0 + 16 * stripe;
         const uint32_t w0 = r[0], w1 = r[1];
         const uint32_t w2 = sh ? r[2] : 0u;
         return join64(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh));
     };
+#endif
+    constexpr uint32_t B = HALO_XXH3_BATCH;  // stripes whose loads are issued together
     uint32_t stripe = 0, remaining = len;
     while (remaining > 1024) {
 #pragma unroll 1
-        for (uint32_t st = 0; st < 16; st += 4) {
-            uint64_t w[4];
+        for (uint32_t st = 0; st < 16; st += B) {
+            uint64_t w[B];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) w[u] = word(stripe + st + u);
+            for (uint32_t u = 0; u < B; ++u) w[u] = word(stripe + st + u);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) stripe_acc(acc, w[u], sec.w8[st + u + j]);
+            for (uint32_t u = 0; u < B; ++u) stripe_acc(acc, w[u], sec.w8[st + u + j]);
         }
         stripe += 16;
         remaining -= 1024;
@@ -212,12 +235,12 @@ __device__ uint64_t hash_long8(const uint8_t* d, uint32_t len, uint32_t j, const
     }
     const uint32_t stripes = (remaining - 1) / 64;
     uint32_t st = 0;
-    for (; st + 4 <= stripes; st += 4) {
-        uint64_t w[4];
+    for (; st + B <= stripes; st += B) {
+        uint64_t w[B];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) w[u] = word(stripe + st + u);
+        for (uint32_t u = 0; u < B; ++u) w[u] = word(stripe + st + u);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) stripe_acc(acc, w[u], sec.w8[st + u + j]);
+        for (uint32_t u = 0; u < B; ++u) stripe_acc(acc, w[u], sec.w8[st + u + j]);
     }
     for (; st < stripes; ++st) stripe_acc(acc, word(stripe + st), sec.w8[st + j]);
     stripe_acc(acc, ld64(d + len - 64 + 8 * j), sec.last[j]);  // last stripe, secret offset 121
@@ -289,9 +312,9 @@ __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
 // strings > 240 B: each wave scans 64 strings, ranks its long ones by length (longest first) and
 // hashes them eight at a time, one per 8-lane group — rank order keeps the eight strings of a
 // round about equally long, so groups do not idle behind the round's longest string
-__global__ void __launch_bounds__(256) xxh3_long_kernel(const XxhParams p) {
+__global__ void __launch_bounds__(HALO_XXH3_LONG_BLOCK) xxh3_long_kernel(const XxhParams p) {
     __shared__ LongSecrets s_sec;
-    __shared__ uint8_t s_order[4][64];  // per wave: lane holding the string of each rank
+    __shared__ uint8_t s_order[HALO_XXH3_LONG_BLOCK / 64][64];  // per wave: lane holding the string of each rank
     load_secrets(s_sec);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -370,7 +393,9 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
     hipLaunchKernelGGL(halo::xxh3_short_kernel, dim3(halo::blocks_for((n + halo::kShortScan / 64 - 1) /
                                                                        (halo::kShortScan / 64))),
                        dim3(256), 0, s, p);
-    hipLaunchKernelGGL(halo::xxh3_long_kernel, dim3(halo::blocks_for(n)), dim3(256), 0, s, p);
+    constexpr uint32_t wpb = HALO_XXH3_LONG_BLOCK / 64;
+    const uint32_t long_blocks = (uint32_t)(((uint64_t)halo::blocks_for(n) * 4 + wpb - 1) / wpb);
+    hipLaunchKernelGGL(halo::xxh3_long_kernel, dim3(long_blocks), dim3(HALO_XXH3_LONG_BLOCK), 0, s, p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 
