@@ -180,11 +180,14 @@ __device__ __forceinline__ void stripe_acc(uint64_t& acc, uint64_t in, uint64_t 
 #ifndef HALO_XXH3_X3
 #define HALO_XXH3_X3 1
 #endif
+// Stripes per load batch and threads per block of the long kernel: 4 and one-wave blocks
+// (profiles/r02/ab_xxh3_batch_block.log: 8 / 16 stripes 11 / 30 % slower, one-wave blocks 2 %
+// faster than 256-thread ones).
 #ifndef HALO_XXH3_BATCH
 #define HALO_XXH3_BATCH 4
 #endif
 #ifndef HALO_XXH3_LONG_BLOCK
-#define HALO_XXH3_LONG_BLOCK 256
+#define HALO_XXH3_LONG_BLOCK 64
 #endif
 // hashLong (xxh3.go:132-178) on a group of 8 lanes; lane j = accumulator j. Result in every lane.
 // Stripe words are read as aligned dwords (three when the string is not 4-byte aligned) four
