@@ -979,8 +979,14 @@ rx_stream_kernel(const RxParams p) {
     flush_hist(p, hist);
 }
 
+// Grid cap, in 4-wave blocks (the lane kernel scales it to its block size). Effectively no cap:
+// a launch takes one wave per 64 frames (per frame group) and lets the dispatcher refill CUs as
+// waves finish. The round-1 cap of 16384 blocks made waves loop over several groups in big batches,
+// and a looping wave serialises its round trips: lifting it took 16M x 64 B 314 -> 294 us,
+// 128M x 64 B 2.74 -> 2.32 ms, IMIX 1.32 -> 1.28 ms, jumbo 6.20 -> 6.14 ms, 1500 B within noise
+// (profiles/r02/ab_grid_cap_raised.log).
 #ifndef HALO_RX_MAX_BLOCKS
-#define HALO_RX_MAX_BLOCKS (256ull * 8 * 8)  // 256 CUs x 8 resident blocks x 8 rounds
+#define HALO_RX_MAX_BLOCKS 4194304ull
 #endif
 #ifndef HALO_RX_LANE_MAX_BLOCKS
 #define HALO_RX_LANE_MAX_BLOCKS HALO_RX_MAX_BLOCKS

@@ -30,6 +30,7 @@ def main():
         ("64B", dict(length=64), 1 << 20, 8, [1, -1, -2]),
         ("64B4M", dict(length=64), 4 << 20, 2, [1]),
         ("64B16M", dict(length=64), 16 << 20, 1, [1]),
+        ("64B128M", dict(length=64), 128 << 20, 1, [1]),
         ("128B", dict(length=128), 1 << 20, 8, [1, 4, -1, -2]),
         ("570B", dict(length=570), 1 << 20, 2, [4, 8, -1, -2]),
         ("1500B", dict(length=1500), 1 << 20, 2, [4, 8, -1, -2]),
