@@ -71,6 +71,30 @@ __device__ __forceinline__ void acc_segment(const uint32_t (&w)[4], uint32_t d0,
     }
 }
 
+// Lane-per-frame form of acc_segment (G = 1): the end mask from one clamped shift (v_med3 + a
+// 64-bit shift) instead of two compares and selects, and each dword's two 16-bit halves added into
+// a u32 with one v_dot2_u32_u16 instead of a 64-bit add. A halves sum keeps the value mod 0xFFFF
+// (2^16 == 1) and is zero exactly when the masked bytes are, which is all fold16 looks at; it stays
+// below 2^32 for any frame (<= 2254 dwords x 2 x 0xFFFF). e8 = 8 * seg_end.
+#ifndef HALO_RX_LANE_DOT2
+#define HALO_RX_LANE_DOT2 1
+#endif
+template <bool L3>
+__device__ __forceinline__ void acc_segment_dot2(const uint32_t (&w)[4], uint32_t d0, int32_t e8, uint32_t& h) {
+    constexpr uint32_t kSeg = kIpOff<L3> + 20u;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 one = {1, 1};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t d = d0 + j;
+        const int32_t r8 = e8 - (int32_t)(32u * d);
+        const int32_t sh = r8 < 0 ? 0 : (r8 > 32 ? 32 : r8);  // segment bits left in this dword
+        uint32_t keep = (uint32_t)~(~0ull << sh);
+        keep &= d >= (kSeg + 3u) / 4u ? 0xFFFFFFFFu : ((kSeg & 2u) && d == kSeg / 4u ? 0xFFFF0000u : 0u);
+        h = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w[j] & keep), one, h, false);
+    }
+}
+
 struct Verdict {
     uint32_t status, flags, ethertype, ip_proto, ip_total_len, src_ip, dst_ip, sport, dport;
     uint32_t pay_off, pay_len, l4_aux, l4_seq, l4_ack;
@@ -369,7 +393,21 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
 
     // L4 segment sum over [kIpOff + 20, seg_end): round 0 from registers, then U chunks per round
     uint64_t c = 0;
-    if (v.seg_end) {
+    if (v.seg_end && G == 1 && HALO_RX_LANE_DOT2) {
+        uint32_t hs = 0;
+        const int32_t e8 = (int32_t)(8u * v.seg_end);
+#pragma unroll
+        for (int u = 0; u < U0; ++u) acc_segment_dot2<L3>(st.buf[u], u * 4, e8, hs);
+        const uint32_t seg_dw = (v.seg_end + 3) >> 2;
+        for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
+            uint32_t x[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load4(st.frame, r0 + u * 4, seg_dw, x[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc_segment_dot2<L3>(x[u], r0 + u * 4, e8, hs);
+        }
+        c = hs;
+    } else if (v.seg_end) {
 #pragma unroll
         for (int u = 0; u < U0; ++u) acc_segment<L3>(st.buf[u], (u * G + gl) * 4, v.seg_end, c);
         const uint32_t seg_dw = (v.seg_end + 3) >> 2;
