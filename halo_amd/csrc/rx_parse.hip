@@ -835,10 +835,19 @@ __device__ __forceinline__ void stream_sum(const uint32_t (&x)[4][4], uint32_t l
 // has passed; the header checks run once after the stream. Every byte of a dense window is then
 // fetched from HBM exactly once. Without HDR (checksums off: only ICMP frames have a segment),
 // the lane reads its header first and the stream covers only the windows' segments.
-template <int LAYOUT, int FUSE, bool HDR>
-__global__ void __launch_bounds__(HALO_RX_STREAM_BLOCK) __attribute__((amdgpu_waves_per_eu(HALO_RX_STREAM_WAVES)))
+// Mixed-size batches (IMIX) take the stream kernel in one-wave blocks with 1.5 KB of LDS padding
+// (22 blocks = 5.5 waves per SIMD resident): IMIX 1.27 -> 1.25 ms; uniform batches keep 256-thread
+// blocks, which the 570 B line prefers (127 vs 133 us; profiles/r02/ab_stream_group_block_uncapped.log).
+#ifndef HALO_RX_STREAM_MIXED_BLOCK
+#define HALO_RX_STREAM_MIXED_BLOCK 64
+#endif
+#ifndef HALO_RX_STREAM_MIXED_LDS_PAD
+#define HALO_RX_STREAM_MIXED_LDS_PAD 1536
+#endif
+template <int LAYOUT, int FUSE, bool HDR, int BLK = HALO_RX_STREAM_BLOCK>
+__global__ void __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(HALO_RX_STREAM_WAVES)))
 rx_stream_kernel(const RxParams p) {
-    constexpr int kW = HALO_RX_STREAM_BLOCK / 64;
+    constexpr int kW = BLK / 64;
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     __shared__ uint4 s_x[kW][kStreamStep / 16];       // per wave: the step's bytes (records at the end)
     __shared__ uint32_t s_base[kW][kStreamStep / 16];  // per wave: P at each 16-byte sub-chunk
@@ -1029,7 +1038,7 @@ rx_stream_kernel(const RxParams p) {
 #ifndef HALO_RX_LANE_MAX_BLOCKS
 #define HALO_RX_LANE_MAX_BLOCKS HALO_RX_MAX_BLOCKS
 #endif
-constexpr int kVariantMix = -1, kVariantStream = 2;
+constexpr int kVariantMix = -1, kVariantStream = 2, kVariantStreamMixed = 3;
 
 uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS,
                   uint32_t waves_per_block = 4) {
@@ -1056,6 +1065,16 @@ hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
                 hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, true>), g, b, HALO_RX_STREAM_LDS_PAD, s, p);
             else
                 hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, false>), g, b, HALO_RX_STREAM_LDS_PAD, s, p);
+            break;
+        }
+        case kVariantStreamMixed: {
+            constexpr int BLK = HALO_RX_STREAM_MIXED_BLOCK;
+            constexpr uint32_t wpb = BLK / 64;
+            const dim3 g(grid_for(p.n, 64, HALO_RX_MAX_BLOCKS * 4 / wpb, wpb)), b(BLK);
+            if (HALO_RX_STREAM_HDR && (p.flags & HALO_RX_CSUM_ENABLE))
+                hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, true, BLK>), g, b, HALO_RX_STREAM_MIXED_LDS_PAD, s, p);
+            else
+                hipLaunchKernelGGL((rx_stream_kernel<LAYOUT, FUSE, false, BLK>), g, b, HALO_RX_STREAM_MIXED_LDS_PAD, s, p);
             break;
         }
         case 4: case 8: case 16: {
@@ -1092,7 +1111,7 @@ int pick_variant(uint32_t max_len, bool uniform, bool dense, uint32_t flags) {
     }
     if (flags & HALO_RX_UNIFORM_LEN) uniform = max_len != 0;
     if (max_len != 0 && max_len <= 64) return 1;
-    if (!uniform) return dense ? kVariantStream : kVariantMix;
+    if (!uniform) return dense ? kVariantStreamMixed : kVariantMix;
     if (max_len <= 1024) return dense ? kVariantStream : max_len <= 128 ? 1 : 4;
     if (max_len <= 4096) return 8;
     return 16;
