@@ -8,12 +8,16 @@ one batch of 1M frames. Batches rotate over --rotate distinct slices of the synt
 so the working set (8 x 102 MB) exceeds the 256 MB Infinity Cache and every step streams
 from HBM.
 
-Multi-GPU (torchrun, one process per GPU, --gpus N > 1): BASELINE config 4, the scaling run —
-128M x 64 B frames sharded by index, 128M/N per rank (strong scaling), one launch per step over
-the rank's whole shard. No data-path collective: the gloo group carries only the barrier, the
-max-over-ranks wall time and every rank's own average launch duration (per_rank_kernel_ms).
-value = 128M x steps / max wall time. At N=1 the headline stays config 2 (BASELINE's metric
-config) and the same config-4 run on one GPU is reported under "config4", the curve's 1-GPU point.
+Multi-GPU (--gpus N, one process per GPU): BASELINE config 4, the scaling run. Every rank owns
+one contiguous 16M-frame slice of the 64 B frame stream (rank r: global frames [r*16M, (r+1)*16M),
+so N = 8 covers config 4's 128M frames) and runs exactly the N=1 headline step on it: one
+1M-frame launch per step, rotating over its 16 batches (weak scaling: the work per GPU is fixed).
+No data-path collective: the gloo group carries only the barriers, the max-over-ranks wall time
+and per-rank facts (launch duration, PCI bus id, the shard's own validation). value = N x 1M x
+steps / max wall time. When --gpus N > 1 is given without a launcher around it (WORLD_SIZE unset),
+bench.py starts torch.distributed.run as a CHILD process (never an exec) before anything touches
+the GPU, and exits with its return code; rank 0's JSON line is the child's stdout. A WORLD_SIZE
+that disagrees with --gpus is refused (exit 2).
 
 Extra fields: roofline (dominant kernel, algorithmic bytes / HIP-event kernel time vs the
 8 TB/s HBM3E spec peak), cpu_baseline (the C oracle, a scalar port of the Go path, timed on
@@ -47,7 +51,8 @@ def parse_args():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per batch per GPU")
-    p.add_argument("--rotate", type=int, default=8, help="distinct batches cycled through")
+    p.add_argument("--rotate", type=int, default=16,
+                   help="distinct batches cycled through (frames x rotate = one GPU's shard: 16M = config 4 / 8)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-secondary", action="store_true")
@@ -90,15 +95,138 @@ class Dist:
         self.pg.all_gather(parts, torch.tensor([x], dtype=torch.float64))
         return [float(t.item()) for t in parts]
 
+    def gather_obj(self, x) -> list:
+        """A small JSON-able object from every rank, in rank order (gloo, host memory only)."""
+        if not self.pg:
+            return [x]
+        parts = [None] * self.world
+        self.pg.all_gather_object(parts, x)
+        return parts
+
     def close(self):
         if self.pg:
             self.pg.destroy_process_group()
+
+
+def rank_plan(gpus: int, env) -> str:
+    """How this invocation runs: "single" (N = 1, no launcher), "ranks" (one rank of a launched
+    N-rank job whose WORLD_SIZE equals --gpus), "spawn" (--gpus N > 1 and no launcher: start
+    torch.distributed.run as a child) or "mismatch" (a launcher whose WORLD_SIZE is not --gpus)."""
+    world = env.get("WORLD_SIZE")
+    if world is None:
+        return "spawn" if gpus > 1 else "single"
+    return "ranks" if int(world) == gpus else "mismatch"
+
+
+def launch_ranks(gpus: int, argv: list) -> int:
+    """Run this script as an N-rank job under torch.distributed.run in a CHILD process and return its
+    exit code. Called before anything in this process touches the GPU (no exec: the box forbids
+    replacing a process that has initialised it). Rank 0's JSON line reaches our stdout directly."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"[launcher] --gpus {gpus} without WORLD_SIZE: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def shard_first_index(rank: int, batch: int, n: int, rotate: int) -> int:
     """Global index of the first frame of `batch` on `rank`: ranks own disjoint, contiguous
     slices of the synthetic stream (index sharding) and never exchange data."""
     return (rank * rotate + batch) * n
+
+
+def shard_batches(dev, netif, *, rank: int, n: int, rotate: int):
+    """One rank's shard of the 64 B frame stream — global frames [rank*n*rotate, (rank+1)*n*rotate)
+    — generated as ONE contiguous ragged batch on the rank's GPU, and the `rotate` n-frame batches
+    the timed steps cycle through as views of it (batch b = frames shard_first_index(rank, b, ..),
+    byte base at its first frame, offsets rebased to it). Frame i depends only on (seed, i), so
+    the views hold exactly the frames make_batches generates for the same indices."""
+    import numpy as np
+    import torch
+
+    from halo_amd import synth
+
+    first = shard_first_index(rank, 0, n * rotate, 1)
+    lay = synth.layout(n * rotate, length=64, first_index=first)
+    shard = synth.frames_device(lay, netif, device=dev)
+    shard["layout"] = lay
+    batches = []
+    for b in range(rotate):
+        lo = b * n
+        assert first + lo == shard_first_index(rank, b, n, rotate)
+        o0 = int(lay["offsets_dw"][lo])
+        offs = (lay["offsets_dw"][lo:lo + n] - np.uint32(o0)).astype(np.uint32)
+        sub = {"n": n, "lens": lay["lens"][lo:lo + n], "offsets_dw": offs, "kinds": lay["kinds"][lo:lo + n],
+               "seed": lay["seed"], "first_index": first + lo}
+        batches.append({"bytes": shard["bytes"][4 * o0:], "offsets_dw": torch.from_numpy(offs.view(np.int32)).to(dev),
+                        "lens": shard["lens"][lo:lo + n], "layout": sub})
+    return batches, shard
+
+
+def validate_shard(batches, netif, dev, rank: int, flips: int = 64) -> dict:
+    """After the timed steps, on the rank's own device, through the product entry point:
+    (1) every batch of the shard parsed once more with a status histogram — the histogram must sum
+        to the shard's frame count and every (clean, synthetic) frame must be OK;
+    (2) a known-answer probe: one bit flipped in each of `flips` seeded frames of batch 0 (a byte in
+        [14, 64): IPv4 header or UDP segment, so the IPv4 header or UDP checksum must catch it) must
+        turn exactly those frames to a failing status and leave every other frame OK. The flips are
+        undone afterwards. No oracle: the expected answers follow from the one's-complement sum."""
+    import numpy as np
+    import torch
+
+    from halo_amd import protocol
+
+    n = batches[0]["layout"]["n"]
+    hist = torch.zeros(14, dtype=torch.int32, device=dev)
+    out = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
+    ok = torch.zeros((), dtype=torch.int64, device=dev)
+    for b in batches:
+        protocol.parse_frames_batch(b["bytes"], b["offsets_dw"], b["lens"], netif=netif, max_len_hint=64, out=out,
+                                    hist=hist)
+        ok += (out[:, 0] == 0).sum()
+    h = hist.cpu().numpy().astype(np.int64)
+    frames = n * len(batches)
+    rng = np.random.default_rng(0x464C4950 + rank)
+    idx = np.sort(rng.choice(n, size=min(flips, n), replace=False))
+    pos = batches[0]["layout"]["offsets_dw"][idx].astype(np.int64) * 4 + rng.integers(14, 64, idx.size)
+    bit = (1 << rng.integers(0, 8, idx.size)).astype(np.uint8)
+    b0 = batches[0]["bytes"]
+    pos_d, bit_d = torch.from_numpy(pos).to(dev), torch.from_numpy(bit).to(dev)
+    b0[pos_d] ^= bit_d
+    protocol.parse_frames_batch(b0, batches[0]["offsets_dw"], batches[0]["lens"], netif=netif, max_len_hint=64,
+                                out=out)
+    st = out[:, 0].cpu().numpy()
+    b0[pos_d] ^= bit_d
+    torch.cuda.synchronize()
+    flipped = np.zeros(n, bool)
+    flipped[idx] = True
+    probe = {"flipped": int(idx.size), "rejected": int((st[flipped] != 0).sum()),
+             "others_ok": bool((st[~flipped] == 0).all())}
+    res = {"frames": frames, "hist_sum": int(h.sum()), "ok_frames": int(ok.item()), "hist_ok": int(h[0]),
+           "flip_probe": probe}
+    res["valid"] = bool(res["hist_sum"] == frames and res["ok_frames"] == frames and res["hist_ok"] == frames
+                        and probe["rejected"] == probe["flipped"] and probe["others_ok"])
+    return res
+
+
+def device_identity(gpu: int) -> dict:
+    """PCI bus id (hipDeviceGetPCIBusId) and name of the device this rank runs on."""
+    import ctypes
+
+    import torch
+
+    buf = ctypes.create_string_buffer(64)
+    rc = bench_lib().halo_bench_pci_bus_id(gpu, buf, len(buf))
+    return {"device": gpu, "pci_bus_id": buf.value.decode() if rc == 0 else f"error {rc}",
+            "name": torch.cuda.get_device_name(gpu)}
 
 
 def make_batches(dev, netif, *, n, rotate, rank, length=64, size_mode=0, proto_mode=0, strided=False):
@@ -161,6 +289,8 @@ def bench_lib():
         L.halo_bench_stream_rw.argtypes = [vp, vp, i32, u64, u64, vp] + tail
         L.halo_bench_ring_scan_steps.restype = ctypes.c_int
         L.halo_bench_ring_scan_steps.argtypes = [i32, vp, u64, u64, u32, vp, vp, vp, vp, u64] + tail
+        L.halo_bench_pci_bus_id.restype = ctypes.c_int
+        L.halo_bench_pci_bus_id.argtypes = [i32, ctypes.c_char_p, i32]
         _BENCH_LIB = L
     return _BENCH_LIB
 
@@ -195,44 +325,34 @@ def time_steps(batches, out, netif, *, flags, hint, steps, warmup, d: Dist, stri
     return d.max(wall.value), region.value / steps
 
 
-CONFIG4_FRAMES = 128 << 20  # BASELINE configs[3]: 128M x 64 B IPv4/UDP, sharded by index
+CONFIG4_FRAMES = 128 << 20  # BASELINE configs[3]: 128M x 64 B IPv4/UDP, sharded by index over 8 GPUs
+CONFIG4_PER_GPU = CONFIG4_FRAMES // 8  # one GPU's shard: 16M frames = bench.py's default frames x rotate
 
 
-def config4_shard(rank: int, world: int, total: int = CONFIG4_FRAMES):
+def config4_shard(rank: int, per: int = CONFIG4_PER_GPU):
     """(first global frame index, frame count) of `rank`'s config-4 shard: contiguous, disjoint,
-    equal ranges covering [0, total) (total is a multiple of 1, 2, 4 and 8)."""
-    per = total // world
-    assert per * world == total, (total, world)
+    equal ranges; ranks 0..7 together cover config 4's [0, 128M)."""
     return rank * per, per
 
 
-def config4_run(dev, netif, d: Dist, steps: int, warmup: int) -> dict:
-    """BASELINE config 4 on the ranks of this job: the 128M x 64 B frame stream sharded by index,
-    rank r parsing global frames [r * 128M/N, (r + 1) * 128M/N) on its own GPU, one launch per step
-    over its whole shard (strong scaling: the total is fixed). No data-path collective: the gloo
-    group carries only the start barrier, the max-over-ranks wall time and each rank's own average
-    launch duration. value = 128M frames x steps / max wall."""
+def config4_one_gpu(dev, netif, d: Dist, steps: int, warmup: int) -> dict:
+    """All of BASELINE config 4 on ONE GPU: the 128M x 64 B frames (8 GB + 4 GB of records) in one
+    launch per step — what one GPU does with the whole job, beside the N-rank curve."""
     import torch
 
-    first, per = config4_shard(d.rank, d.world)
-    log(f"[rank {d.rank}] config4: generating {per} frames of 64 B (global frames {first}..)")
-    assert shard_first_index(d.rank, 0, per, 1) == first
-    fr = make_batches(dev, netif, n=per, rotate=1, rank=d.rank)
+    per = CONFIG4_FRAMES
+    log(f"[rank {d.rank}] config4 on one GPU: generating {per} frames of 64 B")
+    fr = make_batches(dev, netif, n=per, rotate=1, rank=0)
     out = torch.empty((per, RESULT_BYTES), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     wall, kms = time_steps(fr, out, netif, flags=1, hint=64, steps=steps, warmup=warmup, d=d)
-    per_rank = d.gather(kms)
     fb = frame_bytes(fr[0])
     alg = fb + per * (4 + 2 + RESULT_BYTES)
-    res = {"workload": f"config4: {CONFIG4_FRAMES >> 20}M x 64B IPv4/UDP frames sharded by index over {d.world} "
-                       f"GPU(s), {per >> 20}M frames per GPU per step, CheckSumEnable=true, 32B record/frame",
-           "frames_total": CONFIG4_FRAMES, "frames_per_rank": per, "steps": steps,
-           "value": round(CONFIG4_FRAMES * steps / wall / 1e6, 2), "unit": "Mpps",
-           "gbit_s": round(fb * d.world * steps * 8 / wall / 1e9, 2),
-           "ms_per_step": round(wall / steps * 1e3, 4), "scaling": "strong",
-           "per_rank_kernel_ms": [round(k, 5) for k in per_rank],
-           "roofline_rank0": roofline(alg, per_rank[0], load_traffic(f"config4_{per >> 20}M")),
-           "alg_bytes_per_rank_launch": alg}
+    res = {"workload": f"config4 whole on one GPU: {per >> 20}M x 64B IPv4/UDP frames in one launch per step, "
+                       "CheckSumEnable=true, 32B record/frame",
+           "frames": per, "steps": steps, "value": round(per * steps / wall / 1e6, 2), "unit": "Mpps",
+           "gbit_s": round(fb * steps * 8 / wall / 1e9, 2), "ms_per_step": round(wall / steps * 1e3, 4),
+           "kernel_ms": round(kms, 5), "roofline": roofline(alg, kms), "alg_bytes_per_launch": alg}
     del fr, out
     torch.cuda.empty_cache()
     return res
@@ -872,11 +992,19 @@ def cpu_baseline(fr, seconds: float):
 
 def main():
     args = parse_args()
+    plan = rank_plan(args.gpus, os.environ)
+    if plan == "spawn":  # nothing has touched the GPU in this process: run the N ranks as a child job
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if plan == "mismatch":
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}: refusing to report a "
+            "line whose n_gpus is not the job's rank count")
+        sys.exit(2)
     import numpy as np  # noqa: F401
     import torch
 
     d = Dist()
-    # one process per GPU; ranks beyond the visible devices share them (rehearsals on fewer GPUs)
+    # one process per GPU; ranks beyond the visible devices share them (rehearsals on fewer GPUs:
+    # the line's distinct_devices says so)
     gpu = d.local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -887,52 +1015,74 @@ def main():
     netif = NetIf.make()  # eth0 of example.UsePcapDev (example/example.go:768-773)
     measure_read_peak(dev, d)
     n = args.frames
-    if d.world > 1:
-        # BASELINE config 4, the scaling-curve run: 128M x 64 B sharded by index over the N GPUs
-        c4 = config4_run(dev, netif, d, args.steps, args.warmup)
-        line = {
-            "metric": METRIC, "value": c4["value"], "unit": "Mpps", "n_gpus": d.world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": c4["ms_per_step"], "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": c4["workload"], "frames_total": CONFIG4_FRAMES,
-                       "frames_per_gpu_per_step": c4["frames_per_rank"], "frame_bytes": 64,
-                       "parallelism": f"index-sharded x{d.world}, no collective"},
-            "gbit_s": c4["gbit_s"], "per_rank_kernel_ms": c4["per_rank_kernel_ms"],
-            "kernel_ms": max(c4["per_rank_kernel_ms"]),
-            "kernel": "rx_lane_kernel<0, 0> (lane per frame, ragged, no fused pass)",
-            "roofline": c4["roofline_rank0"], "cpu_baseline": None,
-            "note": "N=1 runs report BASELINE config 2 as value and this same config-4 run on one GPU under "
-                    "'config4' (the 1-GPU point of this curve)"}
-        d.close()
-        if d.rank == 0:
-            print(json.dumps(line), flush=True)
-        return
+    shard_frames = n * args.rotate
 
-    log(f"[rank {d.rank}] generating {args.rotate} x {n} frames of 64 B")
-    batches = make_batches(dev, netif, n=n, rotate=args.rotate, rank=d.rank)
+    # The headline step on every rank (config 2 at N = 1; config 4's scaling curve at N > 1): one
+    # n-frame launch per step over the rank's own shard of the global stream, batches rotating.
+    log(f"[rank {d.rank}] generating a {shard_frames}-frame shard of 64 B (global frames "
+        f"{shard_first_index(d.rank, 0, shard_frames, 1)}..) as {args.rotate} x {n}-frame batches")
+    batches, shard = shard_batches(dev, netif, rank=d.rank, n=n, rotate=args.rotate)
     out = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     wall, kern_ms = time_steps(batches, out, netif, flags=1, hint=64, steps=args.steps, warmup=args.warmup, d=d)
+    per_rank_kms = d.gather(kern_ms)
     frames_total = n * args.steps * d.world
     mpps = frames_total / wall / 1e6
     fbytes = frame_bytes(batches[0])
     gbit = fbytes * args.steps * d.world * 8 / wall / 1e9
     alg = fbytes + n * (4 + 2 + RESULT_BYTES)  # frames + dword offset + u16 len + record
+    # every rank checks its own shard on its own device after the timed region, and says which device
+    ident = device_identity(gpu)
+    ident["rank"] = d.rank
+    ident["kernel_ms"] = round(kern_ms, 5)
+    ident["validation"] = validate_shard(batches, netif, dev, d.rank)
+    ranks = d.gather_obj(ident)
+    distinct = len({r["pci_bus_id"] for r in ranks}) == d.world
+    if d.world == 1:
+        workload = ("config2: 1M x 64B IPv4/UDP frames resident in HBM, CheckSumEnable=true, ragged ring-record "
+                    "layout (u32 dword offsets + u16 lens), 32B record/frame")
+    else:
+        workload = (f"config4: 64B IPv4/UDP frames index-sharded over {d.world} GPUs, {shard_frames >> 20}M frames "
+                    f"per GPU ({d.world * shard_frames >> 20}M in all; 128M at N=8), each GPU parsing {n >> 20}M "
+                    "frames per step (the N=1 headline step), CheckSumEnable=true, 32B record/frame")
     line = {
         "metric": METRIC, "value": round(mpps, 2), "unit": "Mpps", "n_gpus": d.world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": "config2: 1M x 64B IPv4/UDP frames resident in HBM, CheckSumEnable=true, "
-                               "ragged ring-record layout (u32 dword offsets + u16 lens), 32B record/frame",
-                   "frames_per_gpu_per_step": n, "frame_bytes": 64, "rotating_batches": args.rotate,
+        "config": {"workload": workload, "frames_per_gpu_per_step": n, "frame_bytes": 64,
+                   "rotating_batches": args.rotate, "frames_per_gpu": shard_frames,
+                   "frames_total": shard_frames * d.world,
                    "parallelism": f"index-sharded x{d.world}, no collective"},
         "gbit_s": round(gbit, 2),
-        "kernel_ms": round(kern_ms, 5),
+        "kernel_ms": round(max(per_rank_kms), 5),
+        "per_rank_kernel_ms": [round(k, 5) for k in per_rank_kms],
         "kernel": "rx_lane_kernel<0, 0> (lane per frame, ragged, no fused pass)",
         "roofline": roofline(alg, kern_ms, load_traffic("config2")),
         "alg_bytes_per_launch": alg,
+        "per_rank": ranks,
+        "distinct_devices": distinct,
+        "validated": all(r["validation"]["valid"] for r in ranks),
         "cpu_baseline": None,
     }
+    if d.world > 1:
+        # the same shards, each parsed whole in ONE launch per step (16M frames per GPU per launch)
+        sh_out = torch.empty((shard_frames, RESULT_BYTES), dtype=torch.uint8, device=dev)
+        st = max(5, args.steps // 5)
+        w2, k2 = time_steps([shard], sh_out, netif, flags=1, hint=64, steps=st, warmup=2, d=d)
+        ks = d.gather(k2)
+        line["whole_shard_launch"] = {
+            "value": round(shard_frames * d.world * st / w2 / 1e6, 2), "unit": "Mpps", "steps": st,
+            "ms_per_step": round(w2 / st * 1e3, 4), "per_rank_kernel_ms": [round(k, 5) for k in ks],
+            "what": f"each GPU's {shard_frames >> 20}M-frame shard in one launch per step"}
+        del sh_out
+        if not distinct:
+            line["note"] = ("ranks shared a device (fewer GPUs than ranks): a rehearsal of the N-rank path, "
+                            "not a scaling point")
+        d.close()
+        if d.rank == 0:
+            print(json.dumps(line), flush=True)
+        sys.exit(0 if line["validated"] else 3)
+    del shard
     line["roofline"]["note"] = ("achieved = (frame bytes + 6 B metadata + 32 B record) per launch / average "
                                 "launch duration (one HIP event pair over the timed region / steps); "
                                 "peak = HBM3E spec; traffic = 2 x FETCH_SIZE + WRITE_SIZE per launch from "
@@ -992,7 +1142,7 @@ def main():
         torch.cuda.empty_cache()
         sec["route_lpm_500k_prefixes"] = route_secondary(dev, max(10, args.steps // 4), 3, d, with_cpu=not args.no_cpu)
         torch.cuda.empty_cache()
-        line["config4"] = config4_run(dev, netif, d, max(20, args.steps // 4), 3)
+        line["config4_128M_one_gpu"] = config4_one_gpu(dev, netif, d, max(20, args.steps // 4), 3)
         for name, kw, hint, strided_len, flags in [
             ("config4_shard_16M_64B", dict(length=64), 64, 0, 1),
             ("1500B_udp_1M", dict(length=1500), 1500, 0, 1 | _lib.HALO_RX_UNIFORM_LEN),
@@ -1038,6 +1188,8 @@ def main():
     d.close()
     if d.rank == 0:
         print(json.dumps(line), flush=True)
+    if not line["validated"]:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -710,7 +710,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
 // fetched once, in full 128-byte lines, whatever the sizes, and no lane waits on a longer
 // neighbour. The step's bytes and its prefix at each 16-byte sub-chunk go to LDS; a lane whose
 // segment starts or ends in the step reads its prefix back from there. A window whose frames are
-// not dense in memory (span > 2 x their segment bytes + 8 KB) sums each frame on its own lane.
+// not dense in memory (span > 2 x their segment bytes + 8 KB, or a 4 KB page of the span holding
+// no frame byte: window_pages_covered) sums each frame on its own lane.
 constexpr uint32_t kStreamStep = 4096;  // bytes per wave per step: 64 lanes x 64 B
 
 template <typename Op>
@@ -776,10 +777,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // This lane's 64 bytes of the step at s0 (sub-chunk u at s0 + 1024u + 16 lane, so each load
 // instruction reads 1 KB contiguous): always four 16-byte loads, no branch, so the load counter
-// stays exact across steps. Positions are 16-byte aligned in memory, and a 16-byte aligned block
-// never straddles a page, so a block holding any byte of the window's frames [lo, hi) is
-// readable; a sub-chunk wholly outside reads the nearest such block instead. Bytes outside the
-// frames are never inside a segment or header, and P differences cancel them.
+// stays exact across steps. Positions are 16-byte aligned in memory and a window streams only
+// when every page of [lo, hi) holds a frame dword (window_pages_covered), so every block in
+// [lo, hi) is readable; a sub-chunk wholly outside reads the nearest such block instead. Bytes
+// outside the frames are never inside a segment or header, and P differences cancel them.
 __device__ __forceinline__ void stream_load(uint64_t B, uint32_t s0, uint32_t lane, uint32_t lo, uint32_t hi,
                                             uint32_t (&x)[4][4]) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(16)));
@@ -791,6 +792,29 @@ __device__ __forceinline__ void stream_load(uint64_t B, uint32_t s0, uint32_t la
         const u32x4 q = *(const __attribute__((address_space(1))) u32x4*)(B + a);
         x[u][0] = q.x; x[u][1] = q.y; x[u][2] = q.z; x[u][3] = q.w;
     }
+}
+
+// The read contract of include/halo_rx.h: no kernel reads a page that holds no frame byte. The
+// stream reads every 16-byte block in [lo, hi) (clamped to it), so a window streams only when
+// every 4 KB page of [lo, hi) holds a readable dword of one of its frames (member lanes `in`,
+// frame dwords [ps, ps + nb)); pg0 = the stream base's offset in its page, so (position + pg0)
+// >> 12 counts real pages. Pages are checked 32 at a time: each member lane ORs in the pages its
+// frame touches, and the wave's union must be all of them. A window with a page-sized hole
+// (frames in two allocations addressed from one base, or a sparse layout the 2x density test
+// lets through) sums its frames lane by lane, reading nothing outside them.
+__device__ __forceinline__ bool window_pages_covered(bool in, uint32_t ps, uint32_t nb, uint32_t lo, uint32_t hi,
+                                                     uint32_t pg0) {
+    const uint32_t P0 = (lo + pg0) >> 12;
+    const uint32_t np = ((hi - 1u + pg0) >> 12) - P0 + 1u;
+    const uint32_t a = in ? ((ps + pg0) >> 12) - P0 : 1u, b = in ? ((ps + nb - 1u + pg0) >> 12) - P0 : 0u;
+    const auto uor = [](uint32_t x, uint32_t y) { return x | y; };
+    for (uint32_t w0 = 0; w0 < np; w0 += 32) {
+        const uint32_t w1 = np - 1u < w0 + 31u ? np - 1u : w0 + 31u;
+        const uint32_t lb = a > w0 ? a : w0, hb = b < w1 ? b : w1;
+        const uint32_t m = lb <= hb ? ((2u << (hb - lb)) - 1u) << (lb - w0) : 0u;
+        if (wave_allreduce(m, uor) != (2u << (w1 - w0)) - 1u) return false;
+    }
+    return true;
 }
 
 // A/B knobs: threads per block and dynamic LDS padding per block.
@@ -894,7 +918,8 @@ rx_stream_kernel(const RxParams p) {
                 const uint32_t sum = wave_allreduce(rd ? st.L : 0u, uadd);
                 const uint32_t G0 = lo & ~(uint32_t)(HALO_RX_STREAM_ALIGN - 1);
                 const uint32_t span = hi - G0;
-                if (!__ballot(rd && d64 >= (1ull << 31)) && span <= 2 * sum + 8192u) {
+                if (!__ballot(rd && d64 >= (1ull << 31)) && span <= 2 * sum + 8192u &&
+                    window_pages_covered(rd, ps, 4 * st.ndw, lo, hi, (uint32_t)B & 4095u)) {
 #pragma unroll
                     for (int j = 0; j < 12; ++j) h[j] = 0;
                     const uint32_t pa = ps + kSeg;
@@ -969,7 +994,8 @@ rx_stream_kernel(const RxParams p) {
                 const uint32_t sum = wave_allreduce(seg ? v.seg_end - kSeg : 0u, uadd);
                 const uint32_t G0 = S & ~(uint32_t)(HALO_RX_STREAM_ALIGN - 1);
                 const uint32_t span = E - G0;
-                if (!__ballot(seg && d64 >= (1ull << 31)) && span <= 2 * sum + 8192u) {
+                if (!__ballot(seg && d64 >= (1ull << 31)) && span <= 2 * sum + 8192u &&
+                    window_pages_covered(seg, ps, 4 * st.ndw, lo, hi, (uint32_t)B & 4095u)) {
                     uint32_t PA = 0, PB = 0, carry = 0;
                     const uint32_t ea = pe - 1;  // the segment's last byte
                     const uint32_t nsteps = (span + kStreamStep - 1) / kStreamStep;

@@ -36,9 +36,13 @@
  *              long. u32 dword offsets address 16 GiB per call.
  *   - strided: frame i starts at bytes + i*stride (stride a multiple of 4), length
  *              lens[i] or, when lens == NULL, the uniform length `len`.
- *   The kernels read no page that holds no frame byte: the per-frame kernels never read past
- *   the 4-byte word holding a frame's last byte; the byte-stream kernel (HALO_RX_VARIANT_STREAM)
- *   reads whole 16-byte-aligned blocks between a window's lowest and highest frame bytes.
+ *   Read contract: no kernel reads a 4 KB page that holds no byte of a frame of the call, so the
+ *   frames may sit in several allocations (or around unmapped holes) addressed from one base.
+ *   The per-frame kernels never read past the 4-byte word holding a frame's last byte; the
+ *   byte-stream kernel (HALO_RX_VARIANT_STREAM) reads whole 16-byte-aligned blocks between a
+ *   window's (64 consecutive frames') lowest and highest frame bytes only when every page of
+ *   that range holds a frame byte, and otherwise sums that window frame by frame. Bytes between
+ *   frames that it does read never enter a record.
  */
 #ifndef HALO_RX_H
 #define HALO_RX_H

@@ -135,3 +135,24 @@ def test_windows_without_segments(dev, oracle_lib, frames):
     data, offs, lens = _pack(sub, np.arange(n), np.zeros(n, np.int64))
     _check(dev, oracle_lib, data, offs, lens, 1, what="runts")
     _check(dev, oracle_lib, data, offs, lens, 0, what="runts flags=0")
+
+
+@pytest.mark.parametrize("flags", [1, 0])
+def test_dense_windows_with_page_holes(dev, oracle_lib, frames, flags):
+    """The read contract (include/halo_rx.h): windows that pass the 2x density test but hold a
+    hole of >= 16 KB (whole 4 KB pages with no frame byte) in the middle of every 64-frame window.
+    The stream kernel must sum those windows frame by frame (window_pages_covered) and read no
+    block in the hole; records bit-exact against the oracle. Holes of one page at every other
+    window, and of less than a page (still streamed), are mixed in."""
+    n = 12_800
+    sub = frames[:n]
+    gaps = np.zeros(n, np.int64)
+    gaps[32::64] = 4096 + 1024          # 20 KB inside every window
+    gaps[96::128] = 1024 + 3            # ~4 KB: at most one empty page at those windows
+    gaps[16::64] = 300                  # 1.2 KB: no empty page
+    data, offs, lens = _pack(sub, np.arange(n), gaps)
+    # the density test alone would stream these windows: span <= 2 x frame bytes + 8 KB
+    w0 = offs[:64]
+    span = int((w0 + lens[:64]).max() - w0.min())
+    assert span <= 2 * int(lens[:64].astype(np.int64).sum()) + 8192 and span > 16384
+    _check(dev, oracle_lib, data, offs, lens, flags, what="page holes")

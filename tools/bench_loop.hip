@@ -230,6 +230,12 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_stream_rw(const
     return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
 }
 
+// Which physical device a rank ran on (bench.py's per-rank identity in the N-GPU line).
+extern "C" __attribute__((visibility("default"))) int halo_bench_pci_bus_id(int device, char* buf, int len) {
+    if (!buf || len < 13) return HALO_E_INVAL;
+    return hipDeviceGetPCIBusId(buf, len, device) == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+
 // The fused receive + NAT flow-key pass (halo_rx_parse_flow_batch_device), rotating batches.
 extern "C" __attribute__((visibility("default"))) int halo_bench_rx_flow_steps(
     int nbatch, const uint8_t* const* bytes, const uint32_t* const* offsets_dw, const uint16_t* const* lens,
