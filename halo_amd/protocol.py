@@ -44,7 +44,8 @@ TCP_FLAGS_RST = 0x04
 TCP_FLAGS_SYN = 0x02
 TCP_FLAGS_FIN = 0x01
 
-# status -> the error the reference returns at that check (None: no error / build-defined)
+# status -> the error the reference returns at that check (None: no error / build-defined). The
+# L4 length check has one text per protocol: L4_LEN_TEXT[ip_proto] (error_text picks it).
 ERROR_TEXT = {
     "OK": None,
     "ETH_LEN": "ethernet frame len must >= 42 and <= 1514 bytes",   # ethernet.go:32
@@ -56,11 +57,26 @@ ERROR_TEXT = {
     "IP_HDR_CKSUM": "header check sum error",                       # ipv4.go:76
     "IP_TOTLEN_UNDERFLOW": None,  # Go: slice-bounds panic (ipv4.go:84)
     "IP_TOTLEN_OVERRUN": None,    # Go: stale bytes or slice-bounds panic (ipv4.go:84)
-    "L4_LEN": "udp/tcp/icmp packet len out of range",               # udp.go:23 / tcp.go:38 / icmp.go:35
+    "L4_LEN": None,               # per protocol: L4_LEN_TEXT
     "ICMP_TYPE": "not support type of icmp packet",                 # icmp.go:46
     "ICMP_CODE": "not support type of icmp packet",                 # icmp.go:50
-    "L4_CKSUM": "check sum error",                                  # udp.go:43 / tcp.go:55 / icmp.go:54
+    "L4_CKSUM": "check sum error",                                  # udp.go:43 / tcp.go:64 / icmp.go:54
 }
+L4_LEN_TEXT = {
+    IPH_PROTO_UDP: "udp packet len must >= 8 and <= 1480 bytes",    # udp.go:23
+    IPH_PROTO_TCP: "tcp packet len must >= 20 and <= 1480 bytes",   # tcp.go:38
+    IPH_PROTO_ICMP: "icmp packet len must >= 8 and <= 1480 bytes",  # icmp.go:35
+}
+
+
+def error_text(status: int, ip_proto: int = IPH_PROTO_UNKNOWN):
+    """The error string the reference function that failed returns for a record's status (None for
+    OK and for the build-defined totalLen statuses, where Go panics). L4_LEN is told apart by the
+    record's ip_proto, which ParseIpv4Pkt set before the L4 parser ran."""
+    name = STATUS_NAMES[status]
+    if name == "L4_LEN":
+        return L4_LEN_TEXT[ip_proto]
+    return ERROR_TEXT[name]
 
 
 def flags_word(check_sum_enable: bool = True, jumbo: bool = False, variant: int = 0, uniform_len: bool = False,
@@ -147,7 +163,6 @@ def status_name(code: int) -> str:
     return STATUS_NAMES[code] if 0 <= code < len(STATUS_NAMES) else "UNKNOWN"
 
 
-__all__ = [name for name in dir() if not name.startswith("_")] + ["STATUS"]
 
 
 # ---- forward / transmit direction -------------------------------------
@@ -254,3 +269,130 @@ def icmp_ttl_deep_nat_batch(frames, offsets_dw, lens, *, nat=None, check_sum_ena
         HALO_RX_CSUM_ENABLE if check_sum_enable else 0, _lib.ptr(quote), _lib.ptr(applied), _stream_handle(stream))
     _lib.check("halo_tx_icmp_deep_nat_batch_device", rc)
     return quote, applied
+
+
+# ---- single-frame Parse* with the reference's signatures ------------------------------------------
+# For callers that hold one frame or packet at a time — an Ipv4PktFwdHook (engine/engine.go:132,
+# example/example.go:162-168) or code ported from the reference — each wrapper returns exactly the
+# tuple its Go function returns, with `err` the reference's error string (None on success). The
+# frame goes through the GPU like a batch of one (halo_rx_parse_batch_host, a per-process host
+# context): there is no CPU path. Batches of frames belong on parse_frames_batch / engine.
+CheckSumEnable = True  # protocol.CheckSumEnable (protocol/utils.go:8) for the wrappers below
+DEVICE = 0             # the device the wrappers' host context uses
+
+
+class ReferencePanic(RuntimeError):
+    """The Go function panics on this input: ParseIpv4Pkt with totalLen < 20 or > len(pkt) slices
+    pkt[20:totalLen] out of bounds (protocol/ipv4.go:84). Batches report these as the build-defined
+    statuses IP_TOTLEN_UNDERFLOW / IP_TOTLEN_OVERRUN."""
+
+
+_ctx = {}
+
+
+def _parse_one(buf: bytes, l3: bool) -> np.void:
+    """One Ethernet frame (or, l3, one bare IPv4 packet) parsed on the GPU: its halo_rx_result_t.
+    Lengths past 65535 are passed as 65535 (any length over the reference's caps gets the same
+    ETH_LEN / IP_LEN verdict)."""
+    import ctypes
+
+    if DEVICE not in _ctx:
+        h = ctypes.c_void_p()
+        _lib.check("halo_rx_host_ctx_create", _lib.lib.halo_rx_host_ctx_create(DEVICE, 64, 1 << 16, ctypes.byref(h)))
+        _ctx[DEVICE] = h
+    n = min(len(buf), 0xFFFF)
+    data = np.zeros(max(4, n), np.uint8)
+    data[:n] = np.frombuffer(bytes(buf[:n]), np.uint8)
+    offs = np.zeros(1, np.uint64)
+    lens = np.array([n], np.uint16)
+    out = np.zeros(1, RESULT_DTYPE)
+    rc = _lib.lib.halo_rx_parse_batch_host(_ctx[DEVICE], _lib.ptr(data), _lib.ptr(offs), _lib.ptr(lens), 1,
+                                           flags_word(CheckSumEnable, l3_start=l3), NetIf.make(), _lib.ptr(out), None)
+    _lib.check("halo_rx_parse_batch_host", rc)
+    return out[0]
+
+
+def _ip_wrap(seg: bytes, proto: int, src: bytes, dst: bytes) -> bytes:
+    """seg behind a minimal valid IPv4 header (0x45, DF, the given protocol and addresses, header
+    checksum filled), so the L3 parse hands exactly `seg` to the L4 parser: pkt[20:totalLen] = seg,
+    and the pseudo header carries src / dst. Only its verdicts for seg are read back."""
+    tl = 20 + len(seg)
+    h = bytearray(20)
+    h[0], h[6], h[8], h[9] = 0x45, 0x40, 64, proto
+    h[2:4] = (tl & 0xFFFF).to_bytes(2, "big")
+    h[12:16], h[16:20] = src, dst
+    s = sum(int.from_bytes(h[k:k + 2], "big") for k in range(0, 20, 2))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    h[10:12] = (~s & 0xFFFF).to_bytes(2, "big")
+    return bytes(h) + bytes(seg)
+
+
+def _addr4(a) -> bytes:
+    a = bytes(a)
+    if len(a) != 4:
+        raise ValueError("srcAddr / dstAddr must be 4-byte IPv4 addresses")
+    return a
+
+
+def ParseEthFrm(frm):
+    """protocol.ParseEthFrm (protocol/ethernet.go:29-55): (payload, dstMac, srcMac, ethProto, err)."""
+    r = _parse_one(frm, False)
+    if STATUS_NAMES[r["status"]] in ("ETH_LEN", "ETH_TYPE"):
+        return None, None, None, ETH_PROTO_UNKNOWN, error_text(int(r["status"]))
+    frm = bytes(frm)
+    return frm[14:], frm[0:6], frm[6:12], int(r["ethertype"]), None
+
+
+def ParseIpv4Pkt(pkt):
+    """protocol.ParseIpv4Pkt (protocol/ipv4.go:48-86): (payload, ipHeadProto, srcAddr, dstAddr, err).
+    Raises ReferencePanic where the Go slice expression panics."""
+    r = _parse_one(pkt, True)
+    name = STATUS_NAMES[r["status"]]
+    if name in ("IP_TOTLEN_UNDERFLOW", "IP_TOTLEN_OVERRUN"):
+        raise ReferencePanic(f"ParseIpv4Pkt: totalLen {int(r['ip_total_len'])} outside [20, {len(pkt)}]")
+    if name in ("IP_LEN", "IP_VER", "IP_FRAG", "IP_PROTO", "IP_HDR_CKSUM"):
+        return None, IPH_PROTO_UNKNOWN, None, None, error_text(int(r["status"]))
+    pkt = bytes(pkt)
+    return pkt[20:int(r["ip_total_len"])], int(r["ip_proto"]), pkt[12:16], pkt[16:20], None
+
+
+def _l4(seg, proto: int, src, dst):
+    """The record of seg's L4 parse, and the error text for it (None when it passed)."""
+    r = _parse_one(_ip_wrap(bytes(seg), proto, _addr4(src), _addr4(dst)), True)
+    name = STATUS_NAMES[r["status"]]
+    if name in ("IP_LEN", "L4_LEN"):  # IP_LEN: 20 + len(seg) > 1500, i.e. len(seg) > 1480
+        return r, L4_LEN_TEXT[proto]
+    return r, (None if name == "OK" else error_text(int(r["status"]), proto))
+
+
+def ParseUdpPkt(pkt, srcAddr, dstAddr):
+    """protocol.ParseUdpPkt (protocol/udp.go:21-49): (payload, srcPort, dstPort, err)."""
+    r, err = _l4(pkt, IPH_PROTO_UDP, srcAddr, dstAddr)
+    if err:
+        return None, 0, 0, err
+    return bytes(pkt)[8:], int(r["sport"]), int(r["dport"]), None
+
+
+def ParseTcpPkt(pkt, srcAddr, dstAddr):
+    """protocol.ParseTcpPkt (protocol/tcp.go:36-70): (payload, srcPort, dstPort, seqNum, ackNum, flags,
+    err); the payload starts at the data-offset nibble used as BYTES, as tcp.go:49,68 does."""
+    r, err = _l4(pkt, IPH_PROTO_TCP, srcAddr, dstAddr)
+    if err:
+        return None, 0, 0, 0, 0, 0, err
+    off = int(r["payload_off"]) - 20  # record offsets are in the wrapped packet's coordinates
+    return (bytes(pkt)[off:], int(r["sport"]), int(r["dport"]), int(r["l4_seq"]), int(r["l4_ack"]),
+            int(r["l4_aux"]), None)
+
+
+def ParseIcmpPkt(pkt):
+    """protocol.ParseIcmpPkt (protocol/icmp.go:33-63): (payload, icmpType, icmpId, icmpSeq, err).
+    The checksum is always verified, as the reference does."""
+    r, err = _l4(pkt, IPH_PROTO_ICMP, b"\0\0\0\0", b"\0\0\0\0")
+    if err:
+        return None, ICMP_UNKNOWN, None, 0, err
+    seq = int(r["l4_seq"])
+    return bytes(pkt)[8:], int(r["l4_aux"]), (seq >> 16).to_bytes(2, "big"), seq & 0xFFFF, None
+
+
+__all__ = [name for name in dir() if not name.startswith("_")] + ["STATUS"]

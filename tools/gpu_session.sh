@@ -39,6 +39,9 @@ for s in "$@"; do
     kwrite) step kwrite 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/kwrite" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
     ksq)   step ksq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ksq" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
     tuneq) step tuneq 600 python tools/tune.py --quick ;;
+    tstream) step pytest_stream 600 python -u -m pytest tests/test_gpu_stream.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    gpus2) step gpus2 600 python bench.py --gpus 2 --steps 50 --warmup 5 --no-secondary --no-cpu ;;
+    tunes) step tune_stream 600 python tools/tune.py --spec imix:-2,570B:-2,128B:-2,1500B:8 ;;
     *) echo "unknown step $s" ;;
   esac
 done
