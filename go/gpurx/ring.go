@@ -1,0 +1,53 @@
+package gpurx
+
+// #include "gpurx_shim.h"
+import "C"
+
+import (
+	"errors"
+	"unsafe"
+)
+
+// RingRx is a GPU consumer of one of halo's SPSC packet rings (mem.RingBuffer = ring_buffer_t,
+// mem/ring_buffer.go:18-26, cgo/ring_buffer.h:20-55): the C lcore keeps producing exactly as
+// before (cgo/dpdk.c:280-307); one Poll replaces every ReadPacket + RxEthernet between the
+// consumer's tail and the producer's head, and the frames stay in the ring until Commit.
+type RingRx struct{ r *C.halo_rx_ring_t }
+
+// AttachRing replaces mem.NewRingBufferConsumer(rb, offset) (mem/ring_buffer.go:226-246).
+// capacity is ReadPacket's len(data): 1514 for the DPDK driver (dpdk/dpdk.go:139) and
+// engine.Wire. The ring is registered for DMA (it must start on a page boundary; DPDK's hugepage
+// rings do).
+func AttachRing(device int, rb unsafe.Pointer, offset int64, capacity uint32) (*RingRx, error) {
+	var r *C.halo_rx_ring_t
+	if err := halo(C.halo_rx_ring_attach(C.int(device), rb, C.int64_t(offset), C.uint32_t(capacity), 0, 0,
+		C.HALO_RING_REGISTER, &r)); err != nil {
+		return nil, err
+	}
+	return &RingRx{r}, nil
+}
+
+// Poll parses every frame repeated ReadPacket calls would return now; pos[i] is frame i's record
+// position in the ring stream (its bytes start 4 bytes later, modulo the ring size). out and pos
+// must hold the attach's max_frames entries (default: ring size / 8).
+func (x *RingRx) Poll(netif *NetIfCfg, out []Result, pos []uint64) (int, error) {
+	if len(out) == 0 || len(pos) < len(out) {
+		return 0, errors.New("gpurx: empty result or position slice")
+	}
+	nif, err := netif.c()
+	if err != nil {
+		return 0, err
+	}
+	var info C.halo_rx_ring_scan_t
+	if err := halo(C.halo_rx_ring_poll(x.r, csumFlag(), &nif, (*C.halo_rx_result_t)(unsafe.Pointer(&out[0])), nil,
+		(*C.uint64_t)(unsafe.Pointer(&pos[0])), &info)); err != nil {
+		return 0, err
+	}
+	return int(info.n_frames), nil
+}
+
+// Commit hands the polled records back to the producer (ReadPacket's tail store).
+func (x *RingRx) Commit() error { return halo(C.halo_rx_ring_commit(x.r)) }
+
+// Detach synchronises and frees the consumer (the ring memory must outlive it).
+func (x *RingRx) Detach() error { return halo(C.halo_rx_ring_detach(x.r)) }

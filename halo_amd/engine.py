@@ -8,10 +8,13 @@ and verifies the whole batch on the GPU through ``halo_rx_parse_batch_host`` (pi
 staging, double-buffered H2D -> kernel -> D2H), maps every record to the reference
 engine's decision with ``halo_rx_dispatch`` and invokes the registered UDP / TCP service
 handlers in frame order, with the same session and payload arguments as
-engine/udp_engine.go:16-20 and engine/tcp_engine.go:79-88. After each batch it drains the
-NetIf's ``LoChan`` (bare IPv4 packets: TxIpv4's loopback copies, Ipv4RouteForward's copies for
-another NetIf's address) the way PacketHandle does every 99 polls (engine/engine.go:353-381):
-one HALO_RX_L3_START batch parse, ``halo_rx_dispatch_loopback``, then the same handlers.
+engine/udp_engine.go:16-20 and engine/tcp_engine.go:79-88. It drains the NetIf's ``LoChan``
+(bare IPv4 packets: TxIpv4's loopback copies, Ipv4RouteForward's copies for another NetIf's
+address) the way PacketHandle does (engine/engine.go:353-381): a HALO_RX_L3_START batch parse,
+``halo_rx_dispatch_loopback``, then the same handlers, until the channel is empty — after every
+batch by default, or, with ``drain_every=99``, at PacketHandle's own cadence of one drain per 99
+polls (a batch then ends at that poll), which reproduces the reference's order of handler calls
+and drains exactly.
 """
 from __future__ import annotations
 
@@ -114,6 +117,7 @@ class NetIf:
         self.abi = NetIfAbi.make(self.MacAddr, self.IpAddr, self.NatEnable)
         self._batcher: Optional[HostBatcher] = None
         self.action_counts = np.zeros(len(ACTION_NAMES), dtype=np.int64)
+        self._polls = 0  # EthRxFunc polls since the last LoChan drain: PacketHandle's n
 
     def RecvUdp(self, port: int, handle: Callable):  # engine/udp_engine.go:56-58
         self.UdpServiceMap[port] = handle
@@ -121,54 +125,70 @@ class NetIf:
     def RecvTcp(self, port: int, handle: Callable):  # engine/tcp_engine.go:112-114
         self.TcpServiceMap[port] = handle
 
-    def packet_handle_batch(self, batch: int = 4096):
-        """One batched iteration of PacketHandle: drain, parse on GPU, dispatch.
+    def packet_handle_batch(self, batch: int = 4096, drain_every: int = 0):
+        """One batched iteration of PacketHandle: poll, parse on the GPU, dispatch, deliver; then
+        drain LoChan when it is due.
 
-        Returns (results, actions) for the frames drained this iteration.
-        """
+        drain_every = 0: a batch ends at ``batch`` frames or at the first poll that returns None,
+        and LoChan is drained after every batch. drain_every = 99: PacketHandle's cadence
+        (engine/engine.go:353, ``n == 100-1``) — polls are counted across calls (None polls
+        included), a batch also ends at the poll that makes the count 99, and the drain runs
+        there, so handlers and drains run in the reference's order.
+        Returns (results, actions) for the frames polled this iteration."""
         frames = []
-        for _ in range(batch):
+        while len(frames) < batch:
             f = self.EthRxFunc()
-            if f is None:
+            self._polls += 1
+            if f is not None:
+                frames.append(bytes(f))
+            if drain_every and self._polls >= drain_every:
                 break
-            frames.append(bytes(f))
-        if not frames:  # EthRxFunc returned nil every time: PacketHandle still drains LoChan
+            if f is None and not drain_every:
+                break
+        res, actions = np.empty(0, RESULT_DTYPE), np.empty(0, np.uint8)
+        if frames:
+            lens = np.fromiter((len(f) for f in frames), dtype=np.uint16, count=len(frames))
+            offsets = np.zeros(len(frames), dtype=np.uint64)
+            np.cumsum(lens[:-1], out=offsets[1:])
+            data = np.frombuffer(b"".join(frames), dtype=np.uint8)
+            if self._batcher is None:
+                self._batcher = HostBatcher(self.device)
+            res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable))
+            actions = dispatch(res, self.abi)
+            self._deliver(frames, res, actions)
+        if not drain_every or self._polls >= drain_every:
             self.lo_drain()
-            return np.empty(0, RESULT_DTYPE), np.empty(0, np.uint8)
-        lens = np.fromiter((len(f) for f in frames), dtype=np.uint16, count=len(frames))
-        offsets = np.zeros(len(frames), dtype=np.uint64)
-        np.cumsum(lens[:-1], out=offsets[1:])
-        data = np.frombuffer(b"".join(frames), dtype=np.uint8)
-        if self._batcher is None:
-            self._batcher = HostBatcher(self.device)
-        res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable))
-        actions = dispatch(res, self.abi)
-        self._deliver(frames, res, actions)
-        self.lo_drain()
+            self._polls = 0
         return res, actions
 
-    def lo_drain(self):
-        """PacketHandle's loopback drain (engine/engine.go:353-381) over everything queued in
-        LoChan: ParseIpv4Pkt, own-address filter, local RxIcmp / RxUdp / RxTcp — one GPU batch.
-        Returns (results, actions) for the packets drained."""
-        pkts = []
+    def lo_drain(self, max_batch: int = 4096):
+        """PacketHandle's loopback drain (engine/engine.go:353-381): until LoChan is empty, parse
+        what is queued (ParseIpv4Pkt, own-address filter, local RxIcmp / RxUdp / RxTcp) as one GPU
+        batch of at most ``max_batch`` packets and deliver it in order; packets the handlers queue
+        meanwhile are drained by the same call, as the reference's select loop drains them.
+        Returns (results, actions) for every packet drained."""
+        all_res, all_act = [], []
         while self.LoChan:
-            pkts.append(bytes(self.LoChan.popleft()))
-        if not pkts:
+            pkts = []
+            while self.LoChan and len(pkts) < max_batch:
+                pkts.append(bytes(self.LoChan.popleft()))
+            lens = np.fromiter((len(p) for p in pkts), dtype=np.uint16, count=len(pkts))
+            sizes = (lens.astype(np.uint64) + 3) & ~np.uint64(3)  # 4-byte aligned starts, like ring records
+            offsets = np.zeros(len(pkts), dtype=np.uint64)
+            np.cumsum(sizes[:-1], out=offsets[1:])
+            data = np.zeros(int(sizes.sum()) + 4, dtype=np.uint8)
+            for o, p in zip(offsets, pkts):
+                data[int(o):int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
+            if self._batcher is None:
+                self._batcher = HostBatcher(self.device)
+            res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable, l3_start=True))
+            actions = dispatch_loopback(res, self.abi)
+            self._deliver(pkts, res, actions)
+            all_res.append(res)
+            all_act.append(actions)
+        if not all_res:
             return np.empty(0, RESULT_DTYPE), np.empty(0, np.uint8)
-        lens = np.fromiter((len(p) for p in pkts), dtype=np.uint16, count=len(pkts))
-        sizes = (lens.astype(np.uint64) + 3) & ~np.uint64(3)  # 4-byte aligned starts, like ring records
-        offsets = np.zeros(len(pkts), dtype=np.uint64)
-        np.cumsum(sizes[:-1], out=offsets[1:])
-        data = np.zeros(int(sizes.sum()) + 4, dtype=np.uint8)
-        for o, p in zip(offsets, pkts):
-            data[int(o):int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
-        if self._batcher is None:
-            self._batcher = HostBatcher(self.device)
-        res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable, l3_start=True))
-        actions = dispatch_loopback(res, self.abi)
-        self._deliver(pkts, res, actions)
-        return res, actions
+        return np.concatenate(all_res), np.concatenate(all_act)
 
     def _deliver(self, bufs, res, actions):
         """Invoke the UDP / TCP service handlers for the LOCAL_UDP / LOCAL_TCP records, in order."""
