@@ -12,11 +12,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "halo_amd", "csrc")
 OUT = os.path.join(ROOT, "halo_amd", "lib", "libhalo_rx.so")
 SOURCES = ["rx_parse.hip", "tx_fixup.hip", "tx_build.hip", "deep_nat.hip", "flow_hash.hip", "route_lpm.hip", "synth.hip", "host_path.hip",
-           "ring_rx.hip"]
+           "ring_rx.hip", "host_logic.cc"]
 # measurement tooling (bench.py's native step loop), linked against the product library
 BENCH_SRC = os.path.join(ROOT, "tools", "bench_loop.hip")
 BENCH_OUT = os.path.join(ROOT, "tools", "libhalo_bench.so")
-HEADERS = ["halo_common.h", "device_util.h", os.path.join("..", "..", "include", "halo_rx.h")]
+HEADERS = ["halo_common.h", "halo_limits.h", "host_logic.h", "device_util.h", os.path.join("..", "..", "include", "halo_rx.h")]
 
 
 def _hipcc() -> str:

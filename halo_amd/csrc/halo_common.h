@@ -4,21 +4,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "halo_limits.h"
 #include "halo_rx.h"
+#include "host_logic.h"
 
 namespace halo {
-
-// Reference limits (protocol/ethernet.go:31, protocol/ipv4.go:49, protocol/udp.go:22,
-// protocol/tcp.go:37, protocol/icmp.go:34) and the build-defined jumbo extension.
-constexpr uint32_t kEthMin = 42, kEthMax = 1514, kIpMax = 1500, kL4Max = 1480;
-constexpr uint32_t kEthMaxJumbo = 9014, kIpMaxJumbo = 9000, kL4MaxJumbo = 8980;
-
-// EtherTypes (protocol/ethernet.go:16-22), IP protocol ids (protocol/ipv4.go:27-32),
-// ICMP types (protocol/icmp.go:25-30).
-constexpr uint16_t kEthIeee8023 = 0x05DC, kEthIpv4 = 0x0800, kEthArp = 0x0806,
-                   kEthIpv6 = 0x86DD, kEthUnknown = 0xFFFF;
-constexpr uint8_t kIpIcmp = 0x01, kIpTcp = 0x06, kIpUdp = 0x11, kIpUnknown = 0xFF;
-constexpr uint8_t kIcmpRequest = 0x08, kIcmpReply = 0x00, kIcmpTtl = 0x0B;
 
 // Kernel parameter block (passed by value; one per launch).
 struct RxParams {
@@ -66,12 +56,10 @@ enum SynthSlot : uint32_t {
 
 int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 
-// Live host registrations (hipHostRegister) made through this library — halo_rx_host_register
-// and halo_rx_ring_attach(HALO_RING_REGISTER). A registration pins whole pages, so every one
-// must start on a page boundary and cover whole pages, and no two may share a page; both rules
-// are checked here, before any HIP call. Removal waits for every device this library has
+// Live host registrations made through this library (halo_rx_host_register and
+// halo_rx_ring_attach(HALO_RING_REGISTER)), over RegMap (host_logic.h): page-aligned whole pages,
+// no shared page, checked before any HIP call. Removal waits for every device this library has
 // launched on, unregisters, and checks that the runtime no longer maps the range.
-enum HostRegKind : int { kRegUser = 1, kRegRing = 2 };
 uint64_t host_page_size();
 int host_reg_add(void* base, uint64_t bytes, HostRegKind kind);  // bytes: a page multiple
 int host_reg_remove(void* base, HostRegKind kind);

@@ -7,7 +7,7 @@
 #include <unistd.h>
 
 #include <atomic>
-#include <map>
+#include <algorithm>
 #include <mutex>
 #include <new>
 #include <utility>
@@ -41,16 +41,8 @@ int check_device() {
     return v == 1 ? HALO_OK : v;
 }
 
-// ---- the registry of live host registrations --------------------------------------------
+// ---- host registrations (the interval bookkeeping is RegMap, host_logic.cc) ------------------
 namespace {
-struct Reg {
-    uint64_t bytes;
-    HostRegKind kind;
-    uint8_t* dev;  // the range as the device addresses it (hipHostGetDevicePointer)
-};
-std::mutex g_reg_mu;
-std::map<uintptr_t, Reg> g_regs;  // base -> range (page-aligned, whole pages)
-
 // Waits for all work this library queued on any device: a DMA or kernel still reading or
 // writing the range must finish before its pages are unpinned.
 int sync_used_devices() {
@@ -83,25 +75,21 @@ uint64_t host_page_size() {
     return page;
 }
 
+// The range is reserved first (refused if it shares a page with any registration), registered
+// with the runtime with no lock held, then published.
 int host_reg_add(void* base, uint64_t bytes, HostRegKind kind) {
-    const uint64_t page = host_page_size();
     const uintptr_t b = reinterpret_cast<uintptr_t>(base);
-    if (!base || !bytes || (b % page) || (bytes % page) || b + bytes < b) return HALO_E_INVAL;
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    // the first live registration starting at or after b, and the one before it
-    auto it = g_regs.lower_bound(b);
-    if (it != g_regs.end() && it->first < b + bytes) return HALO_E_INVAL;
-    if (it != g_regs.begin()) {
-        auto pv = std::prev(it);
-        if (pv->first + pv->second.bytes > b) return HALO_E_INVAL;
-    }
+    int rc = registry().reserve(b, bytes, host_page_size(), kind);
+    if (rc) return rc;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
         (void)hipGetLastError();
+        registry().cancel(b);
         return HALO_E_NODEV;
     }
     if (hipHostRegister(base, bytes, hipHostRegisterDefault) != hipSuccess) {
         (void)hipGetLastError();
+        registry().cancel(b);
         return HALO_E_HIP;
     }
     void* dev = nullptr;
@@ -109,51 +97,34 @@ int host_reg_add(void* base, uint64_t bytes, HostRegKind kind) {
         (void)hipGetLastError();
         dev = nullptr;  // no device view: the range is still usable as a DMA source
     }
-    g_regs.emplace(b, Reg{bytes, kind, static_cast<uint8_t*>(dev)});
+    registry().commit(b, static_cast<uint8_t*>(dev));
     return HALO_OK;
 }
 
 bool host_reg_find(const void* p, uintptr_t* base, uint64_t* bytes, uint8_t** dev) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_regs.upper_bound(a);
-    if (it == g_regs.begin()) return false;
-    --it;
-    if (a >= it->first + it->second.bytes) return false;
-    *base = it->first;
-    *bytes = it->second.bytes;
-    *dev = it->second.dev;
-    return true;
+    return registry().find(reinterpret_cast<uintptr_t>(p), base, bytes, dev);
 }
 
 void* host_reg_device_view(const void* p, uint64_t bytes) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    if (!p || a + bytes < a) return nullptr;
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_regs.upper_bound(a);  // the first registration starting after a
-    if (it == g_regs.begin()) return nullptr;
-    --it;
-    if (!it->second.dev || a + bytes > it->first + it->second.bytes) return nullptr;
-    return it->second.dev + (a - it->first);
+    return registry().view(reinterpret_cast<uintptr_t>(p), bytes);
 }
 
+// The entry is marked as being removed (lookups stop seeing it) and the device synchronisation and
+// hipHostUnregister run with no lock held, so other threads' lookups do not wait on device work.
 int host_reg_remove(void* base, HostRegKind kind) {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_regs.find(reinterpret_cast<uintptr_t>(base));
-    if (it == g_regs.end() || it->second.kind != kind) return HALO_E_INVAL;  // not a live base of this kind
-    if (sync_used_devices() != HALO_OK) return HALO_E_HIP;  // the entry stays: the pages stay pinned
-    if (hipHostUnregister(base) != hipSuccess) {
+    const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+    if (!registry().begin_remove(b, kind)) return HALO_E_INVAL;  // not a live base of this kind
+    int rc = sync_used_devices();                                 // the pages stay pinned on failure
+    if (rc == HALO_OK && hipHostUnregister(base) != hipSuccess) {
         (void)hipGetLastError();
-        return HALO_E_HIP;
+        rc = HALO_E_HIP;
     }
-    if (runtime_maps(base)) return HALO_E_HIP;  // still mapped: keep it counted, the caller keeps the memory
-    g_regs.erase(it);
-    return HALO_OK;
+    if (rc == HALO_OK && runtime_maps(base)) rc = HALO_E_HIP;  // still mapped: the caller keeps the memory
+    registry().end_remove(b, rc == HALO_OK);
+    return rc;
 }
 
 }  // namespace halo
-
-extern "C" HALO_API const char* halo_rx_version(void) { return "halo_rx 0.1 (gfx950)"; }
 
 extern "C" HALO_API int halo_rx_init(int device) {
     int count = 0;
@@ -161,112 +132,6 @@ extern "C" HALO_API int halo_rx_init(int device) {
     if (device < 0 || device >= count) return HALO_E_NODEV;
     if (hipSetDevice(device) != hipSuccess) return HALO_E_NODEV;
     return halo::check_device();
-}
-
-extern "C" HALO_API const char* halo_rx_strerror(int code) {
-    switch (code) {
-        case HALO_OK: return "ok";
-        case HALO_E_INVAL: return "invalid argument";
-        case HALO_E_NODEV: return "no HIP device";
-        case HALO_E_ARCH: return "device is not gfx950";
-        case HALO_E_HIP: return "HIP runtime error";
-        case HALO_E_NOMEM: return "out of memory";
-        case HALO_E_RANGE: return "batch exceeds addressing range";
-        default: return "unknown error";
-    }
-}
-
-extern "C" HALO_API const char* halo_rx_status_name(int status) {
-    static const char* const names[HALO_RX_STATUS_COUNT] = {
-        "OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_PROTO", "IP_HDR_CKSUM",
-        "IP_TOTLEN_UNDERFLOW", "IP_TOTLEN_OVERRUN", "L4_LEN", "ICMP_TYPE", "ICMP_CODE", "L4_CKSUM"};
-    return (status >= 0 && status < HALO_RX_STATUS_COUNT) ? names[status] : "UNKNOWN";
-}
-
-// ---- engine decision (engine/ethernet_engine.go:13-31, engine/ipv4_engine.go:18-47) -----
-namespace {
-uint16_t ethertype_of(const halo_rx_result_t& r) { return r.ethertype; }
-uint16_t ethertype_of(const halo_rx_record16_t& r) {
-    if (r.status == HALO_RX_ETH_LEN || r.status == HALO_RX_ETH_TYPE) return halo::kEthUnknown;
-    switch (r.flags & 0x30u) {
-        case HALO_RX_F_ET_ARP: return halo::kEthArp;
-        case HALO_RX_F_ET_IPV6: return halo::kEthIpv6;
-        case HALO_RX_F_ET_8023: return halo::kEthIeee8023;
-        default: return halo::kEthIpv4;
-    }
-}
-
-template <typename Rec>
-int dispatch(const Rec* results, uint32_t n, const halo_rx_netif_t* netif, uint8_t* actions, uint32_t* action_hist) {
-    if (n && (!results || !netif || !actions)) return HALO_E_INVAL;
-    for (uint32_t i = 0; i < n; ++i) {
-        const Rec& r = results[i];
-        const uint16_t ethertype = ethertype_of(r);
-        uint8_t a;
-        if (r.status == HALO_RX_ETH_LEN || r.status == HALO_RX_ETH_TYPE) {
-            a = HALO_RX_ACT_DROP_ETH;                        // ethernet_engine.go:18-21
-        } else if (!(r.flags & HALO_RX_F_MAC_MATCH)) {
-            a = HALO_RX_ACT_IGNORE_MAC;                      // ethernet_engine.go:22
-        } else if (ethertype == halo::kEthArp) {
-            a = HALO_RX_ACT_ARP;                             // ethernet_engine.go:24-25
-        } else if (ethertype != halo::kEthIpv4) {
-            a = HALO_RX_ACT_IGNORE_TYPE;                     // ethernet_engine.go:28
-        } else if (r.status >= HALO_RX_IP_LEN && r.status <= HALO_RX_IP_TOTLEN_OVERRUN) {
-            a = HALO_RX_ACT_DROP_IP;                         // ipv4_engine.go:19-23
-        } else if (r.flags & HALO_RX_F_IP_BCAST) {           // ipv4_engine.go:24-30
-            if (r.ip_proto == halo::kIpUdp)
-                a = r.status == HALO_RX_OK ? HALO_RX_ACT_BCAST_UDP : HALO_RX_ACT_DROP_BCAST_UDP;
-            else
-                a = HALO_RX_ACT_IGNORE_BCAST;
-        } else if (!(r.flags & HALO_RX_F_DST_IS_OWN) || netif->nat_enable) {
-            a = HALO_RX_ACT_FORWARD;                         // ipv4_engine.go:31-37
-        } else if (r.status != HALO_RX_OK) {
-            a = HALO_RX_ACT_DROP_L4;                         // {udp,tcp,icmp}_engine.go Rx*
-        } else {
-            a = r.ip_proto == halo::kIpIcmp ? HALO_RX_ACT_LOCAL_ICMP
-              : r.ip_proto == halo::kIpUdp  ? HALO_RX_ACT_LOCAL_UDP
-                                            : HALO_RX_ACT_LOCAL_TCP;  // ipv4_engine.go:38-46
-        }
-        actions[i] = a;
-        if (action_hist) ++action_hist[a];
-    }
-    return HALO_OK;
-}
-}  // namespace
-
-extern "C" HALO_API int halo_rx_dispatch(const halo_rx_result_t* results, uint32_t n, const halo_rx_netif_t* netif,
-                                         uint8_t* actions, uint32_t* action_hist) {
-    return dispatch(results, n, netif, actions, action_hist);
-}
-
-extern "C" HALO_API int halo_rx_dispatch_loopback(const halo_rx_result_t* results, uint32_t n,
-                                                  const halo_rx_netif_t* netif, uint8_t* actions,
-                                                  uint32_t* action_hist) {
-    if (n && (!results || !netif || !actions)) return HALO_E_INVAL;
-    for (uint32_t i = 0; i < n; ++i) {
-        const halo_rx_result_t& r = results[i];
-        uint8_t a;
-        if (r.status >= HALO_RX_ETH_LEN && r.status <= HALO_RX_IP_TOTLEN_OVERRUN) {
-            a = HALO_RX_ACT_DROP_IP;                         // engine.go:362-365 (no Ethernet layer)
-        } else if (!(r.flags & HALO_RX_F_DST_IS_OWN)) {
-            a = HALO_RX_ACT_LO_NOT_OWN;                      // engine.go:366-368
-        } else if (r.status != HALO_RX_OK) {
-            a = HALO_RX_ACT_DROP_L4;                         // Rx{Icmp,Udp,Tcp} log and drop
-        } else {
-            a = r.ip_proto == halo::kIpIcmp ? HALO_RX_ACT_LOCAL_ICMP
-              : r.ip_proto == halo::kIpUdp  ? HALO_RX_ACT_LOCAL_UDP
-                                            : HALO_RX_ACT_LOCAL_TCP;  // engine.go:369-376
-        }
-        actions[i] = a;
-        if (action_hist) ++action_hist[a];
-    }
-    return HALO_OK;
-}
-
-extern "C" HALO_API int halo_rx_dispatch_compact(const halo_rx_record16_t* records, uint32_t n,
-                                                 const halo_rx_netif_t* netif, uint8_t* actions,
-                                                 uint32_t* action_hist) {
-    return dispatch(records, n, netif, actions, action_hist);
 }
 
 // ---- host-memory batch path ---------------------------------------------------------------
@@ -360,7 +225,7 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
     // zero-copy chunks with GPU-converted metadata stage nothing on the host, so they can be
     // larger: fewer chunk boundaries (1M x 64 B: 1.87 ms in 256k-frame chunks, 1.60 ms in one;
     // profiles/r02/r2o/host_zc_sweep.log); the device metadata and record buffers are sized for them
-    c->zc_frames = chunk_frames <= (1u << 30) ? chunk_frames * 4u : chunk_frames;
+    c->zc_frames = (uint32_t)std::min<uint64_t>(4ull * chunk_frames, 0xFFFFFFFFull);
     c->chunk_bytes = chunk_bytes;
     bool ok = true;
     for (auto& s : c->slot) {
@@ -476,15 +341,10 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
             }
             // (b) metadata converted by the host, into the slot's pinned staging
             if (cnt > ctx->chunk_frames) cnt = ctx->chunk_frames;
-            uint64_t lo = ~0ull, hi = 0, mis = 0;
-            for (uint32_t j = 0; j < cnt; ++j) {  // span and relative alignment (vectorisable)
-                const uint64_t e = o[j] + l[j];
-                lo = o[j] < lo ? o[j] : lo;
-                hi = e > hi ? e : hi;
-                mis |= o[j] - o[0];
-            }
+            uint64_t lo = 0, hi = 0;
+            const bool rel_aligned = halo::span_aligned(o, l, cnt, &lo, &hi);
             const uint64_t span = hi > lo ? hi - lo : 1;
-            const uint8_t* view = (mis & 3u) || span > (16ull << 30)
+            const uint8_t* view = !rel_aligned || span > (16ull << 30)
                                       ? nullptr
                                       : static_cast<const uint8_t*>(halo::host_reg_device_view(bytes + lo, span));
             if (view && !(reinterpret_cast<uintptr_t>(view) & 3u)) {
@@ -518,41 +378,17 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
         // Direct mode: frames in order, 4-byte aligned relative to the first, spanning at most
         // chunk_bytes (a drained ring segment, or a packed batch): one DMA of the caller's span
         // (pinned if registered with halo_rx_host_register), no CPU copy of frame bytes.
-        uint64_t used = 0;
-        uint32_t cnt = 0;
+        uint64_t used = 0, lo = 0, hi = 0;
         const uint8_t* src = s.h_bytes;
-        {
-            const uint64_t lo = offsets[next];
-            uint64_t hi = lo;
-            while (next + cnt < n && cnt < ctx->chunk_frames) {
-                const uint64_t o = offsets[next + cnt];
-                const uint64_t e = o + lens[next + cnt];
-                if (o < lo || ((o - lo) & 3u) || (e > hi ? e : hi) - lo > ctx->chunk_bytes) break;
-                s.h_off[cnt] = (uint32_t)((o - lo) >> 2);
-                s.h_len[cnt] = lens[next + cnt];
-                if (e > hi) hi = e;
-                ++cnt;
-            }
-            // take the direct path only when it covers the whole chunk's worth of frames
-            if (cnt > 0 && (next + cnt == n || cnt == ctx->chunk_frames || hi - lo > ctx->chunk_bytes / 2)) {
-                used = hi - lo;
-                src = bytes + lo;
-            } else {
-                cnt = 0;
-            }
-        }
-        // Pack mode: copy frames [next, ...) into the pinned slot, 4-byte aligned (ring-record style)
-        if (cnt == 0) {
-            while (next + cnt < n && cnt < ctx->chunk_frames) {
-                const uint32_t L = lens[next + cnt];
-                const uint64_t need = L <= cap ? ((L + 3u) & ~3u) : 0;  // over-long frames are never read
-                if (used + need > ctx->chunk_bytes) break;
-                if (need) memcpy(s.h_bytes + used, bytes + offsets[next + cnt], L);
-                s.h_off[cnt] = (uint32_t)(used >> 2);
-                s.h_len[cnt] = (uint16_t)L;
-                used += need;
-                ++cnt;
-            }
+        uint32_t cnt = halo::plan_direct(offsets, lens, n, next, ctx->chunk_frames, ctx->chunk_bytes, s.h_off, s.h_len,
+                                         &lo, &hi);
+        if (cnt) {
+            used = hi - lo;
+            src = bytes + lo;
+        } else {
+            // Pack mode: copy frames [next, ...) into the pinned slot, 4-byte aligned (ring-record style)
+            cnt = halo::pack_chunk(bytes, offsets, lens, n, next, ctx->chunk_frames, ctx->chunk_bytes, cap, s.h_bytes,
+                                   s.h_off, s.h_len, &used);
         }
         hipError_t e = hipSuccess;
         if (used) e = hipMemcpyAsync(s.d_bytes, src, used, hipMemcpyHostToDevice, s.stream);
@@ -614,18 +450,9 @@ extern "C" HALO_API int halo_rx_host_unregister(const void* ptr) {
 }
 
 extern "C" HALO_API uint32_t halo_rx_host_registered_count(void) {
-    std::lock_guard<std::mutex> lk(halo::g_reg_mu);
-    return (uint32_t)halo::g_regs.size();
+    return halo::registry().list(nullptr, nullptr, 0);
 }
 
 extern "C" HALO_API uint32_t halo_rx_host_registrations(void** bases, uint64_t* bytes, uint32_t cap) {
-    std::lock_guard<std::mutex> lk(halo::g_reg_mu);
-    uint32_t i = 0;
-    for (const auto& kv : halo::g_regs) {
-        if (i >= cap) break;
-        if (bases) bases[i] = reinterpret_cast<void*>(kv.first);
-        if (bytes) bytes[i] = kv.second.bytes;
-        ++i;
-    }
-    return (uint32_t)halo::g_regs.size();
+    return halo::registry().list(bases, bytes, cap);
 }

@@ -48,7 +48,6 @@ constexpr uint32_t kLdsStop = 0x8000u;           // jump-table target: the walk 
 constexpr uint32_t kMapStop = 0xFFFFFFFFu;       // tile / superblock map entry: the walk stops
 constexpr uint32_t kMapLds = 8192;               // map entries (uint2) staged in LDS: 64 KB
 constexpr uint32_t kMaxCapacity = 4 * kTile - 8; // the longest record must fit a tile's entry window
-constexpr uint32_t kRbHeader = 128;              // sizeof(RingBuffer), mem/ring_buffer.go:18-26
 constexpr uint64_t kMaxSpan = (16ull << 30) - (64ull << 10);  // dword offsets stay below 2^32
 constexpr uint64_t kPieceBytes = 16ull << 20;    // DMA piece (1024 tiles) whose maps start on arrival
 constexpr uint64_t kSmallPoll = 4ull << 20;      // default: polls up to this size take the small path
@@ -482,32 +481,6 @@ int launch_finish(const Scan& s, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 
-bool pow2(uint64_t x) { return x >= 8 && (x & (x - 1)) == 0; }
-
-// ring_buffer_mapping + ring_buffer_consumer_init (cgo/ring_buffer.h:158-204, :228-246).
-int validate_ring(const uint8_t* mem, int64_t offset, uint64_t* size, uint64_t* tail) {
-    if (!mem || (reinterpret_cast<uintptr_t>(mem) & 7u)) return HALO_E_INVAL;
-    if (mem[8] != 1) return HALO_E_INVAL;  // layout version
-    for (int i = 9; i <= 63; ++i)
-        if (mem[i] != 0xAA) return HALO_E_INVAL;
-    for (int i = 96; i <= 127; ++i)
-        if (mem[i] != 0xFF) return HALO_E_INVAL;
-    uint64_t sz, mask, stored;
-    memcpy(&sz, mem + 72, 8);
-    memcpy(&mask, mem + 80, 8);
-    memcpy(&stored, mem + 88, 8);
-    if (!stored || !pow2(sz) || sz > (1ull << 62) || mask != sz - 1) return HALO_E_INVAL;
-    const uint64_t t = __atomic_load_n(reinterpret_cast<const uint64_t*>(mem + 64), __ATOMIC_ACQUIRE);
-    const uint64_t h = __atomic_load_n(reinterpret_cast<const uint64_t*>(mem), __ATOMIC_ACQUIRE);
-    if (h - t > sz) return HALO_E_INVAL;
-    // ring_buffer_local_data: the caller's offset must match this mapping
-    const uint64_t local = reinterpret_cast<uintptr_t>(mem + kRbHeader);
-    if ((int64_t)(local - stored) != offset) return HALO_E_INVAL;
-    *size = sz;
-    *tail = t;
-    return HALO_OK;
-}
-
 }  // namespace
 }  // namespace halo
 
@@ -622,28 +595,12 @@ int alloc_small(halo_rx_ring* r, uint64_t bytes) {
 // of the data area: that poll takes the pipelined path, which linearises the span.
 int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_netif_t* netif,
                halo_rx_result_t* out, uint32_t* status_hist, uint64_t* positions, halo_rx_ring_scan_t* info) {
-    const uint64_t mask = r->size - 1, half = r->size >> 1;
-    uint64_t a = 0;
-    uint32_t n = 0, max_len = 0, stop;
-    for (;;) {
-        if (used - a < 4) { stop = HALO_RING_STOP_EMPTY; break; }
-        const uint64_t p = (r->cursor + a) & mask;
-        uint32_t len;
-        memcpy(&len, r->data + p, 4);
-        if (len == 0 || len > half) { stop = HALO_RING_STOP_BAD_LEN; break; }
-        const uint64_t bytes = (4ull + len + 3ull) & ~3ull;
-        if (used - a < bytes) { stop = HALO_RING_STOP_PARTIAL; break; }
-        if (len > r->cap) { stop = HALO_RING_STOP_CAPACITY; break; }
-        if (n == r->max_frames) { stop = HALO_RING_STOP_MAX; break; }
-        const uint64_t f = (p + 4) & mask;
-        if (f + len > r->size) return 1;
-        r->h_soff[n] = (uint32_t)(f >> 2);
-        r->h_slen[n] = (uint16_t)len;
-        if (positions) positions[n] = r->cursor + a;
-        max_len = std::max(max_len, len);
-        ++n;
-        a += bytes;
-    }
+    // every record is >= 8 bytes and used <= small, so at most small_frames frames fit: the bound
+    // below never cuts a walk, it only keeps the pinned arrays' size in the contract
+    const halo::RingWalk w = halo::ring_walk(r->data, r->size, r->cursor, used, r->cap,
+                                             std::min(r->max_frames, r->small_frames), r->h_soff, r->h_slen, positions);
+    if (w.wraps) return 1;
+    const uint32_t n = w.n, max_len = w.max_len;
     if (n) {
         const uint64_t rb = sizeof(halo_rx_result_t) * (uint64_t)n;
         // looked up per poll (not cached): the caller may unregister or reuse the array between polls
@@ -662,10 +619,10 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
             for (uint32_t i = 0; i < n; ++i) ++status_hist[out[i].status];  // the statuses the kernel wrote
     }
     info->n_frames = n;
-    info->stop = stop;
-    info->end_bytes = a;
+    info->stop = w.stop;
+    info->end_bytes = w.end_bytes;
     info->max_len = max_len;
-    r->cursor += a;
+    r->cursor += w.end_bytes;
     return HALO_OK;
 }
 }  // namespace
@@ -904,76 +861,6 @@ extern "C" HALO_API int halo_rx_ring_commit(halo_rx_ring_t* r) {
     return HALO_OK;
 }
 
-// ---- producer side (engine.NewWire / Wire.Tx) ------------------------------------------------
-extern "C" HALO_API int halo_ring_create(void* memory, uint64_t bytes) {
-    uint8_t* m = static_cast<uint8_t*>(memory);
-    if (!m || (reinterpret_cast<uintptr_t>(m) & 63u) || bytes < halo::kRbHeader + 8) return HALO_E_INVAL;
-    const uint64_t size = bytes - halo::kRbHeader;
-    if (!halo::pow2(size) || size > (1ull << 62)) return HALO_E_INVAL;
-    memset(m, 0, halo::kRbHeader);
-    const uint64_t mask = size - 1;
-    const uintptr_t buffer = reinterpret_cast<uintptr_t>(m + halo::kRbHeader);
-    memcpy(m + 72, &size, 8);
-    memcpy(m + 80, &mask, 8);
-    memcpy(m + 88, &buffer, 8);
-    m[8] = 1;  // layout version
-    memset(m + 9, 0xAA, 55);
-    memset(m + 96, 0xFF, 32);
-    return HALO_OK;
-}
-
-extern "C" HALO_API int halo_ring_write_batch(void* memory, const uint8_t* bytes, const uint64_t* offsets,
-                                              const uint16_t* lens, uint32_t n, uint8_t* accepted,
-                                              uint32_t* written) {
-    uint64_t size = 0, tail_unused = 0;
-    uint8_t* m = static_cast<uint8_t*>(memory);
-    if (!m) return HALO_E_INVAL;
-    uint64_t stored;
-    memcpy(&stored, m + 88, 8);
-    int rc = halo::validate_ring(m, (int64_t)(reinterpret_cast<uintptr_t>(m + halo::kRbHeader) - stored), &size,
-                                 &tail_unused);
-    if (rc) return rc;
-    if (n && (!bytes || !offsets || !lens)) return HALO_E_INVAL;
-    uint64_t* head_p = reinterpret_cast<uint64_t*>(m);
-    const uint64_t* tail_p = reinterpret_cast<const uint64_t*>(m + 64);
-    uint8_t* data = m + halo::kRbHeader;
-    const uint64_t mask = size - 1;
-    uint64_t head = __atomic_load_n(head_p, __ATOMIC_RELAXED);  // this process is the producer
-    uint64_t cached_tail = __atomic_load_n(tail_p, __ATOMIC_ACQUIRE);
-    uint32_t count = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t len = lens[i];
-        bool ok = len != 0 && (uint64_t)len <= size / 2;
-        const uint64_t total = (4ull + len + 3ull) & ~3ull;
-        if (ok) {  // WritePacket's space check, re-reading the tail only when short
-            uint64_t used = head - cached_tail;
-            if (used > size || size - used < total) {
-                cached_tail = __atomic_load_n(tail_p, __ATOMIC_ACQUIRE);
-                used = head - cached_tail;
-                ok = used <= size && size - used >= total;
-            }
-        }
-        if (ok) {
-            const uint64_t pos = head & mask;
-            memcpy(data + pos, &len, 4);
-            const uint64_t dpos = (pos + 4) & mask, after = size - dpos;
-            const uint8_t* src = bytes + offsets[i];
-            if (after >= len) {
-                memcpy(data + dpos, src, len);
-            } else {
-                memcpy(data + dpos, src, after);
-                memcpy(data, src + after, len - after);
-            }
-            head += total;
-            __atomic_store_n(head_p, head, __ATOMIC_RELEASE);
-            ++count;
-        }
-        if (accepted) accepted[i] = ok ? 1 : 0;
-    }
-    if (written) *written = count;
-    return HALO_OK;
-}
-
 // ---- several devices, one host batch ------------------------------------------
 extern "C" HALO_API int halo_rx_shard_multi(halo_rx_host_ctx_t* const* ctxs, uint32_t n_ctx, const uint8_t* bytes,
                                             const uint64_t* offsets, const uint16_t* lens, uint32_t n, uint32_t flags,
@@ -985,16 +872,7 @@ extern "C" HALO_API int halo_rx_shard_multi(halo_rx_host_ctx_t* const* ctxs, uin
     if (n && (!bytes || !offsets || !lens || !out)) return HALO_E_INVAL;
     // contiguous index ranges balanced by frame bytes
     std::vector<uint32_t> first(n_ctx + 1, n);
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; ++i) total += lens[i];
-    first[0] = 0;
-    uint64_t acc = 0;
-    uint32_t k = 1;
-    for (uint32_t i = 0; i < n && k < n_ctx; ++i) {
-        while (k < n_ctx && acc >= total * k / n_ctx) first[k++] = i;
-        acc += lens[i];
-    }
-    while (k < n_ctx) first[k++] = n;
+    halo::shard_bounds(lens, n, n_ctx, first.data());
     if (shard_first)
         for (uint32_t j = 0; j <= n_ctx; ++j) shard_first[j] = first[j];
     std::vector<int> rcs(n_ctx, HALO_OK);
