@@ -31,8 +31,8 @@ HALO_RX_UNIFORM_LEN = 0x8
 HALO_RX_L3_START = 0x10  # LoChan packets: every buffer starts at its IPv4 header
 HALO_RX_VARIANT_SHIFT = 8
 # lanes per frame -> HALO_RX_VARIANT_* (0 = automatic, -1 = the size-class mix kernel,
-# -2 = the byte-stream kernel)
-_VARIANT_CODE = {0: 0, 1: 1, 4: 2, 8: 3, 16: 4, -1: 5, -2: 6}
+# -2 = the byte-stream kernel, -3 = one round trip per frame)
+_VARIANT_CODE = {0: 0, 1: 1, 4: 2, 8: 3, 16: 4, -1: 5, -2: 6, -3: 7}
 
 
 def variant_flags(lanes_per_frame: int) -> int:

@@ -603,8 +603,11 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
     const uint32_t n = w.n, max_len = w.max_len;
     if (n) {
         const uint64_t rb = sizeof(halo_rx_result_t) * (uint64_t)n;
-        // looked up per poll (not cached): the caller may unregister or reuse the array between polls
-        halo_rx_result_t* dout = static_cast<halo_rx_result_t*>(device_view(out, rb));
+        // looked up per poll (not cached): the caller may unregister or reuse the array between polls.
+        // A registration made through the library is found in its registry without a runtime call
+        // (two hipHostGetDevicePointer calls per poll otherwise); other pinned memory by the runtime.
+        auto* dout = static_cast<halo_rx_result_t*>(halo::host_reg_device_view(out, rb));
+        if (!dout) dout = static_cast<halo_rx_result_t*>(device_view(out, rb));
         if (!dout && !r->h_sres) {
             const uint64_t sb = sizeof(halo_rx_result_t) * (uint64_t)r->small_frames;
             if (hipHostMalloc((void**)&r->h_sres, sb, hipHostMallocDefault) != hipSuccess) return HALO_E_NOMEM;

@@ -95,6 +95,24 @@ __device__ __forceinline__ void acc_segment_dot2(const uint32_t (&w)[4], uint32_
     }
 }
 
+// Group form (G > 1): the halves sum (v_dot2_u32_u16, as acc_segment_dot2) of the segment bytes in
+// dwords [d0, d0+4). A chunk wholly inside the segment needs no mask, and whether every lane's chunk
+// is is one wave-uniform test, so the common case costs four v_dot2 per chunk; only a wave whose
+// chunk meets the segment's start or end (FIRST: round 0's header chunk) takes the masked path.
+template <bool L3, bool FIRST = false>
+__device__ __forceinline__ void acc_chunk(const uint32_t (&w)[4], uint32_t d0, uint32_t seg_end, uint32_t& hs) {
+    constexpr uint32_t kSeg = kIpOff<L3> + 20u;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 one = {1, 1};
+    const bool inside = 4u * d0 >= kSeg && 4u * d0 + 16u <= seg_end;
+    if (!FIRST && __builtin_amdgcn_ballot_w64(!inside) == 0) {  // wave-uniform: no masks
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hs = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w[j]), one, hs, false);
+        return;
+    }
+    acc_segment_dot2<L3>(w, d0, (int32_t)(8u * seg_end), hs);
+}
+
 struct Verdict {
     uint32_t status, flags, ethertype, ip_proto, ip_total_len, src_ip, dst_ip, sport, dport;
     uint32_t pay_off, pay_len, l4_aux, l4_seq, l4_ack;
@@ -268,6 +286,16 @@ struct Hist {
 // ~55 VGPRs (occupancy 5 -> 3) and lost more than it gained; kept as a knob.
 template <int G>
 constexpr int kRound0 = 4;
+// Round 0 of the uniform-length group kernels only (A/B knobs): chunks per lane issued before the
+// header parse. 12 for G = 8 covers a whole 1536 B frame in one round trip.
+#ifndef HALO_RX_G8_ROUND0
+#define HALO_RX_G8_ROUND0 4
+#endif
+#ifndef HALO_RX_G4_ROUND0
+#define HALO_RX_G4_ROUND0 4
+#endif
+template <int G>
+constexpr int kGroupRound0 = G == 8 ? HALO_RX_G8_ROUND0 : G == 4 ? HALO_RX_G4_ROUND0 : 4;
 
 // One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
 template <int G, int R0 = kRound0<G>>
@@ -389,10 +417,21 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
     constexpr int U0 = R0;            // chunks already loaded
     uint32_t h[12];
     frame_header(st, grp_base, h);
+    uint64_t c = 0;
+    uint32_t hs = 0;  // group kernels: halves sum of this lane's segment dwords
+    if constexpr (G > 1) {
+        // Round 0 is summed before the header checks run, so its buffers are dead during them (a
+        // group kernel can then issue more of the frame in round 0). The segment end is the one
+        // parse_header computes (IPv4 offset + totalLen) whenever the L4 sum decides the verdict;
+        // for any other frame the sum is never read.
+        const uint32_t tl = L3 ? bswap16(h[0] >> 16) : bswap16(h[4] & 0xFFFFu);
+        acc_chunk<L3, true>(st.buf[0], gl * 4, kIpOff<L3> + tl, hs);
+#pragma unroll
+        for (int u = 1; u < U0; ++u) acc_chunk<L3>(st.buf[u], (u * G + gl) * 4, kIpOff<L3> + tl, hs);
+    }
     Verdict v = parse_header<L3>(h, st.L, present, p);
 
     // L4 segment sum over [kIpOff + 20, seg_end): round 0 from registers, then U chunks per round
-    uint64_t c = 0;
     if (v.seg_end && G == 1 && HALO_RX_LANE_DOT2) {
         uint32_t hs = 0;
         const int32_t e8 = (int32_t)(8u * v.seg_end);
@@ -407,29 +446,41 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
             for (int u = 0; u < U; ++u) acc_segment_dot2<L3>(x[u], r0 + u * 4, e8, hs);
         }
         c = hs;
-    } else if (v.seg_end) {
+    } else if (v.seg_end && G == 1) {
 #pragma unroll
-        for (int u = 0; u < U0; ++u) acc_segment<L3>(st.buf[u], (u * G + gl) * 4, v.seg_end, c);
+        for (int u = 0; u < U0; ++u) acc_segment<L3>(st.buf[u], u * 4, v.seg_end, c);
         const uint32_t seg_dw = (v.seg_end + 3) >> 2;
+        for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
+            uint32_t x[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load4(st.frame, r0 + u * 4, seg_dw, x[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc_segment<L3>(x[u], r0 + u * 4, v.seg_end, c);
+        }
+    } else if constexpr (G > 1) {
+        // later rounds: the group's loop bound is wave-uniform in practice (one length per batch),
+        // and a group with no segment (or a frame not present) loads nothing
+        const uint32_t seg_dw = v.seg_end ? (v.seg_end + 3) >> 2 : 0u;
         for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
             uint32_t x[U][4];
 #pragma unroll
             for (int u = 0; u < U; ++u) load4(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) acc_segment<L3>(x[u], r0 + (u * G + gl) * 4, v.seg_end, c);
+            for (int u = 0; u < U; ++u) acc_chunk<L3>(x[u], r0 + (u * G + gl) * 4, v.seg_end, hs);
         }
+        c = hs;
     }
     frame_store<G, FUSE, L3>(p, i, present, gl, h, v, c, hist, stage);
 }
 
-// The whole chain for frame i on a group of G lanes.
-template <int G, int LAYOUT, int FUSE>
+// The whole chain for frame i on a group of G lanes: R0 chunks per lane in round 0, U per later round.
+template <int G, int LAYOUT, int FUSE, int R0, int U>
 __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, bool present, uint32_t gl,
                                               uint32_t grp_base, Hist& hist) {
-    FrameState<G> st;
+    FrameState<G, R0> st;
     frame_meta<LAYOUT>(p, i, present, st);
-    frame_loads<G>(gl, st);
-    frame_finish<G, FUSE, HALO_RX_LATER_CHUNKS, kRound0<G>, kL3<LAYOUT>>(p, i, present, gl, grp_base, st, hist);
+    frame_loads(gl, st);
+    frame_finish<G, FUSE, U, R0, kL3<LAYOUT>>(p, i, present, gl, grp_base, st, hist);
 }
 
 __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
@@ -443,7 +494,7 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
 }
 
 // Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
-template <int G, int LAYOUT, int FUSE>
+template <int G, int LAYOUT, int FUSE, int R0 = kGroupRound0<G>, int U = HALO_RX_LATER_CHUNKS>
 __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     constexpr uint32_t FPW = 64 / G;  // frames per wave
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
@@ -458,7 +509,7 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t base = wave * FPW; base < p.n; base += nwaves * FPW) {
         const uint32_t i = base + lane / G;
-        process_frame<G, LAYOUT, FUSE>(p, i, i < p.n, gl, grp_base, hist);
+        process_frame<G, LAYOUT, FUSE, R0, U>(p, i, i < p.n, gl, grp_base, hist);
     }
     flush_hist(p, hist);
 }
@@ -568,6 +619,19 @@ __global__ void __launch_bounds__(HALO_RX_GROUP_BLOCK) __attribute__((amdgpu_wav
 rx_group_kernel(const RxParams p) {
     static_assert(G == 4 || G == 8 || G == 16, "G must be 4, 8 or 16");
     group_kernel_body<G, LAYOUT, FUSE>(p);
+}
+
+// One round trip per frame for uniform frames up to R0 x G x 16 bytes (1500 B: G = 8, R0 = 12):
+// the whole frame is issued before the header is parsed, round 0 is summed as soon as it lands
+// (frame_finish), and a frame longer than that (a wrong length hint) continues in later rounds of
+// U = 2 chunks, which cost few registers.
+#ifndef HALO_RX_ONE_ROUND_WAVES
+#define HALO_RX_ONE_ROUND_WAVES 5
+#endif
+template <int G, int R0, int LAYOUT, int FUSE>
+__global__ void __launch_bounds__(HALO_RX_GROUP_BLOCK) __attribute__((amdgpu_waves_per_eu(HALO_RX_ONE_ROUND_WAVES)))
+rx_group1_kernel(const RxParams p) {
+    group_kernel_body<G, LAYOUT, FUSE, R0, 2>(p);
 }
 
 // Mixed sizes (IMIX): each wave takes a window of 256 consecutive frames (four per lane), sorts
@@ -1065,6 +1129,7 @@ rx_stream_kernel(const RxParams p) {
 #define HALO_RX_LANE_MAX_BLOCKS HALO_RX_MAX_BLOCKS
 #endif
 constexpr int kVariantMix = -1, kVariantStream = 2, kVariantStreamMixed = 3;
+constexpr int kVariantG4One = 41, kVariantG8One = 81;  // rx_group1_kernel: G = 4, R0 = 9 / G = 8, R0 = 12
 
 uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS,
                   uint32_t waves_per_block = 4) {
@@ -1115,6 +1180,16 @@ hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
                 hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT, FUSE>), dim3(grid_for(p.n, 4, cap, wpb)), b, HALO_RX_GROUP_LDS_PAD, s, p);
             break;
         }
+        case kVariantG4One: case kVariantG8One: {
+            constexpr uint32_t wpb = HALO_RX_GROUP_BLOCK / 64;
+            const dim3 b(HALO_RX_GROUP_BLOCK);
+            const uint64_t cap = HALO_RX_MAX_BLOCKS * 4 / wpb;
+            if (variant == kVariantG4One)
+                hipLaunchKernelGGL((rx_group1_kernel<4, 9, LAYOUT, FUSE>), dim3(grid_for(p.n, 16, cap, wpb)), b, 0, s, p);
+            else
+                hipLaunchKernelGGL((rx_group1_kernel<8, 12, LAYOUT, FUSE>), dim3(grid_for(p.n, 8, cap, wpb)), b, 0, s, p);
+            break;
+        }
         default: hipLaunchKernelGGL((rx_mix_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, kMixWindow)), block, 0, s, p); break;
     }
     return hipGetLastError();
@@ -1133,6 +1208,7 @@ int pick_variant(uint32_t max_len, bool uniform, bool dense, uint32_t flags) {
         case HALO_RX_VARIANT_G16: return 16;
         case HALO_RX_VARIANT_MIX: return kVariantMix;
         case HALO_RX_VARIANT_STREAM: return kVariantStream;
+        case HALO_RX_VARIANT_ONE_ROUND: return max_len != 0 && max_len <= 576 ? kVariantG4One : kVariantG8One;
         default: break;
     }
     if (flags & HALO_RX_UNIFORM_LEN) uniform = max_len != 0;
@@ -1168,7 +1244,7 @@ int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* 
     if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_RECORD_COMPACT | HALO_RX_UNIFORM_LEN |
                   HALO_RX_L3_START | HALO_RX_VARIANT_MASK))
         return HALO_E_INVAL;
-    if (((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) > HALO_RX_VARIANT_STREAM) return HALO_E_INVAL;
+    if (((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) > HALO_RX_VARIANT_ONE_ROUND) return HALO_E_INVAL;
     if (reinterpret_cast<uintptr_t>(d_out) & 15u) return HALO_E_INVAL;
     p.n = n;
     p.flags = flags;

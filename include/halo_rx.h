@@ -106,6 +106,8 @@ extern "C" {
 #define HALO_RX_VARIANT_G16 4u
 #define HALO_RX_VARIANT_MIX 5u
 #define HALO_RX_VARIANT_STREAM 6u
+#define HALO_RX_VARIANT_ONE_ROUND 7u /* the whole frame in one round trip: 4 lanes x 9 chunks up to 576 B, */
+                                    /* else 8 lanes x 12 chunks (1536 B; longer frames in later rounds)  */
 
 /* ---- per-frame status: the FIRST failing check in reference order, 0 = OK ---------- */
 typedef enum halo_rx_status {

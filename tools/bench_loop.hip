@@ -250,3 +250,33 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_rx_flow_steps(
     };
     return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
 }
+
+// BASELINE config 1 as a compiled caller runs it (the cgo PacketHandle of go/gpurx/ring.go): per
+// batch the producer writes m frames into the ring (WritePacket per frame, untimed: the NIC side
+// of engine.Wire / the DPDK lcore), then one halo_rx_ring_poll + halo_rx_ring_commit is timed —
+// no Python between batches. us[k] = batch k's poll + commit time; *bad counts batches that did
+// not return exactly m frames, all OK.
+extern "C" __attribute__((visibility("default"))) int halo_bench_ring_polls(
+    void* ring_mem, halo_rx_ring_t* ring, const uint8_t* bytes, const uint64_t* offs, const uint16_t* lens, uint32_t m,
+    uint32_t flags, const halo_rx_netif_t* netif, halo_rx_result_t* out, int warmup, int iters, double* us,
+    uint32_t* bad) {
+    if (!ring_mem || !ring || !netif || !out || !us || !bad || iters <= 0) return HALO_E_INVAL;
+    *bad = 0;
+    for (int k = 0; k < warmup + iters; ++k) {
+        uint32_t w = 0;
+        int rc = halo_ring_write_batch(ring_mem, bytes, offs, lens, m, nullptr, &w);
+        if (rc) return rc;
+        if (w != m) return HALO_E_RANGE;  // the ring is full: the caller sized it wrong
+        halo_rx_ring_scan_t info;
+        const auto t0 = std::chrono::steady_clock::now();
+        rc = halo_rx_ring_poll(ring, flags, netif, out, nullptr, nullptr, &info);
+        if (!rc) rc = halo_rx_ring_commit(ring);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc) return rc;
+        bool ok = info.n_frames == m;
+        for (uint32_t i = 0; ok && i < m; ++i) ok = out[i].status == HALO_RX_OK;
+        if (!ok) ++*bad;
+        if (k >= warmup) us[k - warmup] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+    }
+    return HALO_OK;
+}

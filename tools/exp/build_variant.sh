@@ -6,5 +6,5 @@ cd "$(dirname "$0")/../.."
 name=$1; shift
 C=halo_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fvisibility=hidden "$@" -Iinclude -I$C \
-  $C/*.hip \
+  $C/*.hip $C/*.cc \
   -o tools/exp/libhalo_rx_$name.so

@@ -42,6 +42,11 @@ for s in "$@"; do
     tstream) step pytest_stream 600 python -u -m pytest tests/test_gpu_stream.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     gpus2) step gpus2 600 python bench.py --gpus 2 --steps 50 --warmup 5 --no-secondary --no-cpu ;;
     tunes) step tune_stream 600 python tools/tune.py --spec imix:-2,570B:-2,128B:-2,1500B:8 ;;
+    ringn) step ring_native 600 python tools/bench_ring_native.py --sweep ;;
+    ringprof) step ring_prof 600 rocprofv3 --kernel-trace --hip-runtime-trace --stats --output-format csv -d "$OUT/ringprof" -o run -- python3 tools/bench_ring_native.py --iters 500 ;;
+    tunev) step tune_variants 600 python tools/tune.py --only 570B,1500B,jumbo9000,imix --variants 4,8,16,-3,-2,-1 ;;
+    abold) step ab_old_new 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,570B:4,jumbo9000:16,imix:-1,64B:1" old new ;;
+    ab1r) step ab_one_round 600 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:-3,570B:-3" new new_w4 ;;
     *) echo "unknown step $s" ;;
   esac
 done
