@@ -287,16 +287,19 @@ __device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f
     const uint32_t H = f.hdr_end, PE = f.hdr_end + f.plen, ndw = (f.flen + 3u) >> 2;
     const uint64_t sv = f.pay - H;  // virtual address of frame byte 0 in payload space
     const uint32_t sh = (uint32_t)(sv & 3u);
-    const uint64_t sb = sv - sh;
-    const uint64_t lo = f.pay & ~3ull, hi = (f.pay + f.plen + 3u) & ~3ull;  // readable dwords [lo, hi)
     typedef const __attribute__((address_space(1))) uint32_t gu32_t;
+    // source dword 7 + m (frame bytes 4(7+m).. in payload space) as a signed dword index r relative
+    // to the payload's first readable dword, clamped into the readable dwords [0, last] in 32 bits
+    // (v_med3_i32) on one 64-bit base, instead of two 64-bit clamps per load
+    const uint64_t lo = f.pay & ~3ull;
+    const int32_t last = (int32_t)(((f.pay + f.plen + 3u) & ~3ull) - lo) / 4 - 1;
+    const int32_t r0 = (int32_t)((int64_t)(sv - sh) - (int64_t)lo) / 4;  // exact: both are dword aligned
+    gu32_t* base = (gu32_t*)(f.plen ? lo : reinterpret_cast<uint64_t>(safe));
     uint32_t src[10];  // source dwords 7..16
 #pragma unroll
     for (int m = 0; m < 10; ++m) {
-        uint64_t a = sb + 4u * (7u + m);
-        a = a < lo ? lo : a;
-        a = a + 4u > hi ? hi - 4u : a;
-        src[m] = *(gu32_t*)(f.plen ? a : reinterpret_cast<uint64_t>(safe));
+        const int32_t r = r0 + 7 + m;
+        src[m] = base[f.plen ? (r < 0 ? 0 : r > last ? last : r) : 0];
     }
     uint32_t o[16];
 #pragma unroll
@@ -429,8 +432,13 @@ tx_build_kernel(const BuildParams p) {
             uint32_t e[18];
             eth_header(f, id, ipv4_cksum(f, id, (p.flags & HALO_RX_CSUM_ENABLE) != 0), p, e);
             const bool l3 = f.mode == HALO_TX_BUILD_LOOPBACK;
+            if (__builtin_amdgcn_ballot_w64(l3) == 0) {  // wave-uniform: no loopback packet, no shift
 #pragma unroll
-            for (int k = 0; k < 16; ++k) hv[k] = k >= 14 ? 0u : l3 ? ((e[k + 3] >> 16) | (e[k + 4] << 16)) : e[k];
+                for (int k = 0; k < 16; ++k) hv[k] = k >= 14 ? 0u : e[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) hv[k] = k >= 14 ? 0u : l3 ? ((e[k + 3] >> 16) | (e[k + 4] << 16)) : e[k];
+            }
         }
         if constexpr (G == 1) {
             // a frame of <= 64 B keeps its header in registers; longer ones read it from LDS
