@@ -31,8 +31,8 @@ HALO_RX_UNIFORM_LEN = 0x8
 HALO_RX_L3_START = 0x10  # LoChan packets: every buffer starts at its IPv4 header
 HALO_RX_VARIANT_SHIFT = 8
 # lanes per frame -> HALO_RX_VARIANT_* (0 = automatic, -1 = the size-class mix kernel,
-# -2 = the byte-stream kernel, -3 = one round trip per frame)
-_VARIANT_CODE = {0: 0, 1: 1, 4: 2, 8: 3, 16: 4, -1: 5, -2: 6, -3: 7}
+# -2 = the byte-stream kernel)
+_VARIANT_CODE = {0: 0, 1: 1, 4: 2, 8: 3, 16: 4, -1: 5, -2: 6}
 
 
 def variant_flags(lanes_per_frame: int) -> int:
@@ -114,6 +114,7 @@ assert RING_SCAN_DTYPE.itemsize == 24
 RING_STOP_NAMES = ("EMPTY", "BAD_LEN", "PARTIAL", "CAPACITY", "MAX", "BAD_CURSOR")
 RING_STOP = {name: code for code, name in enumerate(RING_STOP_NAMES)}
 RING_REGISTER = 0x1
+RING_PERSISTENT = 0x2  # HALO_RING_PERSISTENT: small polls served by a resident consumer kernel
 
 def host_array(shape, dtype=np.uint8) -> np.ndarray:
     """A zeroed host array on pages of its own: an anonymous mmap, page-aligned, its size rounded
@@ -286,11 +287,31 @@ class HaloError(RuntimeError):
         self.code = code
 
 
+def _same_hip_runtime_as_torch() -> None:
+    """One HIP runtime per process. libhalo_rx.so needs libamdhip64.so.7; PyTorch-ROCm ships its own
+    copy (same soname) and links it by the name libamdhip64.so. Whichever loads first decides: if
+    torch comes first, our library binds to torch's copy; if we came first with /opt/rocm's, torch
+    would later load its copy as a SECOND runtime, and the two fight over the device (every call
+    here then fails with HALO_E_NODEV). So when torch is installed, load its runtime first (without
+    importing torch). Processes without torch (a cgo host) use the system runtime."""
+    import importlib.util
+
+    if "torch" in __import__("sys").modules:
+        return
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    rt = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(rt):
+        ctypes.CDLL(rt, mode=ctypes.RTLD_GLOBAL)
+
+
 def _load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build the HIP library first "
             "(python -c 'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
+    _same_hip_runtime_as_torch()
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _PROTOS.items():
         fn = getattr(lib, name)

@@ -56,6 +56,24 @@ enum SynthSlot : uint32_t {
 
 int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 
+// The resident small-poll consumer of a ring attached with HALO_RING_PERSISTENT (ring_rx.hip
+// drives it, rx_parse.hip runs it): one workgroup that waits on this control block, in pinned
+// host memory, for a request, parses its n frames as the lane kernel would (frames at
+// data + 4 * off_dw[i], the host's ReadPacket walk wrote off_dw / lens into pinned memory) and
+// writes their records to `out`, then publishes done_seq. The host never launches per poll.
+struct RingServiceCtl {
+    uint32_t req_seq;   // host: the request number (store-release after every field below)
+    uint32_t done_seq;  // device: req_seq once that request's records are visible (system scope)
+    uint32_t stop;      // host: 1 = exit now
+    uint32_t alive;     // device: 1 while the kernel runs (diagnostics)
+    uint32_t n, flags, mac_lo, mac_hi, own_ip, pad;
+    uint64_t out;       // device address of the request's records
+};
+// Launches the consumer on `s`: it serves requests after `last`, and exits when `stop` is set or
+// after idle_us microseconds without a request.
+int launch_ring_service(RingServiceCtl* d_ctl, const uint8_t* d_data, const uint32_t* d_off,
+                        const uint16_t* d_len, uint32_t last, uint32_t idle_us, hipStream_t s);
+
 // Live host registrations made through this library (halo_rx_host_register and
 // halo_rx_ring_attach(HALO_RING_REGISTER)), over RegMap (host_logic.h): page-aligned whole pages,
 // no shared page, checked before any HIP call. Removal waits for every device this library has

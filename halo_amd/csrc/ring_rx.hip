@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <thread>
 #include <vector>
@@ -519,12 +520,30 @@ struct halo_rx_ring {
     uint32_t* d_soff = nullptr;
     uint16_t* d_slen = nullptr;
     halo_rx_result_t* d_sres = nullptr;
+    // HALO_RING_PERSISTENT: the resident small-poll consumer (rx_parse.hip ring_service_kernel)
+    halo::RingServiceCtl* svc = nullptr;    // pinned, coherent
+    halo::RingServiceCtl* d_svc = nullptr;  // its device address
+    hipStream_t s_svc = nullptr;
+    uint32_t svc_seq = 0;                   // the last request made
+    bool svc_launched = false;
+    std::chrono::steady_clock::time_point svc_last{};  // when the last request completed
 };
 
 namespace {
 // Returns false when the ring memory could not be unregistered (the caller must not free it then:
 // the pages stay mapped for the device).
+// Stops the resident consumer (if any) and waits for its kernel to end.
+void stop_service(halo_rx_ring* r) {
+    if (!r->svc) return;
+    __atomic_store_n(&r->svc->stop, 1u, __ATOMIC_RELEASE);
+    if (r->s_svc) (void)hipStreamSynchronize(r->s_svc);
+    r->svc_launched = false;
+}
+
 bool free_ring(halo_rx_ring* r) {
+    stop_service(r);
+    if (r->s_svc) (void)hipStreamDestroy(r->s_svc);
+    if (r->svc) (void)hipHostFree(r->svc);
     for (hipEvent_t e : r->ev)
         if (e) (void)hipEventDestroy(e);
     if (r->s_copy) (void)hipStreamDestroy(r->s_copy);
@@ -585,6 +604,56 @@ int alloc_small(halo_rx_ring* r, uint64_t bytes) {
     return HALO_OK;
 }
 
+constexpr uint32_t kSvcMaxFrames = 16384;  // larger small polls take a full-grid launch
+constexpr uint32_t kSvcIdleUs = 20000;      // the resident consumer exits after 20 ms without a request
+
+// One request to the resident consumer: the frames' offsets / lengths are already in the pinned
+// arrays it reads (d_soff / d_slen). Fields first, then req_seq with release; spin on done_seq. A
+// consumer that went idle (or exited between its last check and the request) is relaunched: the
+// stream says whether its kernel is still running. Every wait is bounded.
+int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
+                    halo_rx_result_t* dout) {
+    using clk = std::chrono::steady_clock;
+    halo::RingServiceCtl* c = r->svc;
+    c->n = n;
+    c->flags = flags;
+    c->mac_lo = (uint32_t)netif->mac[0] | ((uint32_t)netif->mac[1] << 8) | ((uint32_t)netif->mac[2] << 16) |
+                ((uint32_t)netif->mac[3] << 24);
+    c->mac_hi = (uint32_t)netif->mac[4] | ((uint32_t)netif->mac[5] << 8);
+    c->own_ip = netif->ip;
+    c->out = reinterpret_cast<uint64_t>(dout);
+    auto launch = [&](uint32_t last) {
+        r->svc_launched = halo::launch_ring_service(r->d_svc, r->d_data, r->d_soff, r->d_slen, last, kSvcIdleUs,
+                                                    r->s_svc) == HALO_OK;
+        return r->svc_launched;
+    };
+    const uint32_t seq = r->svc_seq + 1;
+    // idle past half the timeout: the kernel may have exited; ask the stream (cheap, rare)
+    if (!r->svc_launched ||
+        (clk::now() - r->svc_last > std::chrono::microseconds(kSvcIdleUs / 2) && hipStreamQuery(r->s_svc) == hipSuccess)) {
+        if (!launch(r->svc_seq)) return HALO_E_HIP;
+    }
+    r->svc_seq = seq;
+    __atomic_store_n(&c->req_seq, seq, __ATOMIC_RELEASE);
+    const auto t0 = clk::now();
+    auto t_check = t0;
+    for (uint32_t k = 1;; ++k) {
+        if (__atomic_load_n(&c->done_seq, __ATOMIC_ACQUIRE) == seq) break;
+        __builtin_ia32_pause();
+        if ((k & 255u) == 0) {
+            const auto now = clk::now();
+            if (now - t_check > std::chrono::milliseconds(2)) {
+                t_check = now;
+                // the kernel ended before it saw this request (idle exit racing it): start another
+                if (hipStreamQuery(r->s_svc) == hipSuccess && !launch(seq - 1)) return HALO_E_HIP;
+            }
+            if (now - t0 > std::chrono::seconds(2)) return HALO_E_HIP;  // never wait forever
+        }
+    }
+    r->svc_last = clk::now();
+    return HALO_OK;
+}
+
 // The small path (BASELINE config 1: 1k-frame batches through engine.Wire). The host reads the
 // records' length fields exactly as ReadPacket does (mem/ring_buffer.go:309-335: 4 bytes per
 // record, never a frame byte); one rx launch then parses the frames where they lie in the
@@ -613,10 +682,15 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
             if (hipHostMalloc((void**)&r->h_sres, sb, hipHostMallocDefault) != hipSuccess) return HALO_E_NOMEM;
             if (!(r->d_sres = static_cast<halo_rx_result_t*>(device_view(r->h_sres, sb)))) return HALO_E_NOMEM;
         }
-        int rc = halo_rx_parse_batch_device(r->d_data, r->d_soff, r->d_slen, n, flags, netif, max_len,
+        int rc;
+        if (r->svc && n <= kSvcMaxFrames) {
+            rc = service_request(r, n, flags, netif, dout ? dout : r->d_sres);
+        } else {
+            rc = halo_rx_parse_batch_device(r->d_data, r->d_soff, r->d_slen, n, flags, netif, max_len,
                                             dout ? dout : r->d_sres, nullptr, r->s_comp);
+            if (!rc && hipStreamSynchronize(r->s_comp) != hipSuccess) rc = HALO_E_HIP;
+        }
         if (rc) return rc;
-        if (hipStreamSynchronize(r->s_comp) != hipSuccess) return HALO_E_HIP;
         if (!dout) memcpy(out, r->h_sres, rb);
         if (status_hist)
             for (uint32_t i = 0; i < n; ++i) ++status_hist[out[i].status];  // the statuses the kernel wrote
@@ -677,7 +751,8 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     uint8_t* mem = static_cast<uint8_t*>(ring_mem);
     int rc = halo::validate_ring(mem, offset, &size, &tail);
     if (rc) return rc;
-    if (attach_flags & ~HALO_RING_REGISTER) return HALO_E_INVAL;
+    if (attach_flags & ~(HALO_RING_REGISTER | HALO_RING_PERSISTENT)) return HALO_E_INVAL;
+    if ((attach_flags & HALO_RING_PERSISTENT) && !(attach_flags & HALO_RING_REGISTER)) return HALO_E_INVAL;
     // a registered ring pins the whole pages it spans: it must start on a page of its own
     const uint64_t page = halo::host_page_size();
     const uint64_t reg_bytes = (halo::kRbHeader + size + page - 1) / page * page;
@@ -724,6 +799,18 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
         if (ok && size <= halo::kMaxSpan + (64ull << 10)) {  // dword offsets into the data area fit u32
             r->d_data = static_cast<uint8_t*>(device_view(r->data, size));
             ok = !r->d_data || alloc_small(r, halo::kSmallPoll) == HALO_OK;
+        }
+        if (ok && (attach_flags & HALO_RING_PERSISTENT) && r->d_data) {
+            void* cp = nullptr;
+            ok = hipHostMalloc(&cp, sizeof(halo::RingServiceCtl), hipHostMallocCoherent | hipHostMallocMapped) ==
+                     hipSuccess &&
+                 hipStreamCreateWithFlags(&r->s_svc, hipStreamNonBlocking) == hipSuccess;
+            r->svc = static_cast<halo::RingServiceCtl*>(cp);
+            if (ok) {
+                memset(cp, 0, sizeof(halo::RingServiceCtl));
+                r->d_svc = static_cast<halo::RingServiceCtl*>(device_view(cp, sizeof(halo::RingServiceCtl)));
+                ok = r->d_svc != nullptr;
+            }
         }
     }
     if (!ok) {

@@ -21,6 +21,7 @@
 #include <atomic>
 #include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <vector>
 
 #include "halo_common.h"
@@ -50,6 +51,10 @@ struct halo_route_table {
     int device = -1;
     std::atomic<int> active{-1};  // published generation, -1 before the first sync
     std::mutex sync_mu;           // one sync at a time
+    // Lookups hold it shared from route_view until their kernel is enqueued (RouteViewLock); a sync
+    // holds it exclusively while it drains the device and rewrites the unpublished generation, so
+    // no lookup can be enqueued against a generation between its view and the drain.
+    mutable std::shared_mutex view_mu;
 };
 
 namespace halo {
@@ -266,6 +271,7 @@ extern "C" HALO_API int halo_route_sync_device(halo_route_table_t* t, int device
         c.walk(0, 0, 0, 0u);
     }
     std::lock_guard<std::mutex> sg(t->sync_mu);
+    std::unique_lock<std::shared_mutex> vl(t->view_mu);  // no lookup between its view and its launch
     const int cur = t->active.load(std::memory_order_acquire);
     // the generation written now was last published before `cur`: lookups launched while it was
     // active may still be running on any stream of the device, so drain the device first
@@ -291,6 +297,13 @@ extern "C" HALO_API int halo_route_sync_device(halo_route_table_t* t, int device
 }
 
 namespace halo {
+RouteViewLock::RouteViewLock(const halo_route_table_t* t) : t_(t) {
+    if (t_) t_->view_mu.lock_shared();
+}
+RouteViewLock::~RouteViewLock() {
+    if (t_) t_->view_mu.unlock_shared();
+}
+
 int route_view(const halo_route_table_t* t, LpmView* out) {
     if (!t || !out) return HALO_E_INVAL;
     const int a = t->active.load(std::memory_order_acquire);
@@ -303,6 +316,7 @@ int route_view(const halo_route_table_t* t, LpmView* out) {
 
 extern "C" HALO_API int halo_route_lookup_device(const halo_route_table_t* t, const uint32_t* d_ips, uint32_t n,
                                                  uint32_t* d_route_ids, halo_stream_t stream) {
+    halo::RouteViewLock lk(t);
     halo::LpmView v;
     if (halo::route_view(t, &v)) return HALO_E_INVAL;
     if (n == 0) return HALO_OK;
@@ -318,6 +332,7 @@ extern "C" HALO_API int halo_route_lookup_device(const halo_route_table_t* t, co
 extern "C" HALO_API int halo_route_lookup_records_device(const halo_route_table_t* t,
                                                          const halo_rx_result_t* d_records, uint32_t n,
                                                          uint32_t* d_route_ids, halo_stream_t stream) {
+    halo::RouteViewLock lk(t);
     halo::LpmView v;
     if (halo::route_view(t, &v)) return HALO_E_INVAL;
     if (n == 0) return HALO_OK;

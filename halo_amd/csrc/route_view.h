@@ -40,7 +40,19 @@ __device__ __forceinline__ uint32_t find_route(const LpmView& v, uint32_t ip) {
     return v.ids[l.x + fnv1a32(ip) % l.y];
 }
 
-// The device view of a table synced with halo_route_sync_device (HALO_E_INVAL otherwise).
+// The device view of a table synced with halo_route_sync_device (HALO_E_INVAL otherwise). Take it
+// under a RouteViewLock held until the kernel using it is enqueued: a concurrent sync then cannot
+// rewrite that generation before the device has drained the launch.
 int route_view(const halo_route_table_t* t, LpmView* out);
+class RouteViewLock {
+public:
+    explicit RouteViewLock(const halo_route_table_t* t);
+    ~RouteViewLock();
+    RouteViewLock(const RouteViewLock&) = delete;
+    RouteViewLock& operator=(const RouteViewLock&) = delete;
+
+private:
+    const halo_route_table_t* t_;
+};
 
 }  // namespace halo

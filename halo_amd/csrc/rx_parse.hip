@@ -286,17 +286,6 @@ struct Hist {
 // ~55 VGPRs (occupancy 5 -> 3) and lost more than it gained; kept as a knob.
 template <int G>
 constexpr int kRound0 = 4;
-// Round 0 of the uniform-length group kernels only (A/B knobs): chunks per lane issued before the
-// header parse. 12 for G = 8 covers a whole 1536 B frame in one round trip.
-#ifndef HALO_RX_G8_ROUND0
-#define HALO_RX_G8_ROUND0 4
-#endif
-#ifndef HALO_RX_G4_ROUND0
-#define HALO_RX_G4_ROUND0 4
-#endif
-template <int G>
-constexpr int kGroupRound0 = G == 8 ? HALO_RX_G8_ROUND0 : G == 4 ? HALO_RX_G4_ROUND0 : 4;
-
 // One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
 template <int G, int R0 = kRound0<G>>
 struct FrameState {
@@ -494,7 +483,7 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
 }
 
 // Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
-template <int G, int LAYOUT, int FUSE, int R0 = kGroupRound0<G>, int U = HALO_RX_LATER_CHUNKS>
+template <int G, int LAYOUT, int FUSE, int R0 = kRound0<G>, int U = HALO_RX_LATER_CHUNKS>
 __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     constexpr uint32_t FPW = 64 / G;  // frames per wave
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
@@ -520,7 +509,21 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
 // consecutive: they are staged in LDS and written with fully coalesced 16-byte stores (a lane
 // writing its own 32 B record at a 32 B stride stored the same bytes 25 % slower:
 // profiles/r01/probe_store_patterns.log).
+// One wave's window of 64 consecutive frames, a lane each (frames base .. base + 63): parse, stage
+// the 64 records in the wave's LDS (s_rec_w: 128 x 16 B) and store them fully coalesced.
 template <int LAYOUT, int FUSE>
+__device__ __forceinline__ void lane_window_finish(const RxParams& p, uint32_t base, uint32_t lane, FrameState<1>& st,
+                                                   uint4* s_rec_w, Hist& hist);
+template <int LAYOUT, int FUSE>
+__device__ __forceinline__ void lane_window(const RxParams& p, uint32_t base, uint32_t lane, uint4* s_rec_w,
+                                           Hist& hist) {
+    const uint32_t i = base + lane;
+    FrameState<1> st;
+    frame_meta<LAYOUT>(p, i, i < p.n, st);
+    frame_loads<1>(0, st);
+    lane_window_finish<LAYOUT, FUSE>(p, base, lane, st, s_rec_w, hist);
+}
+
 #ifndef HALO_RX_LANE_WAVES
 #define HALO_RX_LANE_WAVES 0
 #endif
@@ -550,6 +553,26 @@ template <int LAYOUT, int FUSE>
 #ifndef HALO_RX_LANE_XCD
 #define HALO_RX_LANE_XCD 0
 #endif
+template <int LAYOUT, int FUSE>
+__device__ __forceinline__ void lane_window_finish(const RxParams& p, uint32_t base, uint32_t lane, FrameState<1>& st,
+                                                   uint4* s_rec_w, Hist& hist) {
+    const bool compact = (p.flags & HALO_RX_RECORD_COMPACT) != 0;
+    const uint32_t i = base + lane;
+    frame_finish<1, FUSE, HALO_RX_LANE_LATER, kRound0<1>, kL3<LAYOUT>>(p, i, i < p.n, 0, lane, st, hist,
+                                                                     &s_rec_w[compact ? lane : 2 * lane]);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nrec = p.n - base < 64 ? p.n - base : 64;  // records of this wave
+    if (compact) {
+        if (lane < nrec) store16(reinterpret_cast<uint4*>(p.out) + base + lane, s_rec_w[lane]);
+    } else {
+        uint4* out4 = reinterpret_cast<uint4*>(p.out) + 2ull * base;
+        if (lane < 2 * nrec) store16(out4 + lane, s_rec_w[lane]);
+        if (64 + lane < 2 * nrec) store16(out4 + 64 + lane, s_rec_w[64 + lane]);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int LAYOUT, int FUSE>
 __global__ void __launch_bounds__(HALO_RX_LANE_BLOCK) __attribute__((amdgpu_num_sgpr(80)))
 #if HALO_RX_LANE_WAVES
 __attribute__((amdgpu_waves_per_eu(HALO_RX_LANE_WAVES)))
@@ -562,7 +585,6 @@ rx_lane_kernel(const RxParams p) {
     Hist hist{s_hist, 0};
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = threadIdx.x >> 6;
-    const bool compact = (p.flags & HALO_RX_RECORD_COMPACT) != 0;
 #if HALO_RX_LANE_XCD
     const uint32_t nb = gridDim.x, per = nb >> 3, rem = nb & 7u, xcd = blockIdx.x & 7u;
     const uint32_t lblock = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (blockIdx.x >> 3);
@@ -577,30 +599,85 @@ rx_lane_kernel(const RxParams p) {
     frame_meta<LAYOUT>(p, wave * 64 + lane, wave * 64 + lane < p.n, nx);
 #endif
     for (uint32_t base = wave * 64; base < p.n; base += nwaves * 64) {
+#if HALO_RX_LANE_PREFETCH
         const uint32_t i = base + lane;
         FrameState<1> st;
-#if HALO_RX_LANE_PREFETCH
         st.frame = nx.frame; st.L = nx.L; st.ndw = nx.ndw;
         frame_loads<1>(0, st);
         frame_meta<LAYOUT>(p, i + nwaves * 64, i + nwaves * 64 < p.n, nx);
+        lane_window_finish<LAYOUT, FUSE>(p, base, lane, st, s_rec[w], hist);
 #else
-        frame_meta<LAYOUT>(p, i, i < p.n, st);
-        frame_loads<1>(0, st);
+        lane_window<LAYOUT, FUSE>(p, base, lane, s_rec[w], hist);
 #endif
-        frame_finish<1, FUSE, HALO_RX_LANE_LATER, kRound0<1>, kL3<LAYOUT>>(p, i, i < p.n, 0, lane, st, hist,
-                                                                         &s_rec[w][compact ? lane : 2 * lane]);
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t nrec = p.n - base < 64 ? p.n - base : 64;  // records of this wave
-        if (compact) {
-            if (lane < nrec) store16(reinterpret_cast<uint4*>(p.out) + base + lane, s_rec[w][lane]);
-        } else {
-            uint4* out4 = reinterpret_cast<uint4*>(p.out) + 2ull * base;
-            if (lane < 2 * nrec) store16(out4 + lane, s_rec[w][lane]);
-            if (64 + lane < 2 * nrec) store16(out4 + 64 + lane, s_rec[w][64 + lane]);
-        }
-        __builtin_amdgcn_wave_barrier();
     }
     flush_hist(p, hist);
+}
+
+// The resident small-poll consumer (RingServiceCtl, halo_common.h). Thread 0 waits for a request
+// — a system-scope acquire load of req_seq in pinned host memory, s_sleep between tries, bounded by
+// the stop flag and an idle timeout on the 100 MHz real-time counter, so every wave reaches the
+// exit — and copies it into LDS; the 16 waves then parse its frames 64 at a time with the lane
+// kernel's window code; after a block barrier thread 0 fences and publishes done_seq.
+constexpr uint32_t kSvcWaves = 16;
+__global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServiceCtl* ctl, const uint8_t* data,
+                                                                      const uint32_t* off, const uint16_t* len,
+                                                                      uint32_t last, uint64_t idle_ticks) {
+    __shared__ uint32_t s_cmd[8];  // seq, exit, n, flags, mac_lo, mac_hi, own_ip
+    __shared__ uint64_t s_out;
+    __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
+    __shared__ uint4 s_rec[kSvcWaves][128];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) __hip_atomic_store(&ctl->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint32_t seq = last, quit = 0;
+            for (;;) {
+                seq = __hip_atomic_load(&ctl->req_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (seq != last) break;
+                if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                    __builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
+                    quit = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            s_cmd[0] = seq;
+            s_cmd[1] = quit;
+            if (!quit) {
+                s_cmd[2] = ctl->n;
+                s_cmd[3] = ctl->flags;
+                s_cmd[4] = ctl->mac_lo;
+                s_cmd[5] = ctl->mac_hi;
+                s_cmd[6] = ctl->own_ip;
+                s_out = ctl->out;
+            }
+        }
+        __syncthreads();
+        if (s_cmd[1]) break;
+        RxParams p{};
+        p.bytes = data;
+        p.offsets_dw = off;
+        p.lens = len;
+        p.n = s_cmd[2];
+        p.flags = s_cmd[3];
+        p.mac_lo = s_cmd[4];
+        p.mac_hi = s_cmd[5];
+        p.own_ip = s_cmd[6];
+        p.out = reinterpret_cast<halo_rx_result_t*>(s_out);
+        Hist hist{s_hist, 0};
+        for (uint32_t base = w * 64; base < p.n; base += kSvcWaves * 64) lane_window<0, 0>(p, base, lane, s_rec[w], hist);
+        __syncthreads();  // every record of the request stored
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(&ctl->done_seq, s_cmd[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            last = s_cmd[0];
+            t_idle = __builtin_amdgcn_s_memrealtime();
+        }
+        __syncthreads();  // s_cmd is rewritten by the next wait
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&ctl->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // G lanes per frame (G in {4, 8, 16}); VGPR-limited occupancy, so no SGPR cap.
@@ -619,19 +696,6 @@ __global__ void __launch_bounds__(HALO_RX_GROUP_BLOCK) __attribute__((amdgpu_wav
 rx_group_kernel(const RxParams p) {
     static_assert(G == 4 || G == 8 || G == 16, "G must be 4, 8 or 16");
     group_kernel_body<G, LAYOUT, FUSE>(p);
-}
-
-// One round trip per frame for uniform frames up to R0 x G x 16 bytes (1500 B: G = 8, R0 = 12):
-// the whole frame is issued before the header is parsed, round 0 is summed as soon as it lands
-// (frame_finish), and a frame longer than that (a wrong length hint) continues in later rounds of
-// U = 2 chunks, which cost few registers.
-#ifndef HALO_RX_ONE_ROUND_WAVES
-#define HALO_RX_ONE_ROUND_WAVES 5
-#endif
-template <int G, int R0, int LAYOUT, int FUSE>
-__global__ void __launch_bounds__(HALO_RX_GROUP_BLOCK) __attribute__((amdgpu_waves_per_eu(HALO_RX_ONE_ROUND_WAVES)))
-rx_group1_kernel(const RxParams p) {
-    group_kernel_body<G, LAYOUT, FUSE, R0, 2>(p);
 }
 
 // Mixed sizes (IMIX): each wave takes a window of 256 consecutive frames (four per lane), sorts
@@ -1129,7 +1193,6 @@ rx_stream_kernel(const RxParams p) {
 #define HALO_RX_LANE_MAX_BLOCKS HALO_RX_MAX_BLOCKS
 #endif
 constexpr int kVariantMix = -1, kVariantStream = 2, kVariantStreamMixed = 3;
-constexpr int kVariantG4One = 41, kVariantG8One = 81;  // rx_group1_kernel: G = 4, R0 = 9 / G = 8, R0 = 12
 
 uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS,
                   uint32_t waves_per_block = 4) {
@@ -1180,16 +1243,6 @@ hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
                 hipLaunchKernelGGL((rx_group_kernel<16, LAYOUT, FUSE>), dim3(grid_for(p.n, 4, cap, wpb)), b, HALO_RX_GROUP_LDS_PAD, s, p);
             break;
         }
-        case kVariantG4One: case kVariantG8One: {
-            constexpr uint32_t wpb = HALO_RX_GROUP_BLOCK / 64;
-            const dim3 b(HALO_RX_GROUP_BLOCK);
-            const uint64_t cap = HALO_RX_MAX_BLOCKS * 4 / wpb;
-            if (variant == kVariantG4One)
-                hipLaunchKernelGGL((rx_group1_kernel<4, 9, LAYOUT, FUSE>), dim3(grid_for(p.n, 16, cap, wpb)), b, 0, s, p);
-            else
-                hipLaunchKernelGGL((rx_group1_kernel<8, 12, LAYOUT, FUSE>), dim3(grid_for(p.n, 8, cap, wpb)), b, 0, s, p);
-            break;
-        }
         default: hipLaunchKernelGGL((rx_mix_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, kMixWindow)), block, 0, s, p); break;
     }
     return hipGetLastError();
@@ -1208,7 +1261,6 @@ int pick_variant(uint32_t max_len, bool uniform, bool dense, uint32_t flags) {
         case HALO_RX_VARIANT_G16: return 16;
         case HALO_RX_VARIANT_MIX: return kVariantMix;
         case HALO_RX_VARIANT_STREAM: return kVariantStream;
-        case HALO_RX_VARIANT_ONE_ROUND: return max_len != 0 && max_len <= 576 ? kVariantG4One : kVariantG8One;
         default: break;
     }
     if (flags & HALO_RX_UNIFORM_LEN) uniform = max_len != 0;
@@ -1244,7 +1296,7 @@ int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* 
     if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_RECORD_COMPACT | HALO_RX_UNIFORM_LEN |
                   HALO_RX_L3_START | HALO_RX_VARIANT_MASK))
         return HALO_E_INVAL;
-    if (((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) > HALO_RX_VARIANT_ONE_ROUND) return HALO_E_INVAL;
+    if (((flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT) > HALO_RX_VARIANT_STREAM) return HALO_E_INVAL;
     if (reinterpret_cast<uintptr_t>(d_out) & 15u) return HALO_E_INVAL;
     p.n = n;
     p.flags = flags;
@@ -1311,6 +1363,7 @@ extern "C" HALO_API int halo_rx_parse_route_batch_device(const uint8_t* d_bytes,
                                                          halo_rx_result_t* d_out, uint32_t* d_status_hist,
                                                          const halo_route_table_t* table, uint32_t* d_route_ids,
                                                          halo_stream_t stream) {
+    halo::RouteViewLock lk(table);  // until the fused kernel is enqueued
     halo::LpmView v{};
     if (halo::route_view(table, &v) || !d_route_ids) return HALO_E_INVAL;
     halo::RxParams p{};
@@ -1352,3 +1405,12 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
     const uint32_t max_len = d_lens ? (uint32_t)(stride < 65535 ? stride : 65535) : len;
     return halo::launch_parse(p, d_lens ? 1 : 2, max_len, d_lens == nullptr, static_cast<hipStream_t>(stream));
 }
+
+namespace halo {
+int launch_ring_service(RingServiceCtl* d_ctl, const uint8_t* d_data, const uint32_t* d_off, const uint16_t* d_len,
+                        uint32_t last, uint32_t idle_us, hipStream_t s) {
+    hipLaunchKernelGGL(ring_service_kernel, dim3(1), dim3(64 * kSvcWaves), 0, s, d_ctl, d_data, d_off, d_len, last,
+                       (uint64_t)idle_us * 100u);  // s_memrealtime: 100 MHz
+    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+}  // namespace halo

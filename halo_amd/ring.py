@@ -21,7 +21,7 @@ from typing import Optional
 import numpy as np
 
 from . import _lib
-from ._lib import RESULT_DTYPE, RING_HEADER, RING_REGISTER, RING_SCAN_DTYPE, RING_STOP_NAMES, NetIf
+from ._lib import RESULT_DTYPE, RING_HEADER, RING_PERSISTENT, RING_REGISTER, RING_SCAN_DTYPE, RING_STOP_NAMES, NetIf
 from .protocol import flags_word
 
 WIRE_MAX_PACKET_SIZE = 1514  # engine/engine.go:507
@@ -85,15 +85,18 @@ class RingBuffer:
 class RingConsumer:
     """The GPU consumer of one ring (halo_rx_ring_attach). ``capacity`` is ReadPacket's
     ``len(data)`` (1514 in the DPDK driver and Wire). ``small_poll``: spans up to this many bytes
-    take the one-launch small path (None: the library default; 0: always the pipelined path)."""
+    take the one-launch small path (None: the library default; 0: always the pipelined path).
+    ``persistent``: small polls are served by a resident consumer kernel (HALO_RING_PERSISTENT):
+    no launch and no stream synchronisation per poll."""
 
     def __init__(self, ring: RingBuffer, device: int = 0, capacity: int = MAX_PACKET_SIZE, max_bytes: int = 0,
-                 max_frames: int = 0, register: bool = True, small_poll: int | None = None):
+                 max_frames: int = 0, register: bool = True, small_poll: int | None = None, persistent: bool = False):
         self.ring = ring
         self._out_registered = False
         h = ctypes.c_void_p()
-        rc = _lib.lib.halo_rx_ring_attach(device, ring.mem.ctypes.data, 0, capacity, max_bytes, max_frames,
-                                          RING_REGISTER if register else 0, ctypes.byref(h))
+        flags = (RING_REGISTER if register else 0) | (RING_PERSISTENT if persistent else 0)
+        rc = _lib.lib.halo_rx_ring_attach(device, ring.mem.ctypes.data, 0, capacity, max_bytes, max_frames, flags,
+                                          ctypes.byref(h))
         _lib.check("halo_rx_ring_attach", rc)
         self._h = h
         if small_poll is not None:
@@ -145,9 +148,9 @@ class RingConsumer:
 class Wire:
     """engine.Wire (engine/engine.go:507-559): a ring with an 8 MiB data area as a virtual link."""
 
-    def __init__(self, device: int = 0, data_size: int = 8 << 20):
+    def __init__(self, device: int = 0, data_size: int = 8 << 20, persistent: bool = False):
         self.ring = RingBuffer(data_size)
-        self.consumer = RingConsumer(self.ring, device=device, capacity=WIRE_MAX_PACKET_SIZE)
+        self.consumer = RingConsumer(self.ring, device=device, capacity=WIRE_MAX_PACKET_SIZE, persistent=persistent)
 
     def Tx(self, pkt: bytes) -> None:  # engine/engine.go:548-553
         if len(pkt) == 0 or len(pkt) > WIRE_MAX_PACKET_SIZE:

@@ -106,8 +106,6 @@ extern "C" {
 #define HALO_RX_VARIANT_G16 4u
 #define HALO_RX_VARIANT_MIX 5u
 #define HALO_RX_VARIANT_STREAM 6u
-#define HALO_RX_VARIANT_ONE_ROUND 7u /* the whole frame in one round trip: 4 lanes x 9 chunks up to 576 B, */
-                                    /* else 8 lanes x 12 chunks (1536 B; longer frames in later rounds)  */
 
 /* ---- per-frame status: the FIRST failing check in reference order, 0 = OK ---------- */
 typedef enum halo_rx_status {
@@ -297,6 +295,14 @@ HALO_API int halo_rx_shard_multi(halo_rx_host_ctx_t* const* ctxs, uint32_t n_ctx
                                         of its data area are registered and must not be shared with
                                         another live registration (HALO_E_INVAL; see
                                         halo_rx_host_register)                                      */
+#define HALO_RING_PERSISTENT 0x2u    /* attach (with HALO_RING_REGISTER): small polls of up to 16384
+                                        frames are served by a resident consumer kernel (one
+                                        workgroup on one CU) that waits on a control block in pinned
+                                        memory: a poll writes a request and spins on its completion,
+                                        with no kernel launch and no stream synchronisation. The
+                                        kernel exits after 20 ms without a request (the next poll
+                                        relaunches it) and at detach. Same records, stops and cursor
+                                        as the other paths.                                          */
 
 typedef struct halo_rx_ring_scan {
     uint32_t n_frames;  /* frames taken                                                      */
@@ -554,7 +560,10 @@ HALO_API int halo_route_get(const halo_route_table_t* t, uint32_t id, halo_route
  * Double-buffered: the new table is written into the generation not in use, after the device
  * has drained every lookup that could still read that one (a device synchronisation), and is
  * then published. A lookup sees the table last published when it was launched — never one
- * being rewritten, as FindRoute under RouteTable.RLock never does (engine/ipv4_engine.go:351). */
+ * being rewritten, as FindRoute under RouteTable.RLock never does (engine/ipv4_engine.go:351).
+ * Lookups and syncs may run on different threads: a lookup holds the table's read lock from
+ * taking its view until its kernel is enqueued, and a sync takes the write lock before it
+ * drains the device, so no launch can slip in between (RWMutex semantics, :270-275). */
 HALO_API int halo_route_sync_device(halo_route_table_t* t, int device);
 /* FindRoute for each address (IpAddrToU form) / each record's dst_ip: route id, HALO_ROUTE_NONE
  * or HALO_ROUTE_PANIC. Asynchronous on `stream`; uses the last synced table. */

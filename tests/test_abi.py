@@ -79,10 +79,10 @@ def test_argument_validation_without_gpu():
                                         out.ctypes.data + 4, None, None) == -1  # misaligned output
     assert L.halo_rx_parse_strided_device(buf.ctypes.data, 6, None, 60, 2, 1, n, out.ctypes.data, None,
                                           None) == -1  # stride not a multiple of 4
-    for v in range(8):  # every HALO_RX_VARIANT_* code (0..7 = ONE_ROUND) passes validation: no device here
+    for v in (7,):  # HALO_RX_VARIANT_* codes end at STREAM = 6
         assert L.halo_rx_parse_batch_device(buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 1,
                                             1 | (v << _lib.HALO_RX_VARIANT_SHIFT), n, 0, out.ctypes.data, None,
-                                            None) == -2
+                                            None) == -1
     assert not hasattr(_lib.lib, "halo_rx_tune_variant")  # no process-wide override: per call only
     assert L.halo_rx_parse_strided_device(buf.ctypes.data, 60, None, 64, 2, 1, n, out.ctypes.data, None,
                                           None) == -1  # overlapping uniform frames

@@ -74,7 +74,7 @@ def test_fuzz_auto_variant_bit_exact(dev, corpus, flags):
     assert np.array_equal(engine.dispatch(got, NetIf.make()), engine.dispatch(wrec, NetIf.make()))
 
 
-@pytest.mark.parametrize("variant", [1, 4, 8, 16, -1, -2, -3])
+@pytest.mark.parametrize("variant", [1, 4, 8, 16, -1, -2])
 def test_fuzz_every_variant_full_and_compact(dev, corpus, variant):
     from halo_amd import _lib
     from halo_amd._lib import RECORD16_DTYPE, RESULT_DTYPE, compact_of

@@ -63,8 +63,15 @@ def _span(ring, start, used):
     return ring.mem[128:][idx]
 
 
-SMALL = [0, None, 16 << 20]  # pipelined path only / library default / small path for every poll
-SMALL_IDS = ["pipelined", "default", "small16M"]
+SMALL = [0, None, 16 << 20, "persistent"]  # pipelined only / library default / small path for every poll /
+SMALL_IDS = ["pipelined", "default", "small16M", "persistent"]  # ... served by the resident consumer kernel
+
+
+def _small_kw(small_poll):
+    """RingConsumer keywords for a SMALL entry ("persistent": HALO_RING_PERSISTENT, every poll small)."""
+    if small_poll == "persistent":
+        return {"small_poll": 16 << 20, "persistent": True}
+    return {"small_poll": small_poll}
 
 
 @pytest.mark.parametrize("small_poll", SMALL, ids=SMALL_IDS)
@@ -84,7 +91,7 @@ def test_poll_golden_frames_across_the_wrap(dev, golden, oracle_lib, flags, smal
     assert n_w == int(small.sum())
     want, acts, pos, tail = _oracle_drain(O, ring.mem, O.NetIf.make(), flags, 1514)
     assert len(want) == n_w
-    cons = RingConsumer(ring, capacity=1514, small_poll=small_poll)
+    cons = RingConsumer(ring, capacity=1514, **_small_kw(small_poll))
     got, info, gpos = cons.poll(NetIf.make(), check_sum_enable=bool(flags & 1), jumbo=bool(flags & 2),
                                 positions=True)
     assert_records_equal(got.copy(), want, [n for n, s in zip(names, small) if s], f"ring flags={flags}")
@@ -125,7 +132,7 @@ def test_poll_stops_like_readpacket(dev, golden, oracle_lib, small_poll):
             ring.mem[0:8].view(np.uint64)[0] = ring.head + 8
         ring.write_batch(data, offs[sel].astype(np.uint64) * 4, lens[sel])
         kw = dict(max_frames=50) if case == "max_frames" else dict(max_bytes=6000) if case == "max_bytes" else {}
-        cons = RingConsumer(ring, capacity=1514, small_poll=small_poll, **kw)
+        cons = RingConsumer(ring, capacity=1514, **_small_kw(small_poll), **kw)
         mem_before = ring.mem.copy()
         got_all = []
         for _ in range(200):
@@ -224,7 +231,8 @@ def test_scan_device_matches_walk(dev, oracle_lib, name, gen, cap, max_frames, c
         assert np.array_equal(d_len[:n].cpu().numpy().view(np.uint16), w_len), name
 
 
-def test_small_poll_laps_the_ring(dev, oracle_lib):
+@pytest.mark.parametrize("persistent", [False, True], ids=["launch", "persistent"])
+def test_small_poll_laps_the_ring(dev, oracle_lib, persistent):
     """The small path reads frames in place in the registered ring: 300 produce/poll/commit rounds
     over a 64 KiB ring (the data area is rewritten ~70 times) with fresh frames each round, a
     record wrapping the end now and then (that poll takes the pipelined path), each poll's records
@@ -235,7 +243,7 @@ def test_small_poll_laps_the_ring(dev, oracle_lib):
     O = oracle_lib
     ring = RingBuffer(1 << 16)
     _seek(ring, (1 << 33) - 100)
-    cons = RingConsumer(ring, capacity=1514)
+    cons = RingConsumer(ring, capacity=1514, persistent=persistent)
     rng = np.random.default_rng(17)
     onetif = O.NetIf.make()
     for it in range(300):
@@ -435,3 +443,34 @@ def test_registration_registry_refuses_shared_pages(dev):
     assert regs.get(cons._out.ctypes.data) == _lib.host_pages(cons._out.nbytes), regs
     cons.close()
     assert _lib.registered_count() == 0
+
+
+def test_persistent_consumer_idle_exit_and_relaunch(dev, golden, oracle_lib):
+    """HALO_RING_PERSISTENT: the resident consumer exits after 20 ms without a request and the next
+    poll relaunches it; polls before and after, and a detach while it is idle or running, all give
+    the oracle's records."""
+    import time
+
+    from halo_amd._lib import NetIf
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    O = oracle_lib
+    meta, blob = golden
+    fr = [e for e in meta["frames"] if 0 < e["len"] <= 1514]
+    offs = np.array([e["offset"] for e in fr], np.uint64)
+    lens = np.array([e["len"] for e in fr], np.uint16)
+    onetif = O.NetIf.make()
+    for detach_idle in (False, True):
+        ring = RingBuffer(1 << 20)
+        cons = RingConsumer(ring, capacity=1514, persistent=True)
+        for rnd in range(4):
+            assert ring.write_batch(blob, offs, lens) == len(lens)
+            got, info, _ = cons.poll(NetIf.make())
+            assert info["n_frames"] == len(lens), (rnd, info)
+            want_recs, _, _, _ = _oracle_drain(O, ring.mem, onetif, 1, 1514)
+            assert_records_equal(got.copy(), want_recs, None, f"persistent round {rnd}")
+            cons.commit()
+            time.sleep(0.05 if rnd % 2 == 0 else 0.001)  # > 20 ms: the kernel exits; 1 ms: still resident
+        if detach_idle:
+            time.sleep(0.05)
+        cons.close()

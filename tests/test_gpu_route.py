@@ -168,3 +168,69 @@ def test_route_validation(dev):
     rc = _lib.lib.halo_route_lookup_device(g._t, ips.data_ptr(), 8, ips.data_ptr(), None)
     assert rc == _lib.HALO_E_INVAL  # not synced yet
     assert _lib.lib.halo_route_get(g._t, 5, ctypes.c_void_p(ips.data_ptr())) == _lib.HALO_E_RANGE
+
+
+def test_concurrent_sync_and_lookups(dev):
+    """Syncs on one thread, lookups on another stream and thread (a sync could rewrite
+    the generation a lookup had taken its view of but not yet launched on). Every launch must see
+    exactly one published table: all of its 64k addresses (inside 10.1.0.0/16) get the same id, the
+    /8's or the /16 route current at some sync."""
+    import threading
+
+    import torch
+
+    from halo_amd.route import RouteTable, ip_u
+
+    t = RouteTable(dev.index or 0)
+    base_id = t.AddRoute(t.entry(ip_u("10.0.0.0"), ip_u("255.0.0.0"), ip_u("192.168.1.1"), 1))
+    t.sync()
+    valid = {base_id}
+    lock = threading.Lock()
+    stop = threading.Event()
+    errors = []
+    n = 1 << 16
+    ips = torch.from_numpy((np.uint32(ip_u("10.1.0.0")) + np.arange(n, dtype=np.uint32)).view(np.int32)).to(dev)
+
+    def syncer():
+        try:
+            route = t.entry(ip_u("10.1.0.0"), ip_u("255.255.0.0"), ip_u("192.168.1.2"), 2)
+            for k in range(60):
+                if k % 2 == 0:
+                    rid = t.AddRoute(route)
+                    with lock:
+                        valid.add(rid)
+                else:
+                    t.DeleteRoute(route)  # leaves an emptied list: lookups there panic (ROUTE_PANIC)
+                t.sync()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+        finally:
+            stop.set()
+
+    def looker():
+        s = torch.cuda.Stream(device=dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        launches = 0
+        try:
+            while not stop.is_set() or launches < 5:
+                with torch.cuda.stream(s):
+                    t.FindRoute(ips, out=out, stream=s)
+                s.synchronize()
+                got = out.cpu().numpy().view(np.uint32)
+                launches += 1
+                u = np.unique(got)
+                with lock:
+                    ok = len(u) == 1 and (int(u[0]) in valid or int(u[0]) == 0xFFFFFFFE)
+                if not ok:
+                    errors.append(f"launch {launches}: ids {u[:8]}")
+                    return
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=syncer), threading.Thread(target=looker)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    t.close()
+    assert not errors, errors[:3]

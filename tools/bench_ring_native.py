@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(m: int = 1000, iters: int = 2000, warmup: int = 50, small_poll=None, register_out: bool = True) -> dict:
+def run(m: int = 1000, iters: int = 2000, warmup: int = 50, small_poll=None, register_out: bool = True,
+        persistent: bool = False) -> dict:
     import ctypes
 
     import numpy as np
@@ -37,7 +38,8 @@ def run(m: int = 1000, iters: int = 2000, warmup: int = 50, small_poll=None, reg
     offs = fr["layout"]["offsets_dw"].astype(np.uint64) * 4
     lens = np.ascontiguousarray(fr["layout"]["lens"])
     ring = RingBuffer(8 << 20)
-    cons = RingConsumer(ring, capacity=1514, max_frames=4096, register=True, small_poll=small_poll)
+    cons = RingConsumer(ring, capacity=1514, max_frames=4096, register=True, small_poll=small_poll,
+                        persistent=persistent)
     out = cons._out if register_out else np.zeros(cons.max_frames, _lib.RESULT_DTYPE)
     us = np.zeros(iters, np.float64)
     bad = ctypes.c_uint32()
@@ -47,7 +49,7 @@ def run(m: int = 1000, iters: int = 2000, warmup: int = 50, small_poll=None, reg
                                  ctypes.byref(bad))
     _lib.check("halo_bench_ring_polls", rc)
     cons.close()
-    return {"frames": m, "iters": iters, "bad_batches": int(bad.value), "us_median": round(float(np.median(us)), 2),
+    return {"frames": m, "persistent": persistent, "iters": iters, "bad_batches": int(bad.value), "us_median": round(float(np.median(us)), 2),
             "us_p10": round(float(np.percentile(us, 10)), 2), "us_p90": round(float(np.percentile(us, 90)), 2),
             "mpps": round(m / float(np.median(us)), 3)}
 
@@ -57,9 +59,11 @@ if __name__ == "__main__":
     p.add_argument("--frames", type=int, default=1000)
     p.add_argument("--iters", type=int, default=2000)
     p.add_argument("--sweep", action="store_true")
+    p.add_argument("--persistent", action="store_true")
     a = p.parse_args()
     if a.sweep:
-        for m in (1, 64, 256, 1000, 4000):
-            print(json.dumps(run(m, a.iters)), flush=True)
+        for persistent in (False, True):
+            for m in (1, 64, 256, 1000, 4000, 16000):
+                print(json.dumps(run(m, a.iters, persistent=persistent)), flush=True)
     else:
-        print(json.dumps(run(a.frames, a.iters)), flush=True)
+        print(json.dumps(run(a.frames, a.iters, persistent=a.persistent)), flush=True)

@@ -43,10 +43,9 @@ for s in "$@"; do
     gpus2) step gpus2 600 python bench.py --gpus 2 --steps 50 --warmup 5 --no-secondary --no-cpu ;;
     tunes) step tune_stream 600 python tools/tune.py --spec imix:-2,570B:-2,128B:-2,1500B:8 ;;
     ringn) step ring_native 600 python tools/bench_ring_native.py --sweep ;;
-    ringprof) step ring_prof 600 rocprofv3 --kernel-trace --hip-runtime-trace --stats --output-format csv -d "$OUT/ringprof" -o run -- python3 tools/bench_ring_native.py --iters 500 ;;
+    ringprof) step ring_prof 600 rocprofv3 --kernel-trace --hip-runtime-trace --stats --output-format csv -d "$OUT/ringprof" -o run -- python3 tools/bench_ring_native.py --iters 500 ${RP_ARGS:-} ;;
     tunev) step tune_variants 600 python tools/tune.py --only 570B,1500B,jumbo9000,imix --variants 4,8,16,-3,-2,-1 ;;
     abold) step ab_old_new 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,570B:4,jumbo9000:16,imix:-1,64B:1" old new ;;
-    ab1r) step ab_one_round 600 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:-3,570B:-3" new new_w4 ;;
     abtx) step ab_tx 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_tx.py && python tools/exp/bench_tx_build.py" old new ;;
     ttxall) step pytest_txall 600 python -u -m pytest tests/test_gpu_tx.py tests/test_gpu_tx_build.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
