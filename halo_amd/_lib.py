@@ -111,6 +111,9 @@ ROUTE_NONE, ROUTE_PANIC = 0xFFFFFFFF, 0xFFFFFFFE  # HALO_ROUTE_*
 RING_SCAN_DTYPE = np.dtype([("n_frames", "<u4"), ("stop", "<u4"), ("end_bytes", "<u8"), ("max_len", "<u4"),
                             ("pad", "<u4")])
 assert RING_SCAN_DTYPE.itemsize == 24
+# halo_rx_ring_stats_t (8 x u64)
+RING_STATS_DTYPE = np.dtype([(k, "<u8") for k in ("polls", "frames", "small_polls", "service_requests",
+                                                  "service_launches", "walk_ns", "wait_ns", "service_gpu_ns")])
 RING_STOP_NAMES = ("EMPTY", "BAD_LEN", "PARTIAL", "CAPACITY", "MAX", "BAD_CURSOR")
 RING_STOP = {name: code for code, name in enumerate(RING_STOP_NAMES)}
 RING_REGISTER = 0x1
@@ -264,6 +267,7 @@ _PROTOS = {
     "halo_rx_ring_poll": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(NetIf), _u8p, _u8p, _u8p, _u8p]),
     "halo_rx_ring_commit": (ctypes.c_int, [ctypes.c_void_p]),
+    "halo_rx_ring_get_stats": (ctypes.c_int, [ctypes.c_void_p, _u8p]),
     "halo_rx_ring_set_small_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "halo_rx_ring_scan_workspace": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32]),
     "halo_rx_ring_scan_device": (ctypes.c_int, [

@@ -68,6 +68,8 @@ struct RingServiceCtl {
     uint32_t alive;     // device: 1 while the kernel runs (diagnostics)
     uint32_t n, flags, mac_lo, mac_hi, own_ip, pad;
     uint64_t out;       // device address of the request's records
+    uint64_t t_seen;    // device: real-time counter (100 MHz) when it took the request
+    uint64_t t_done;    // device: ... when it published the records
 };
 // Launches the consumer on `s`: it serves requests after `last`, and exits when `stop` is set or
 // after idle_us microseconds without a request.

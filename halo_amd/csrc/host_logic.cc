@@ -47,8 +47,12 @@ RingWalk ring_walk(const uint8_t* data, uint64_t size, uint64_t cursor, uint64_t
     for (;;) {
         if (used - a < 4) { w.stop = HALO_RING_STOP_EMPTY; break; }
         const uint64_t p = (cursor + a) & mask;
-        uint32_t len = 0;  // the length field, byte by byte modulo the size: never past the data area
-        for (int k = 3; k >= 0; --k) len = (len << 8) | data[(p + (uint64_t)k) & mask];
+        uint32_t len = 0;  // the length field; never read past the data area (a 4-aligned field fits)
+        if (!(p & 3u)) {
+            memcpy(&len, data + p, 4);
+        } else {
+            for (int k = 3; k >= 0; --k) len = (len << 8) | data[(p + (uint64_t)k) & mask];
+        }
         if (len == 0 || len > half) { w.stop = HALO_RING_STOP_BAD_LEN; break; }
         const uint64_t bytes = (4ull + len + 3ull) & ~3ull;
         if (used - a < bytes) { w.stop = HALO_RING_STOP_PARTIAL; break; }

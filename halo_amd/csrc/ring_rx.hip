@@ -527,6 +527,7 @@ struct halo_rx_ring {
     uint32_t svc_seq = 0;                   // the last request made
     bool svc_launched = false;
     std::chrono::steady_clock::time_point svc_last{};  // when the last request completed
+    halo_rx_ring_stats_t stats{};
 };
 
 namespace {
@@ -625,6 +626,7 @@ int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_n
     auto launch = [&](uint32_t last) {
         r->svc_launched = halo::launch_ring_service(r->d_svc, r->d_data, r->d_soff, r->d_slen, last, kSvcIdleUs,
                                                     r->s_svc) == HALO_OK;
+        r->stats.service_launches += r->svc_launched;
         return r->svc_launched;
     };
     const uint32_t seq = r->svc_seq + 1;
@@ -651,6 +653,8 @@ int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_n
         }
     }
     r->svc_last = clk::now();
+    ++r->stats.service_requests;
+    r->stats.service_gpu_ns += (c->t_done - c->t_seen) * 10u;  // 100 MHz ticks
     return HALO_OK;
 }
 
@@ -666,9 +670,14 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
                halo_rx_result_t* out, uint32_t* status_hist, uint64_t* positions, halo_rx_ring_scan_t* info) {
     // every record is >= 8 bytes and used <= small, so at most small_frames frames fit: the bound
     // below never cuts a walk, it only keeps the pinned arrays' size in the contract
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     const halo::RingWalk w = halo::ring_walk(r->data, r->size, r->cursor, used, r->cap,
                                              std::min(r->max_frames, r->small_frames), r->h_soff, r->h_slen, positions);
+    const auto t1 = clk::now();
     if (w.wraps) return 1;
+    r->stats.walk_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    ++r->stats.small_polls;
     const uint32_t n = w.n, max_len = w.max_len;
     if (n) {
         const uint64_t rb = sizeof(halo_rx_result_t) * (uint64_t)n;
@@ -690,6 +699,7 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
                                             dout ? dout : r->d_sres, nullptr, r->s_comp);
             if (!rc && hipStreamSynchronize(r->s_comp) != hipSuccess) rc = HALO_E_HIP;
         }
+        r->stats.wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t1).count();
         if (rc) return rc;
         if (!dout) memcpy(out, r->h_sres, rb);
         if (status_hist)
@@ -700,6 +710,8 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
     info->end_bytes = w.end_bytes;
     info->max_len = max_len;
     r->cursor += w.end_bytes;
+    r->stats.polls += n != 0;
+    r->stats.frames += n;
     return HALO_OK;
 }
 }  // namespace
@@ -931,6 +943,14 @@ extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, con
     info->n_frames = done;
     info->end_bytes = off;
     r->cursor += off;
+    r->stats.polls += done != 0;
+    r->stats.frames += done;
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_ring_get_stats(const halo_rx_ring_t* r, halo_rx_ring_stats_t* out) {
+    if (!r || !out) return HALO_E_INVAL;
+    *out = r->stats;
     return HALO_OK;
 }
 

@@ -646,6 +646,7 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
             s_cmd[0] = seq;
             s_cmd[1] = quit;
             if (!quit) {
+                ctl->t_seen = __builtin_amdgcn_s_memrealtime();
                 s_cmd[2] = ctl->n;
                 s_cmd[3] = ctl->flags;
                 s_cmd[4] = ctl->mac_lo;
@@ -670,6 +671,7 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
         for (uint32_t base = w * 64; base < p.n; base += kSvcWaves * 64) lane_window<0, 0>(p, base, lane, s_rec[w], hist);
         __syncthreads();  // every record of the request stored
         if (threadIdx.x == 0) {
+            ctl->t_done = __builtin_amdgcn_s_memrealtime();
             __threadfence_system();
             __hip_atomic_store(&ctl->done_seq, s_cmd[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             last = s_cmd[0];

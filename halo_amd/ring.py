@@ -21,7 +21,8 @@ from typing import Optional
 import numpy as np
 
 from . import _lib
-from ._lib import RESULT_DTYPE, RING_HEADER, RING_PERSISTENT, RING_REGISTER, RING_SCAN_DTYPE, RING_STOP_NAMES, NetIf
+from ._lib import (RESULT_DTYPE, RING_HEADER, RING_PERSISTENT, RING_REGISTER, RING_SCAN_DTYPE, RING_STATS_DTYPE,
+                   RING_STOP_NAMES, NetIf)
 from .protocol import flags_word
 
 WIRE_MAX_PACKET_SIZE = 1514  # engine/engine.go:507
@@ -143,6 +144,12 @@ class RingConsumer:
 
     def commit(self):
         _lib.check("halo_rx_ring_commit", _lib.lib.halo_rx_ring_commit(self._h))
+
+    def stats(self) -> dict:
+        """halo_rx_ring_get_stats: poll counters and where the small polls' time went."""
+        st = np.zeros(1, RING_STATS_DTYPE)
+        _lib.check("halo_rx_ring_get_stats", _lib.lib.halo_rx_ring_get_stats(self._h, st.ctypes.data))
+        return {k: int(st[k][0]) for k in RING_STATS_DTYPE.names}
 
 
 class Wire:

@@ -342,6 +342,20 @@ HALO_API int halo_rx_ring_poll(halo_rx_ring_t* ring, uint32_t flags, const halo_
 HALO_API int halo_rx_ring_set_small_poll(halo_rx_ring_t* ring, uint64_t bytes);
 /* Release everything polled so far to the producer: tail = cursor (store-release). */
 HALO_API int halo_rx_ring_commit(halo_rx_ring_t* ring);
+/* Counters of a consumer since attach (observability; cheap enough to keep on): where a poll's
+ * time goes. Times are host steady-clock ns, except service_gpu_ns (the resident consumer's own
+ * real-time counter, from seeing a request to publishing its records). */
+typedef struct halo_rx_ring_stats {
+    uint64_t polls;            /* halo_rx_ring_poll calls that found records                      */
+    uint64_t frames;           /* frames returned                                                  */
+    uint64_t small_polls;      /* polls on the small path (one launch, or a service request)      */
+    uint64_t service_requests; /* small polls served by the resident consumer (HALO_RING_PERSISTENT) */
+    uint64_t service_launches; /* resident consumer launches (first use, after idle exits)       */
+    uint64_t walk_ns;          /* small polls: the host's ReadPacket walk of the length fields    */
+    uint64_t wait_ns;          /* small polls: launch + synchronisation, or request to completion */
+    uint64_t service_gpu_ns;   /* resident consumer: GPU time per request, summed                 */
+} halo_rx_ring_stats_t;
+HALO_API int halo_rx_ring_get_stats(const halo_rx_ring_t* ring, halo_rx_ring_stats_t* out);
 
 /* The record walk alone, device-resident: `used` bytes of ring data in stream order at d_span
  * (4-byte aligned; used a multiple of 4, <= ring_size), ring_size = RingBuffer.size. Writes
