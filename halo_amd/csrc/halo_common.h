@@ -2,6 +2,7 @@
 // libhalo_rx.so. Device code is written for gfx950 (CDNA4) only.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "halo_limits.h"
@@ -57,20 +58,44 @@ enum SynthSlot : uint32_t {
 int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 
 // The resident small-poll consumer of a ring attached with HALO_RING_PERSISTENT (ring_rx.hip
-// drives it, rx_parse.hip runs it): one workgroup that waits on this control block, in pinned
-// host memory, for a request, parses its n frames as the lane kernel would (frames at
-// data + 4 * off_dw[i], the host's ReadPacket walk wrote off_dw / lens into pinned memory) and
-// writes their records to `out`, then publishes done_seq. The host never launches per poll.
-struct RingServiceCtl {
-    uint32_t req_seq;   // host: the request number (store-release after every field below)
-    uint32_t done_seq;  // device: req_seq once that request's records are visible (system scope)
-    uint32_t stop;      // host: 1 = exit now
-    uint32_t alive;     // device: 1 while the kernel runs (diagnostics)
-    uint32_t n, flags, mac_lo, mac_hi, own_ip, pad;
-    uint64_t out;       // device address of the request's records
-    uint64_t t_seen;    // device: real-time counter (100 MHz) when it took the request
-    uint64_t t_done;    // device: ... when it published the records
+// drives it, rx_parse.hip runs it): kSvcGroups workgroups that wait on this control block, in
+// pinned host memory, for a request, parse its n frames as the lane kernel would (frames at
+// data + 4 * off_dw[i], the host's ReadPacket walk wrote off_dw / lens into pinned memory; 64-frame
+// windows dealt round-robin over the groups) and write their records to `out`; each group then
+// publishes its done_seq slot. The host never launches per poll.
+#ifndef HALO_SVC_GROUPS
+#define HALO_SVC_GROUPS 16  // workgroups of the resident consumer (each on its own CU)
+#endif
+#ifndef HALO_SVC_WAVES
+#define HALO_SVC_WAVES 4    // waves per workgroup (64 frames each per pass)
+#endif
+constexpr uint32_t kSvcGroups = HALO_SVC_GROUPS;
+constexpr uint32_t kSvcWaves = HALO_SVC_WAVES;
+struct alignas(64) RingServiceCtl {
+    // The request: one 64-byte line. The host writes the fields, then `check` (svc_check of words
+    // 0..7), then req_seq with release. Each workgroup reads the whole line with one 16-lane load
+    // and takes a request whose req_seq is new and whose check matches (a torn read is re-read).
+    uint32_t req_seq;        // host: the request number
+    uint32_t n, flags, mac_lo, mac_hi, own_ip;
+    uint32_t out_lo, out_hi; // device address of the request's records
+    uint32_t stop;           // host: 1 = exit now
+    uint32_t check;
+    uint32_t pad0[6];
+    // Completion: one slot per workgroup, each written by its group after its records are visible
+    // (system-scope release)
+    uint32_t done_seq[kSvcGroups];
+    uint32_t alive[kSvcGroups];   // 1 while the group runs (diagnostics)
+    uint64_t t_seen[kSvcGroups];  // real-time counter (100 MHz) when the group took the request
+    uint64_t t_done[kSvcGroups];  // ... when it published its records
 };
+static_assert(offsetof(RingServiceCtl, done_seq) == 64, "request line");
+__host__ __device__ inline uint32_t svc_check(uint32_t seq, uint32_t n, uint32_t flags, uint32_t mac_lo, uint32_t mac_hi,
+                                              uint32_t own_ip, uint32_t out_lo, uint32_t out_hi) {
+    const uint32_t w[8] = {seq, n, flags, mac_lo, mac_hi, own_ip, out_lo, out_hi};
+    uint32_t h = 0x811C9DC5u;
+    for (int i = 0; i < 8; ++i) h = (h ^ w[i]) * 0x01000193u;
+    return h;
+}
 // Launches the consumer on `s`: it serves requests after `last`, and exits when `stop` is set or
 // after idle_us microseconds without a request.
 int launch_ring_service(RingServiceCtl* d_ctl, const uint8_t* d_data, const uint32_t* d_off,

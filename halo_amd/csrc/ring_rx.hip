@@ -609,27 +609,32 @@ constexpr uint32_t kSvcMaxFrames = 16384;  // larger small polls take a full-gri
 constexpr uint32_t kSvcIdleUs = 20000;      // the resident consumer exits after 20 ms without a request
 
 // One request to the resident consumer: the frames' offsets / lengths are already in the pinned
-// arrays it reads (d_soff / d_slen). Fields first, then req_seq with release; spin on done_seq. A
+// arrays it reads (d_soff / d_slen). Fields and their check first, then req_seq with release; spin
+// until every group's done_seq slot holds it. A
 // consumer that went idle (or exited between its last check and the request) is relaunched: the
 // stream says whether its kernel is still running. Every wait is bounded.
 int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
                     halo_rx_result_t* dout) {
     using clk = std::chrono::steady_clock;
     halo::RingServiceCtl* c = r->svc;
+    const uint32_t seq = r->svc_seq + 1;
+    const uint64_t out = reinterpret_cast<uint64_t>(dout);
     c->n = n;
     c->flags = flags;
     c->mac_lo = (uint32_t)netif->mac[0] | ((uint32_t)netif->mac[1] << 8) | ((uint32_t)netif->mac[2] << 16) |
                 ((uint32_t)netif->mac[3] << 24);
     c->mac_hi = (uint32_t)netif->mac[4] | ((uint32_t)netif->mac[5] << 8);
     c->own_ip = netif->ip;
-    c->out = reinterpret_cast<uint64_t>(dout);
+    c->out_lo = (uint32_t)out;
+    c->out_hi = (uint32_t)(out >> 32);
+    __atomic_store_n(&c->check, halo::svc_check(seq, n, flags, c->mac_lo, c->mac_hi, c->own_ip, c->out_lo, c->out_hi),
+                     __ATOMIC_RELEASE);
     auto launch = [&](uint32_t last) {
         r->svc_launched = halo::launch_ring_service(r->d_svc, r->d_data, r->d_soff, r->d_slen, last, kSvcIdleUs,
                                                     r->s_svc) == HALO_OK;
         r->stats.service_launches += r->svc_launched;
         return r->svc_launched;
     };
-    const uint32_t seq = r->svc_seq + 1;
     // idle past half the timeout: the kernel may have exited; ask the stream (cheap, rare)
     if (!r->svc_launched ||
         (clk::now() - r->svc_last > std::chrono::microseconds(kSvcIdleUs / 2) && hipStreamQuery(r->s_svc) == hipSuccess)) {
@@ -640,7 +645,9 @@ int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_n
     const auto t0 = clk::now();
     auto t_check = t0;
     for (uint32_t k = 1;; ++k) {
-        if (__atomic_load_n(&c->done_seq, __ATOMIC_ACQUIRE) == seq) break;
+        uint32_t done = 0;
+        for (uint32_t g = 0; g < halo::kSvcGroups; ++g) done += __atomic_load_n(&c->done_seq[g], __ATOMIC_ACQUIRE) == seq;
+        if (done == halo::kSvcGroups) break;
         __builtin_ia32_pause();
         if ((k & 255u) == 0) {
             const auto now = clk::now();
@@ -654,7 +661,12 @@ int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_n
     }
     r->svc_last = clk::now();
     ++r->stats.service_requests;
-    r->stats.service_gpu_ns += (c->t_done - c->t_seen) * 10u;  // 100 MHz ticks
+    uint64_t seen = c->t_seen[0], fin = c->t_done[0];
+    for (uint32_t g = 1; g < halo::kSvcGroups; ++g) {
+        seen = std::min(seen, c->t_seen[g]);
+        fin = std::max(fin, c->t_done[g]);
+    }
+    r->stats.service_gpu_ns += (fin - seen) * 10u;  // 100 MHz ticks: first group in to last group out
     return HALO_OK;
 }
 

@@ -613,47 +613,59 @@ rx_lane_kernel(const RxParams p) {
     flush_hist(p, hist);
 }
 
-// The resident small-poll consumer (RingServiceCtl, halo_common.h). Thread 0 waits for a request
-// — a system-scope acquire load of req_seq in pinned host memory, s_sleep between tries, bounded by
-// the stop flag and an idle timeout on the 100 MHz real-time counter, so every wave reaches the
-// exit — and copies it into LDS; the 16 waves then parse its frames 64 at a time with the lane
-// kernel's window code; after a block barrier thread 0 fences and publishes done_seq.
-constexpr uint32_t kSvcWaves = 16;
+// The resident small-poll consumer (RingServiceCtl, halo_common.h), kSvcGroups workgroups of
+// kSvcWaves waves. In each group wave 0 waits for a request: all its lanes load the request line
+// (one 64-byte read of pinned host memory, system scope), s_sleep between tries, bounded by the
+// stop flag and an idle timeout on the 100 MHz real-time counter, so every wave reaches the exit.
+// A new req_seq whose check matches the fields of the same read is taken (the fields arrive with
+// the sequence number: no second round trip); an acquire fence, then the group's waves parse their
+// 64-frame windows (window k goes to group k % kSvcGroups, spreading a 1k-frame request over 16
+// CUs' memory pipelines) with the lane kernel's window code; after a block barrier thread 0 fences
+// and publishes the group's done_seq slot.
 __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServiceCtl* ctl, const uint8_t* data,
                                                                       const uint32_t* off, const uint16_t* len,
                                                                       uint32_t last, uint64_t idle_ticks) {
-    __shared__ uint32_t s_cmd[8];  // seq, exit, n, flags, mac_lo, mac_hi, own_ip
-    __shared__ uint64_t s_out;
+    __shared__ uint32_t s_cmd[10];  // seq, exit, n, flags, mac_lo, mac_hi, own_ip, out_lo, out_hi
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     __shared__ uint4 s_rec[kSvcWaves][128];
-    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, g = blockIdx.x;
+    uint32_t* line = reinterpret_cast<uint32_t*>(ctl);
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) __hip_atomic_store(&ctl->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(&ctl->alive[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        if (threadIdx.x == 0) {
-            uint32_t seq = last, quit = 0;
+        if (w == 0) {
+            uint32_t v, seq, quit = 0;
             for (;;) {
-                seq = __hip_atomic_load(&ctl->req_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (seq != last) break;
-                if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                    __builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
+                v = __hip_atomic_load(&line[lane & 15u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                seq = __builtin_amdgcn_readlane(v, 0);
+                if (seq != last) {
+                    const uint32_t ck = svc_check(seq, __builtin_amdgcn_readlane(v, 1), __builtin_amdgcn_readlane(v, 2),
+                                                  __builtin_amdgcn_readlane(v, 3), __builtin_amdgcn_readlane(v, 4),
+                                                  __builtin_amdgcn_readlane(v, 5), __builtin_amdgcn_readlane(v, 6),
+                                                  __builtin_amdgcn_readlane(v, 7));
+                    if (ck == __builtin_amdgcn_readlane(v, 9)) break;
+                }
+                if (__builtin_amdgcn_readlane(v, 8) || __builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
                     quit = 1;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            s_cmd[0] = seq;
-            s_cmd[1] = quit;
-            if (!quit) {
-                ctl->t_seen = __builtin_amdgcn_s_memrealtime();
-                s_cmd[2] = ctl->n;
-                s_cmd[3] = ctl->flags;
-                s_cmd[4] = ctl->mac_lo;
-                s_cmd[5] = ctl->mac_hi;
-                s_cmd[6] = ctl->own_ip;
-                s_out = ctl->out;
+            if (lane == 0) {
+                s_cmd[0] = seq;
+                s_cmd[1] = quit;
+                s_cmd[2] = __builtin_amdgcn_readlane(v, 1);
+                s_cmd[3] = __builtin_amdgcn_readlane(v, 2);
+                s_cmd[4] = __builtin_amdgcn_readlane(v, 3);
+                s_cmd[5] = __builtin_amdgcn_readlane(v, 4);
+                s_cmd[6] = __builtin_amdgcn_readlane(v, 5);
+                s_cmd[7] = __builtin_amdgcn_readlane(v, 6);
+                s_cmd[8] = __builtin_amdgcn_readlane(v, 7);
+                if (!quit) ctl->t_seen[g] = __builtin_amdgcn_s_memrealtime();
             }
+            // the request's off / len / frames are read after the request was seen
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         }
         __syncthreads();
         if (s_cmd[1]) break;
@@ -666,20 +678,21 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
         p.mac_lo = s_cmd[4];
         p.mac_hi = s_cmd[5];
         p.own_ip = s_cmd[6];
-        p.out = reinterpret_cast<halo_rx_result_t*>(s_out);
+        p.out = reinterpret_cast<halo_rx_result_t*>((uint64_t)s_cmd[7] | ((uint64_t)s_cmd[8] << 32));
         Hist hist{s_hist, 0};
-        for (uint32_t base = w * 64; base < p.n; base += kSvcWaves * 64) lane_window<0, 0>(p, base, lane, s_rec[w], hist);
-        __syncthreads();  // every record of the request stored
+        for (uint32_t base = (w * kSvcGroups + g) * 64; base < p.n; base += kSvcGroups * kSvcWaves * 64)
+            lane_window<0, 0>(p, base, lane, s_rec[w], hist);
+        __syncthreads();  // every record of this group stored
         if (threadIdx.x == 0) {
-            ctl->t_done = __builtin_amdgcn_s_memrealtime();
+            ctl->t_done[g] = __builtin_amdgcn_s_memrealtime();
             __threadfence_system();
-            __hip_atomic_store(&ctl->done_seq, s_cmd[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            last = s_cmd[0];
-            t_idle = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_store(&ctl->done_seq[g], s_cmd[0], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        last = s_cmd[0];
+        t_idle = __builtin_amdgcn_s_memrealtime();
         __syncthreads();  // s_cmd is rewritten by the next wait
     }
-    if (threadIdx.x == 0) __hip_atomic_store(&ctl->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(&ctl->alive[g], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // G lanes per frame (G in {4, 8, 16}); VGPR-limited occupancy, so no SGPR cap.
@@ -1411,7 +1424,7 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
 namespace halo {
 int launch_ring_service(RingServiceCtl* d_ctl, const uint8_t* d_data, const uint32_t* d_off, const uint16_t* d_len,
                         uint32_t last, uint32_t idle_us, hipStream_t s) {
-    hipLaunchKernelGGL(ring_service_kernel, dim3(1), dim3(64 * kSvcWaves), 0, s, d_ctl, d_data, d_off, d_len, last,
+    hipLaunchKernelGGL(ring_service_kernel, dim3(kSvcGroups), dim3(64 * kSvcWaves), 0, s, d_ctl, d_data, d_off, d_len, last,
                        (uint64_t)idle_us * 100u);  // s_memrealtime: 100 MHz
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }

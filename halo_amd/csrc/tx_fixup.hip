@@ -39,6 +39,13 @@ struct TxParams {
 constexpr uint32_t kGoSteps = HALO_TX_NAT_DST | HALO_TX_TTL | HALO_TX_NAT_SRC | HALO_TX_RECALC;
 constexpr uint32_t kHdrDw = 13;  // header dwords 0..12 (frame bytes 0..51: up to the TCP checksum)
 
+#ifndef HALO_TX_NT_STORE
+#define HALO_TX_NT_STORE 0
+#endif
+#ifndef HALO_TX_G1_STORE
+#define HALO_TX_G1_STORE 0
+#endif
+
 // byte b of the header copy / a big-endian 16-bit field at even frame offset b
 #define MB(b) ((m[(b) >> 2] >> (((b)&3) * 8)) & 0xFFu)
 #define SET_BE16(b, v)                                                                              \
@@ -345,14 +352,30 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
         __attribute__((address_space(1))) uint32_t* fw =
             (__attribute__((address_space(1))) uint32_t*)reinterpret_cast<uint32_t*>(frame);
         uint32_t rest = dirty;
-        if ((dirty & 0x0F0u) && L >= 32) {
-            *(__attribute__((address_space(1))) u32x4*)(fw + 4) = (u32x4){m[4], m[5], m[6], m[7]};
+#if HALO_TX_NT_STORE
+#define TX_ST4(d, a, b, c, e) __builtin_nontemporal_store(((u32x4){a, b, c, e}), (__attribute__((address_space(1))) u32x4*)(fw + (d)))
+#else
+#define TX_ST4(d, a, b, c, e) (*(__attribute__((address_space(1))) u32x4*)(fw + (d)) = (u32x4){a, b, c, e})
+#endif
+#if HALO_TX_G1_STORE == 1
+        if (G == 1 && dirty && L >= 64) {
+            // whole first 64 bytes (clean dwords with their own values): full-line writes
+            TX_ST4(0, buf[0][0], buf[0][1], buf[0][2], m[3]);
+            TX_ST4(4, m[4], m[5], m[6], m[7]);
+            TX_ST4(8, m[8], m[9], m[10], m[11]);
+            TX_ST4(12, m[12], buf[3][1], buf[3][2], buf[3][3]);
+            rest = 0;
+        }
+#endif
+        if ((rest & 0x0F0u) && L >= 32) {
+            TX_ST4(4, m[4], m[5], m[6], m[7]);
             rest &= ~0x0F0u;
         }
-        if ((dirty & 0xF00u) && L >= 48) {
-            *(__attribute__((address_space(1))) u32x4*)(fw + 8) = (u32x4){m[8], m[9], m[10], m[11]};
+        if ((rest & 0xF00u) && L >= 48) {
+            TX_ST4(8, m[8], m[9], m[10], m[11]);
             rest &= ~0xF00u;
         }
+#undef TX_ST4
 #pragma unroll
         for (uint32_t d = 3; d < kHdrDw; ++d) {
             if (rest & (1u << d)) {

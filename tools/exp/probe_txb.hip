@@ -83,6 +83,61 @@ __global__ void __launch_bounds__(256) big_frames(const uint8_t* pay, uint8_t* f
     }
 }
 
+
+// lane per 64 B frame as the kernel's build_small loads its payload: NLD clamped dword loads
+// (sources 7..16 or 10..16 of the frame in payload space) instead of one 16 B + one 4 B load
+template <int NLD>
+__global__ void __launch_bounds__(256) small_dwords(const uint2* desc, const uint8_t* pay, uint8_t* frames, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t x = i;
+    const uint2* d = desc + 5ull * i;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { const uint2 v = d[k]; x ^= v.x + v.y; }
+    const uint64_t a = (uint64_t)pay + 22ull * i, lo = a & ~3ull;
+    const int32_t last = (int32_t)(((a + 22 + 3) & ~3ull) - lo) / 4 - 1;
+    const int32_t r0 = -11 + (int32_t)(x & 1u);
+    uint32_t w[10];
+#pragma unroll
+    for (int m = 0; m < NLD; ++m) {
+        const int32_t r = r0 + (10 - NLD) + 7 + m;
+        w[m] = ((gu32*)lo)[r < 0 ? 0 : r > last ? last : r];
+    }
+#pragma unroll
+    for (int m = NLD; m < 10; ++m) w[m] = x;
+    uint4* o = reinterpret_cast<uint4*>(frames + 64ull * i);
+    o[0] = make_uint4(w[0], w[1], x, w[2]);
+    o[1] = make_uint4(w[3], w[5], w[4], w[1]);
+    o[2] = make_uint4(w[2], w[6], w[7], w[3]);
+    o[3] = make_uint4(w[8], w[4], w[9], w[0]);
+}
+
+// four lanes per 64 B frame: the tile's descriptors read coalesced (16 B per lane), each lane one
+// 16 B payload load and one 16 B store of its chunk (a store instruction covers 16 whole frames)
+__global__ void __launch_bounds__(256) quad_frames(const uint4* desc, const uint8_t* pay, uint8_t* frames, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t t = wave; t * 64 < n; t += nw) {
+        // 64 descriptors = 2560 B = 160 x 16 B
+        uint32_t x = 0;
+        const uint4* dt = desc + (uint64_t)t * 160;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t q = lane + 64 * k;
+            if (q < 160) { const uint4 v = dt[q]; x ^= v.x + v.y + v.z + v.w; }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t f = t * 64 + s * 16 + lane / 4, j = lane & 3u;
+            if (f >= n) continue;
+            const uint64_t a = ((uint64_t)pay + 22ull * f + 16 * j) & ~3ull;
+            uint32_t w0 = x, w1 = x, w2 = x, w3 = x;
+            if (j >= 2) { const u32x4 v = *(gv4*)a; w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w; }
+            *reinterpret_cast<uint4*>(frames + 64ull * f + 16 * j) = make_uint4(w0, w1 ^ x, w2, w3);
+        }
+    }
+}
+
 template <typename F>
 static float time_it(F launch, int iters) {
     hipEvent_t a, b;
@@ -120,6 +175,16 @@ int main() {
     SMALL(false, false, true, "64B: frame out only");
     SMALL(true, false, false, "64B: desc in only");
     SMALL(false, true, false, "64B: payload in only");
+    {
+        float us = time_it([&] { hipLaunchKernelGGL(small_dwords<10>, grid, blk, 0, 0, desc, pay, frames, n); }, 50);
+        printf("%-34s %8.2f us\n", "64B: 10 dword payload loads", us);
+        us = time_it([&] { hipLaunchKernelGGL(small_dwords<7>, grid, blk, 0, 0, desc, pay, frames, n); }, 50);
+        printf("%-34s %8.2f us\n", "64B: 7 dword payload loads", us);
+        for (uint32_t gq : {1024u, 2048u, 4096u}) {
+            us = time_it([&] { hipLaunchKernelGGL(quad_frames, dim3(gq), blk, 0, 0, (const uint4*)desc, pay, frames, n); }, 50);
+            printf("64B quad lanes/frame, grid %-5u     %8.2f us\n", gq, us);
+        }
+    }
     const uint32_t nb = n / 4, flen = 1514, stride = 1516, pstride = 1472;
 #define BIG(G, CH, L, S, name)                                                                        \
     {                                                                                                 \

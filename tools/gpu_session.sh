@@ -48,6 +48,10 @@ for s in "$@"; do
     abold) step ab_old_new 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,570B:4,jumbo9000:16,imix:-1,64B:1" old new ;;
     abtx) step ab_tx 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_tx.py && python tools/exp/bench_tx_build.py" old new ;;
     ttxall) step pytest_txall 600 python -u -m pytest tests/test_gpu_tx.py tests/test_gpu_tx_build.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    abtxs) step ab_tx_store 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_tx.py" txa txfull txnt txfullnt ;;
+    kwrq)  step kwrq 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/kwrq" -o run -- python3 tools/exp/bench_tx.py ;;
+    ptxb)  step probe_txb 300 ./tools/exp/probe_txb ;;
+    tring) step pytest_ring 600 python -u -m pytest tests/test_gpu_ring.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
   esac
 done
