@@ -280,11 +280,11 @@ __device__ __forceinline__ uint32_t prefix_mask(int32_t n) {
 // layout, so sources 7..16 cover it), each address clamped into the payload's readable dwords —
 // a clamped value lands only in bytes the masks drop. Header bytes [0, hdr_end) from the lane's
 // header dwords, payload [hdr_end, pay_end), zero padding after; the L4 segment summed with one
-// v_dot2 per dword; four 16-byte stores (single dwords only for a frame that ends mid-chunk).
-__device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f, const uint32_t* hdr, uint8_t* out,
-                                            const void* safe) {
+// v_dot2 per dword. The caller stages o[] in LDS and the wave stores its frames cooperatively.
+__device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f, const uint32_t* hdr,
+                                            const void* safe, uint32_t (&o)[16]) {
     const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
-    const uint32_t H = f.hdr_end, PE = f.hdr_end + f.plen, ndw = (f.flen + 3u) >> 2;
+    const uint32_t H = f.hdr_end, PE = f.hdr_end + f.plen;
     const uint64_t sv = f.pay - H;  // virtual address of frame byte 0 in payload space
     const uint32_t sh = (uint32_t)(sv & 3u);
     typedef const __attribute__((address_space(1))) uint32_t gu32_t;
@@ -301,7 +301,6 @@ __device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f
         const int32_t r = r0 + 7 + m;
         src[m] = base[f.plen ? (r < 0 ? 0 : r > last ? last : r) : 0];
     }
-    uint32_t o[16];
 #pragma unroll
     for (int k = 0; k < 7; ++k) o[k] = hdr[k];  // bytes < 28 <= hdr_end: header only
 #pragma unroll
@@ -330,17 +329,6 @@ __device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f
     const uint32_t ck_dw = ck_at >> 2, ck_v = ck_le << ((ck_at & 2u) * 8u);
 #pragma unroll
     for (int k = 5; k < 13; ++k) o[k] |= (uint32_t)k == ck_dw ? ck_v : 0u;
-    uint32_t* ow = reinterpret_cast<uint32_t*>(out);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        if (4u * c + 4u <= ndw) {
-            *reinterpret_cast<uint4*>(ow + 4 * c) = make_uint4(o[4 * c], o[4 * c + 1], o[4 * c + 2], o[4 * c + 3]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (4u * c + i < ndw) ow[4 * c + i] = o[4 * c + i];
-        }
-    }
 }
 
 // BuildUdpPkt / BuildTcpPkt / BuildIcmpPkt's length limits and the slot check (build-defined):
@@ -381,7 +369,12 @@ tx_build_kernel(const BuildParams p) {
     constexpr uint32_t kMetaDw = (G > 1 || !HALO_TXB_G1_LDS_TRIM) ? kTile : 1;
     __shared__ uint32_t s_desc[kBlock / 64][kDescDw];  // per wave: its tile's descriptors
     __shared__ uint32_t s_meta[kBlock / 64][kMetaDw];
-    __shared__ uint32_t s_hdr[kBlock / 64][kTile * 16 + 1];  // per wave: frame-layout header dwords 0..15
+    // per wave: frame-layout header dwords 0..15 (G > 1); G = 1: a lane's header for a long frame,
+    // or its whole <= 64-byte frame staged for the wave's cooperative store (17-dword rows: the
+    // row-wise writes and the chunk-wise reads both spread over the banks)
+    constexpr uint32_t kRow = G == 1 ? 17 : 16;
+    __shared__ uint32_t s_hdr[kBlock / 64][kTile * kRow + 1];
+    __shared__ uint32_t s_ndw[kBlock / 64][G == 1 ? kTile : 1];  // G = 1: staged frame's dwords (0: none)
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t nw = (gridDim.x * kBlock) >> 6;
     const uint32_t base = *p.ip_id;
@@ -441,21 +434,48 @@ tx_build_kernel(const BuildParams p) {
             }
         }
         if constexpr (G == 1) {
-            // a frame of <= 64 B keeps its header in registers; longer ones read it from LDS
+            // a frame of <= 64 B is built in registers and staged in LDS; longer ones read their
+            // header from LDS and store as they build
+            uint32_t* row = &s_hdr[wv][kRow * lane];
+            uint32_t staged = 0;
             if (mine >> 31) {
                 const Frame f = decode(d, p.payload);
-                uint8_t* o = p.frames + (uint64_t)i * p.stride;
                 if (HALO_TXB_SMALL && f.flen <= 64u) {
-                    build_small(p, f, hv, o, p.desc + i);
+                    uint32_t o[16];
+                    build_small(p, f, hv, p.desc + i, o);
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) row[k] = o[k];
+                    staged = (f.flen + 3u) >> 2;
                 } else {
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) s_hdr[wv][16 * lane + k] = hv[k];
-                    build_frame<G, U>(p, f, &s_hdr[wv][16 * lane], 0, o);
+                    for (int k = 0; k < 16; ++k) row[k] = hv[k];
+                    build_frame<G, U>(p, f, row, 0, p.frames + (uint64_t)i * p.stride);
                 }
             }
+            s_ndw[wv][lane] = staged;
+            __builtin_amdgcn_wave_barrier();
+            // the staged frames, four lanes per frame: lane 4g + c stores chunk c of frame 16s + g,
+            // so one store instruction writes 16 frames' chunks side by side
+#pragma unroll
+            for (uint32_t st = 0; st < 4; ++st) {
+                const uint32_t fl = 16 * st + (lane >> 2), c = lane & 3u;
+                const uint32_t nd = s_ndw[wv][fl];
+                if (4 * c < nd) {
+                    const uint32_t* src = &s_hdr[wv][kRow * fl + 4 * c];
+                    uint32_t* o = reinterpret_cast<uint32_t*>(p.frames + (uint64_t)(first + fl) * p.stride) + 4 * c;
+                    if (4 * c + 4 <= nd) {
+                        *reinterpret_cast<uint4*>(o) = make_uint4(src[0], src[1], src[2], src[3]);
+                    } else {
+#pragma unroll
+                        for (uint32_t q = 0; q < 3; ++q)
+                            if (4 * c + q < nd) o[q] = src[q];
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the region is rewritten for the next tile
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) s_hdr[wv][16 * lane + k] = hv[k];
+            for (int k = 0; k < 16; ++k) s_hdr[wv][kRow * lane + k] = hv[k];
             // the wave's descriptors through its own LDS region (no block barrier), so that they
             // are not live in registers across the build steps
 #pragma unroll
@@ -470,7 +490,7 @@ tx_build_kernel(const BuildParams p) {
                     uint32_t dd[10];
 #pragma unroll
                     for (int k = 0; k < 10; ++k) dd[k] = s_desc[wv][10 * fl + k];
-                    build_frame<G, U>(p, decode(dd, p.payload), &s_hdr[wv][16 * fl], j,
+                    build_frame<G, U>(p, decode(dd, p.payload), &s_hdr[wv][kRow * fl], j,
                                       p.frames + (uint64_t)(first + fl) * p.stride);
                 }
             }

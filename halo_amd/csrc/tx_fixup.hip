@@ -39,12 +39,6 @@ struct TxParams {
 constexpr uint32_t kGoSteps = HALO_TX_NAT_DST | HALO_TX_TTL | HALO_TX_NAT_SRC | HALO_TX_RECALC;
 constexpr uint32_t kHdrDw = 13;  // header dwords 0..12 (frame bytes 0..51: up to the TCP checksum)
 
-#ifndef HALO_TX_NT_STORE
-#define HALO_TX_NT_STORE 0
-#endif
-#ifndef HALO_TX_G1_STORE
-#define HALO_TX_G1_STORE 0
-#endif
 
 // byte b of the header copy / a big-endian 16-bit field at even frame offset b
 #define MB(b) ((m[(b) >> 2] >> (((b)&3) * 8)) & 0xFFu)
@@ -344,29 +338,47 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
         set_l4(pl.dp_field, f);
     }
 
+    if constexpr (G >= 4) {
+        // lane gl owns header chunk gl (dwords 4gl..4gl+3; chunk 0 is never dirty): one 16-byte
+        // store per dirty chunk, so a store instruction covers 64 / G frames' chunks side by side
+        if (present) {
+            const uint32_t cd = gl >= 1 && gl <= 3 ? (dirty >> (4 * gl)) & 0xFu : 0u;
+            if (cd) {
+                uint32_t v[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    v[q] = gl == 1 ? m[4 + q] : gl == 2 ? m[8 + q] : (q == 0 ? m[12] : buf[0][q]);
+                uint32_t* fw = reinterpret_cast<uint32_t*>(frame) + 4 * gl;
+                if (16 * gl + 16 <= L) {
+                    *reinterpret_cast<uint4*>(fw) = make_uint4(v[0], v[1], v[2], v[3]);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t d = 4 * gl + q;
+                        if (!((cd >> q) & 1u)) continue;
+                        if (4 * d + 4 <= L) fw[q] = v[q];
+                        else
+                            for (uint32_t b = 4 * d; b < L; ++b) frame[b] = (uint8_t)(v[q] >> ((b & 3) * 8));
+                    }
+                }
+            }
+            if (gl == 0 && p.result) p.result[i] = (uint8_t)res;
+        }
+        return;
+    }
     if (present && gl == 0) {
         // dirty header dwords back to the frame: 16-byte stores for dwords 4..7 and 8..11 when
         // they lie inside the frame (fewer, wider store instructions; the clean dwords among
-        // them are rewritten with their own values), single dwords / bytes otherwise
+        // them are rewritten with their own values), single dwords / bytes otherwise. Each frame's
+        // stores land in one 64-byte HBM write request (TCC_EA0_WRREQ_64B: 1.016 per frame,
+        // profiles/r03/r3f/tx_fixup_write_requests.json), the floor for a frame with a dirty byte;
+        // writing the whole 64 bytes measured 33.4 -> 40.4 us and non-temporal stores neutral
+        // (profiles/r03/r3f/ab_tx_store.log)
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
         __attribute__((address_space(1))) uint32_t* fw =
             (__attribute__((address_space(1))) uint32_t*)reinterpret_cast<uint32_t*>(frame);
         uint32_t rest = dirty;
-#if HALO_TX_NT_STORE
-#define TX_ST4(d, a, b, c, e) __builtin_nontemporal_store(((u32x4){a, b, c, e}), (__attribute__((address_space(1))) u32x4*)(fw + (d)))
-#else
 #define TX_ST4(d, a, b, c, e) (*(__attribute__((address_space(1))) u32x4*)(fw + (d)) = (u32x4){a, b, c, e})
-#endif
-#if HALO_TX_G1_STORE == 1
-        if (G == 1 && dirty && L >= 64) {
-            // whole first 64 bytes (clean dwords with their own values): full-line writes
-            TX_ST4(0, buf[0][0], buf[0][1], buf[0][2], m[3]);
-            TX_ST4(4, m[4], m[5], m[6], m[7]);
-            TX_ST4(8, m[8], m[9], m[10], m[11]);
-            TX_ST4(12, m[12], buf[3][1], buf[3][2], buf[3][3]);
-            rest = 0;
-        }
-#endif
         if ((rest & 0x0F0u) && L >= 32) {
             TX_ST4(4, m[4], m[5], m[6], m[7]);
             rest &= ~0x0F0u;
@@ -445,7 +457,10 @@ extern "C" HALO_API int halo_tx_fixup_batch_device(uint8_t* d_bytes, const uint3
     const dim3 block(256), block1(HALO_TX_G1_BLOCK);
     // lanes per frame from the longest frame (0: unknown -> widest); any G handles any length
     const uint32_t h = max_len_hint ? max_len_hint : 65535u;
-    if (h <= 128) hipLaunchKernelGGL(halo::tx_fixup_kernel<1>, dim3(halo::tx_grid(n, 64, HALO_TX_G1_BLOCK / 64)), block1, HALO_TX_G1_LDS_PAD, s, p);
+#ifndef HALO_TX_G1_MAX
+#define HALO_TX_G1_MAX 128
+#endif
+    if (h <= HALO_TX_G1_MAX) hipLaunchKernelGGL(halo::tx_fixup_kernel<1>, dim3(halo::tx_grid(n, 64, HALO_TX_G1_BLOCK / 64)), block1, HALO_TX_G1_LDS_PAD, s, p);
     else if (h <= 1024) hipLaunchKernelGGL(halo::tx_fixup_kernel<4>, dim3(halo::tx_grid(n, 16, 4)), block, 0, s, p);
     else if (h <= 4096) hipLaunchKernelGGL(halo::tx_fixup_kernel<8>, dim3(halo::tx_grid(n, 8, 4)), block, 0, s, p);
     else hipLaunchKernelGGL(halo::tx_fixup_kernel<16>, dim3(halo::tx_grid(n, 4, 4)), block, 0, s, p);

@@ -52,6 +52,7 @@ for s in "$@"; do
     kwrq)  step kwrq 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/kwrq" -o run -- python3 tools/exp/bench_tx.py ;;
     ptxb)  step probe_txb 300 ./tools/exp/probe_txb ;;
     tring) step pytest_ring 600 python -u -m pytest tests/test_gpu_ring.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    abtx3) step ab_tx3 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_tx.py && python tools/exp/bench_tx_build.py" txg1 txg4 txbnew ;;
     *) echo "unknown step $s" ;;
   esac
 done
