@@ -789,35 +789,49 @@ def ring_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = False):
     # batch from native code (tools/bench_loop.hip halo_bench_ring_polls: the calls a cgo
     # PacketHandle makes, no Python between batches); the Python-loop figure beside it
     m = 1000
-    wring = RingBuffer(8 << 20)
-    wcons = RingConsumer(wring, capacity=1514, max_frames=4096, register=True)
     host_m = _lib.host_array(int(offs[m - 1] + lens[m - 1]) + 16)
     host_m[:] = host[:host_m.size]
-    us = np.zeros(2000, np.float64)
-    bad = ctypes.c_uint32()
-    _lib.check("halo_bench_ring_polls", bench_lib().halo_bench_ring_polls(
-        wring.mem.ctypes.data, wcons._h, host_m.ctypes.data, offs.ctypes.data, lens.ctypes.data, m, 1,
-        ctypes.addressof(netif), wcons._out.ctypes.data, 100, us.size, us.ctypes.data, ctypes.byref(bad)))
-    el = float(np.median(us)) * 1e-6
-    times = []
-    for s in range(201):
-        assert wring.write_batch(host, offs[:m], lens[:m]) == m
-        t0 = time.perf_counter()
-        recs, inf, _ = wcons.poll(netif)
-        wcons.commit()
-        if s:
-            times.append(time.perf_counter() - t0)
-        assert inf["n_frames"] == m
-    res["config1_wire_1k_64B"] = {"frames": m, "mpps": round(m / el / 1e6, 3), "us_per_batch": round(el * 1e6, 2),
-                                  "us_p10": round(float(np.percentile(us, 10)), 2),
-                                  "us_p90": round(float(np.percentile(us, 90)), 2), "bad_batches": int(bad.value),
-                                  "python_loop_us_per_batch": round(float(np.median(times)) * 1e6, 1),
-                                  "what": "engine.Wire ring (8 MiB), 1k x 64 B UDP, poll + commit per batch from a "
-                                          "native loop (2000 batches, median; the producer's WritePacket calls are "
-                                          "untimed). Small path: the host reads the 1k length fields, one rx launch "
-                                          "parses the frames in place in the registered ring over PCIe and writes the "
-                                          "records into the registered result array"}
-    wcons.close()
+
+    def wire_polls(persistent: bool) -> dict:
+        wring = RingBuffer(8 << 20)
+        wcons = RingConsumer(wring, capacity=1514, max_frames=4096, register=True, persistent=persistent)
+        us = np.zeros(2000, np.float64)
+        bad = ctypes.c_uint32()
+        _lib.check("halo_bench_ring_polls", bench_lib().halo_bench_ring_polls(
+            wring.mem.ctypes.data, wcons._h, host_m.ctypes.data, offs.ctypes.data, lens.ctypes.data, m, 1,
+            ctypes.addressof(netif), wcons._out.ctypes.data, 100, us.size, us.ctypes.data, ctypes.byref(bad)))
+        st = wcons.stats()
+        el = float(np.median(us)) * 1e-6
+        times = []
+        for s in range(201):
+            assert wring.write_batch(host, offs[:m], lens[:m]) == m
+            t0 = time.perf_counter()
+            recs, inf, _ = wcons.poll(netif)
+            wcons.commit()
+            if s:
+                times.append(time.perf_counter() - t0)
+            assert inf["n_frames"] == m and bool((recs["status"] == 0).all())
+        wcons.close()
+        polls = max(1, int(st["small_polls"]))
+        out = {"frames": m, "mpps": round(m / el / 1e6, 3), "us_per_batch": round(el * 1e6, 2),
+               "us_p10": round(float(np.percentile(us, 10)), 2), "us_p90": round(float(np.percentile(us, 90)), 2),
+               "bad_batches": int(bad.value), "python_loop_us_per_batch": round(float(np.median(times)) * 1e6, 1),
+               "per_poll_us": {"walk": round(st["walk_ns"] / polls / 1e3, 2),
+                               "wait": round(st["wait_ns"] / polls / 1e3, 2)}}
+        if persistent:
+            out["per_poll_us"]["consumer_gpu"] = round(st["service_gpu_ns"] / max(1, int(st["service_requests"])) / 1e3, 2)
+            out["consumer_launches"] = int(st["service_launches"])
+        return out
+
+    res["config1_wire_1k_64B"] = wire_polls(True)
+    res["config1_wire_1k_64B"]["what"] = (
+        "engine.Wire ring (8 MiB) attached HALO_RING_PERSISTENT, 1k x 64 B UDP, poll + commit per batch from a "
+        "native loop (2000 batches, median; the producer's WritePacket calls are untimed). The host reads the 1k "
+        "length fields (walk); the resident consumer (16 workgroups waiting on a pinned control block) parses "
+        "the frames in place in the registered ring over PCIe and writes the records into the registered result "
+        "array (wait); no launch or stream synchronisation per poll")
+    res["config1_wire_1k_64B"]["launch_per_poll"] = wire_polls(False)
+    res["config1_wire_1k_64B"]["launch_per_poll"]["what"] = "the same ring attached without HALO_RING_PERSISTENT: one rx launch + one stream synchronisation per poll"
     if with_cpu:
         from oracle import oracle as O
 
@@ -1134,6 +1148,10 @@ def main():
             "mpps": round(n * args.steps / wt / 1e6, 1), "kernel_ms": round(kt, 5),
             "roofline": roofline(algt, kt, load_traffic("tx_config2")), "alg_bytes_per_launch": algt,
             "steps": "NatChangeDst + NatChangeSrc + eth_tx DPDK fill, per-frame addresses/ports"}
+        # the probe moves what the memory system must: the frames + metadata + ops in, and one
+        # 64-byte write per frame (the kernel's TCC_EA0_WRREQ_64B count, profiles/r03/r3f/) + results
+        with_probe(sec["tx_fixup_config2_nat_dpdk"]["roofline"],
+                   size_matched_probe(dev, fbytes + n * (4 + 2 + 16), n * (64 + 1), d, nbuf=args.rotate), kt)
         if not args.no_cpu:
             from oracle import oracle as O
 

@@ -64,10 +64,10 @@ int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 // windows dealt round-robin over the groups) and write their records to `out`; each group then
 // publishes its done_seq slot. The host never launches per poll.
 #ifndef HALO_SVC_GROUPS
-#define HALO_SVC_GROUPS 16  // workgroups of the resident consumer (each on its own CU)
+#define HALO_SVC_GROUPS 8   // workgroups of the resident consumer (each on its own CU)
 #endif
 #ifndef HALO_SVC_WAVES
-#define HALO_SVC_WAVES 4    // waves per workgroup (64 frames each per pass)
+#define HALO_SVC_WAVES 8    // waves per workgroup (64 frames each per pass)
 #endif
 constexpr uint32_t kSvcGroups = HALO_SVC_GROUPS;
 constexpr uint32_t kSvcWaves = HALO_SVC_WAVES;

@@ -284,16 +284,29 @@ struct Hist {
 // 16-byte chunks per lane issued before the header is parsed (a lane-per-frame lane needs its
 // first 64 bytes). Eight for groups would let a 570 B frame finish in one round trip, but costs
 // ~55 VGPRs (occupancy 5 -> 3) and lost more than it gained; kept as a knob.
+#ifndef HALO_RX_R0_G8
+#define HALO_RX_R0_G8 4  // measurement knob: round-0 chunk rows of the 8-lane kernel
+#endif
 template <int G>
-constexpr int kRound0 = 4;
+constexpr int kRound0 = G == 8 ? HALO_RX_R0_G8 : 4;
 // One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
+// HALO_RX_TAIL0 (groups): round 0 takes the frame's last G chunks in place of its R0-th head
+// chunk row, so a 128-byte line shared with the next frame is read by both frames' groups at the
+// same time (the next frame's head is in its round 0) instead of one round trip apart, by when the
+// L2 has often dropped it (1500 B: 3.3 % of the bytes read twice, TCC_EA0_RDREQ_128B).
+#ifndef HALO_RX_TAIL0
+#define HALO_RX_TAIL0 0
+#endif
 template <int G, int R0 = kRound0<G>>
 struct FrameState {
     static constexpr int kR0 = R0;
     const uint8_t* frame;
     uint32_t L, ndw;
-    uint32_t buf[R0][4];  // round 0: chunks (u*G + gl) of 16 bytes
+    uint32_t tail;        // HALO_RX_TAIL0: first chunk of the tail row (chunks tail + gl)
+    uint32_t buf[R0][4];  // round 0: chunks (u*G + gl) of 16 bytes (TAIL0: row R0-1 = the tail)
 };
+template <int G, int R0>
+constexpr bool kTail0 = HALO_RX_TAIL0 && G > 1 && R0 > 1;
 
 template <int LAYOUT, typename FS>
 __device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool present, FS& st) {
@@ -307,8 +320,16 @@ __device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool p
 // L4 end is not known before the header is parsed, and never exceeds the frame length).
 template <int G, int R0>
 __device__ __forceinline__ void frame_loads(uint32_t gl, FrameState<G, R0>& st) {
+    if constexpr (kTail0<G, R0>) {
+        const uint32_t chunks = (st.ndw + 3) >> 2, head = (R0 - 1) * G;
+        st.tail = chunks > head + G ? chunks - G : head;
 #pragma unroll
-    for (int u = 0; u < R0; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
+        for (int u = 0; u < R0 - 1; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
+        load4(st.frame, (st.tail + gl) * 4, st.ndw, st.buf[R0 - 1]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < R0; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
+    }
 }
 
 // Header dwords 0..11 of the frame: the lane's own chunks (G = 1) or chunk 0 of group lanes 0..2.
@@ -415,8 +436,10 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
         // for any other frame the sum is never read.
         const uint32_t tl = L3 ? bswap16(h[0] >> 16) : bswap16(h[4] & 0xFFFFu);
         acc_chunk<L3, true>(st.buf[0], gl * 4, kIpOff<L3> + tl, hs);
+        constexpr int UH = kTail0<G, R0> ? U0 - 1 : U0;
 #pragma unroll
-        for (int u = 1; u < U0; ++u) acc_chunk<L3>(st.buf[u], (u * G + gl) * 4, kIpOff<L3> + tl, hs);
+        for (int u = 1; u < UH; ++u) acc_chunk<L3>(st.buf[u], (u * G + gl) * 4, kIpOff<L3> + tl, hs);
+        if constexpr (kTail0<G, R0>) acc_chunk<L3>(st.buf[U0 - 1], (st.tail + gl) * 4, kIpOff<L3> + tl, hs);
     }
     Verdict v = parse_header<L3>(h, st.L, present, p);
 
@@ -449,8 +472,13 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
     } else if constexpr (G > 1) {
         // later rounds: the group's loop bound is wave-uniform in practice (one length per batch),
         // and a group with no segment (or a frame not present) loads nothing
-        const uint32_t seg_dw = v.seg_end ? (v.seg_end + 3) >> 2 : 0u;
-        for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
+        uint32_t seg_dw = v.seg_end ? (v.seg_end + 3) >> 2 : 0u;
+        uint32_t r_first = U0 * STEP;
+        if constexpr (kTail0<G, R0>) {  // the chunks between the head rows and the tail row
+            r_first = (U0 - 1) * STEP;
+            seg_dw = seg_dw < 4 * st.tail ? seg_dw : 4 * st.tail;
+        }
+        for (uint32_t r0 = r_first; r0 < seg_dw; r0 += U * STEP) {
             uint32_t x[U][4];
 #pragma unroll
             for (int u = 0; u < U; ++u) load4(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
@@ -619,9 +647,14 @@ rx_lane_kernel(const RxParams p) {
 // stop flag and an idle timeout on the 100 MHz real-time counter, so every wave reaches the exit.
 // A new req_seq whose check matches the fields of the same read is taken (the fields arrive with
 // the sequence number: no second round trip); an acquire fence, then the group's waves parse their
-// 64-frame windows (window k goes to group k % kSvcGroups, spreading a 1k-frame request over 16
+// 64-frame windows (window k goes to group k % kSvcGroups, spreading a 1k-frame request over 8
 // CUs' memory pipelines) with the lane kernel's window code; after a block barrier thread 0 fences
-// and publishes the group's done_seq slot.
+// and publishes the group's done_seq slot. Measured on one box (profiles/r03/r3j/ab_svc.log, 1 /
+// 1000 frames per poll): 1 group x 16 waves 17.5 us at 1000; 8 x 8 9.2 / 11.8-12.6 us; 16 x 4
+// 10.3 / 13.2-13.9; 32 x 2 16.5 / 20.4. Rejected: each group also reading its window's lengths
+// with the request (offsets derived in-wave, no metadata read after the request: 11.5 / 13.3-13.6,
+// the wider poll read cost more than the read it saved), and four poll reads in flight per group
+// (profiles/r03/r3h: 25.9 us at 1000: the reads queued ahead of the frame reads).
 __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServiceCtl* ctl, const uint8_t* data,
                                                                       const uint32_t* off, const uint16_t* len,
                                                                       uint32_t last, uint64_t idle_ticks) {

@@ -29,9 +29,10 @@
 // one's-complement sum in the little-endian domain, as rx_parse.hip; the L4 segment starts at an
 // even frame offset), reduced over the group with DPP, and patched into the header chunks, which
 // are stored last. Chunks wholly inside the payload skip every mask; a lane-per-frame frame of
-// <= 64 B is built whole in registers with no per-dword branch (build_small). The kernel is bound by its
-// vector instructions and register budget more than by HBM: tools/exp/probe_txb.hip moves the
-// same bytes in 32 us (64 B) / 161 us (1514 B) with no arithmetic.
+// <= 64 B is built whole in registers with no per-dword branch (build_small), staged in LDS and
+// stored by the wave four lanes per frame: lane-per-frame stores (one instruction touching 64
+// separate slots) cost more than all the rest of the 64 B build (tools/exp/probe_txb.hip,
+// DESIGN.md §10.5).
 #include <hip/hip_runtime.h>
 
 #include <type_traits>

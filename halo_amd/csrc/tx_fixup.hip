@@ -373,7 +373,8 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
         // stores land in one 64-byte HBM write request (TCC_EA0_WRREQ_64B: 1.016 per frame,
         // profiles/r03/r3f/tx_fixup_write_requests.json), the floor for a frame with a dirty byte;
         // writing the whole 64 bytes measured 33.4 -> 40.4 us and non-temporal stores neutral
-        // (profiles/r03/r3f/ab_tx_store.log)
+        // (profiles/r03/r3f/ab_tx_store.log); staging the frames in LDS and storing the dirty chunks
+        // (or whole lines) four lanes per frame 33.0 -> 39.4 (38.5) us (profiles/r03/r3j/ab_txc.log)
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
         __attribute__((address_space(1))) uint32_t* fw =
             (__attribute__((address_space(1))) uint32_t*)reinterpret_cast<uint32_t*>(frame);
@@ -415,6 +416,7 @@ __device__ __forceinline__ void tx_frame(const TxParams& p, uint32_t i, bool pre
 #ifndef HALO_TX_G1_LDS_PAD
 #define HALO_TX_G1_LDS_PAD 8192
 #endif
+
 template <int G>
 constexpr uint32_t kTxBlock = G == 1 ? HALO_TX_G1_BLOCK : 256;
 template <int G>

@@ -296,13 +296,13 @@ HALO_API int halo_rx_shard_multi(halo_rx_host_ctx_t* const* ctxs, uint32_t n_ctx
                                         another live registration (HALO_E_INVAL; see
                                         halo_rx_host_register)                                      */
 #define HALO_RING_PERSISTENT 0x2u    /* attach (with HALO_RING_REGISTER): small polls of up to 16384
-                                        frames are served by a resident consumer kernel (one
-                                        workgroup on one CU) that waits on a control block in pinned
-                                        memory: a poll writes a request and spins on its completion,
-                                        with no kernel launch and no stream synchronisation. The
-                                        kernel exits after 20 ms without a request (the next poll
-                                        relaunches it) and at detach. Same records, stops and cursor
-                                        as the other paths.                                          */
+                                        frames are served by a resident consumer kernel (8
+                                        workgroups, one per CU) that waits on a control block in
+                                        pinned memory: a poll writes a request and spins on its
+                                        completion, with no kernel launch and no stream
+                                        synchronisation. The kernel exits after 20 ms without a
+                                        request (the next poll relaunches it) and at detach. Same
+                                        records, stops and cursor as the other paths.                */
 
 typedef struct halo_rx_ring_scan {
     uint32_t n_frames;  /* frames taken                                                      */

@@ -53,6 +53,16 @@ for s in "$@"; do
     ptxb)  step probe_txb 300 ./tools/exp/probe_txb ;;
     tring) step pytest_ring 600 python -u -m pytest tests/test_gpu_ring.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     abtx3) step ab_tx3 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_tx.py && python tools/exp/bench_tx_build.py" txg1 txg4 txbnew ;;
+    kgap)  step kgap 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/kgap" -o run -- python3 tools/exp/gap_fetch.py ;;
+    absvc) step ab_svc 900 bash tools/exp/ab_variants.sh "python tools/bench_ring_native.py --persistent --frames 1 --iters 3000 && python tools/bench_ring_native.py --persistent --frames 1000 --iters 3000" ${AB_SVC:-svcA svcB} ;;
+    krd)   step krd 600 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krd" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
+    kwrq2) step kwrq2 600 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/kwrq" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
+    krdgap) step krdgap 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krdgap" -o run -- python3 tools/exp/gap_fetch.py ;;
+    abtxc) step ab_txc 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_tx.py" txc0 txc1 txc2 ;;
+    abtail) step ab_tail 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,570B:4,imix:-1,imix:-2,jumbo9000:16" tl0 tl1 ;;
+    vtail) step vtail 600 bash tools/exp/variant_tests.sh "tests/test_gpu_parity.py tests/test_gpu_stream.py -m gpu" tl1 ;;
+    krdtail) step krdtail 600 bash tools/exp/with_variant.sh tl1 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krdtail" -o run -- python3 tools/prof_kernels.py 1500B_udp_1M ;;
+    krdr12) step krdr12 600 bash tools/exp/with_variant.sh r12 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krdr12" -o run -- python3 tools/prof_kernels.py 1500B_udp_1M ;;
     *) echo "unknown step $s" ;;
   esac
 done

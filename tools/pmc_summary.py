@@ -106,7 +106,7 @@ def main():
             res[w]["kernel"] = [r["Kernel_Name"]]
             res[w]["vgpr"] = [int(r["VGPR_Count"])]
             res[w]["sgpr"] = [int(r["SGPR_Count"])]
-    for step in ("kfetch", "kwrite", "ksq"):
+    for step in ("kfetch", "kwrite", "ksq", "krd", "kwrq"):
         rows = _rows(os.path.join(sess, step, "run_counter_collection.csv"))
         amap = attribute(rows)
         per = defaultdict(dict)
@@ -138,6 +138,23 @@ def main():
             s["write_over_alg"] = round(avg["WRITE_SIZE"] * 1024 / wr_alg, 3)
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             s["hbm_bytes_per_launch"] = int(2 * avg["FETCH_SIZE"] * 1024 + avg["WRITE_SIZE"] * 1024)
+        # exact request bytes from the L2's memory-side request counters by size (krd / kwrq passes):
+        # no calibration factor needed (FETCH_SIZE tallies a 128-byte request as 64 bytes on gfx950)
+        r32, r64, r128 = (avg.get(f"TCC_EA0_RDREQ_{b}B_sum") for b in (32, 64, 128))
+        if r32 is not None and r64 is not None and r128 is not None:
+            s["read_bytes_by_request_size"] = int(32 * r32 + 64 * r64 + 128 * r128)
+            s["read_over_alg"] = round(s["read_bytes_by_request_size"] / rd_alg, 4)
+            if avg.get("TCC_EA0_RDREQ_sum"):
+                s["rdreq_sizes_cover_all"] = round((r32 + r64 + r128) / avg["TCC_EA0_RDREQ_sum"], 4)
+        w_all, w64 = avg.get("TCC_EA0_WRREQ_sum"), avg.get("TCC_EA0_WRREQ_64B_sum")
+        if w_all is not None and w64 is not None:
+            s["write_bytes_by_request_size"] = int(64 * w64 + 32 * (w_all - w64))
+            s["write_requests_64B"] = int(w64)
+        if "read_bytes_by_request_size" in s:
+            wb = s.get("write_bytes_by_request_size", s.get("write_bytes"))
+            if wb is not None:
+                s["hbm_bytes_per_launch"] = s["read_bytes_by_request_size"] + wb
+                s["hbm_bytes_method"] = "TCC_EA0_RDREQ_{32,64,128}B + TCC_EA0_WRREQ(_64B) request sizes"
         for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS",
                   "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT"):
             if c in avg:
