@@ -827,7 +827,7 @@ def ring_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = False):
     res["config1_wire_1k_64B"]["what"] = (
         "engine.Wire ring (8 MiB) attached HALO_RING_PERSISTENT, 1k x 64 B UDP, poll + commit per batch from a "
         "native loop (2000 batches, median; the producer's WritePacket calls are untimed). The host reads the 1k "
-        "length fields (walk); the resident consumer (16 workgroups waiting on a pinned control block) parses "
+        "length fields (walk); the resident consumer (8 workgroups waiting on a pinned control block) parses "
         "the frames in place in the registered ring over PCIe and writes the records into the registered result "
         "array (wait); no launch or stream synchronisation per poll")
     res["config1_wire_1k_64B"]["launch_per_poll"] = wire_polls(False)
@@ -1114,8 +1114,10 @@ def main():
     del shard
     line["roofline"]["note"] = ("achieved = (frame bytes + 6 B metadata + 32 B record) per launch / average "
                                 "launch duration (one HIP event pair over the timed region / steps); "
-                                "peak = HBM3E spec; traffic = 2 x FETCH_SIZE + WRITE_SIZE per launch from "
-                                "profiles/pmc_summary.json; size_matched_probe_ms = a no-work kernel streaming "
+                                "peak = HBM3E spec; traffic = HBM request bytes per launch from profiles/pmc_summary.json "
+                                "(rocprofv3 --pmc TCC_EA0_RDREQ_{32,64,128}B and TCC_EA0_WRREQ/_64B, each "
+                                "request at its size; the same kernel and workload, tools/prof_kernels.py); "
+                                "size_matched_probe_ms = a no-work kernel streaming "
                                 "the same bytes in and out with perfect access patterns over the same number of "
                                 "rotating buffers (frac_of_size_matched = probe / kernel time)")
     if d.world == 1 and not args.no_secondary:

@@ -59,6 +59,19 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
 // every later LDS access wait for it).
 typedef const __attribute__((address_space(1))) uint32_t gu32;
 
+// load4 with a non-temporal hint on the 16-byte path (bytes read once: not kept in the L2 ahead
+// of lines another group will read)
+__device__ __forceinline__ void load4_nt(const uint8_t* frame, uint32_t d0, uint32_t ndw, uint32_t (&w)[4]) {
+    gu32* p = (gu32*)(reinterpret_cast<const uint32_t*>(frame) + d0);
+    if (d0 + 4 <= ndw) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+        const u32x4 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)p);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (d0 + j < ndw) ? p[j] : 0u;
+    }
+}
 __device__ __forceinline__ void load4(const uint8_t* frame, uint32_t d0, uint32_t ndw, uint32_t (&w)[4]) {
     gu32* p = (gu32*)(reinterpret_cast<const uint32_t*>(frame) + d0);
     if (d0 + 4 <= ndw) {

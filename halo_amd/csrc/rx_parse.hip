@@ -290,23 +290,29 @@ struct Hist {
 template <int G>
 constexpr int kRound0 = G == 8 ? HALO_RX_R0_G8 : 4;
 // One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
-// HALO_RX_TAIL0 (groups): round 0 takes the frame's last G chunks in place of its R0-th head
-// chunk row, so a 128-byte line shared with the next frame is read by both frames' groups at the
-// same time (the next frame's head is in its round 0) instead of one round trip apart, by when the
-// L2 has often dropped it (1500 B: 3.3 % of the bytes read twice, TCC_EA0_RDREQ_128B).
+// HALO_RX_TAIL0 (groups, knob): 1 = round 0 takes the frame's last G chunks in place of its
+// R0-th head row; 2 = round 0 also takes the frame's last 128-byte line [S, end) as an extra row,
+// issued just before row 0, so that the line a frame shares with the next one is requested by two
+// consecutive load instructions (the next frame's row 0 follows); later rounds stop at S. Packed
+// 1500 B frames otherwise fetch every shared line twice (profiles/r03/r3l/g8_line_sharing.json).
 #ifndef HALO_RX_TAIL0
 #define HALO_RX_TAIL0 0
+#endif
+#ifndef HALO_RX_LATER_NT
+#define HALO_RX_LATER_NT 0
 #endif
 template <int G, int R0 = kRound0<G>>
 struct FrameState {
     static constexpr int kR0 = R0;
     const uint8_t* frame;
     uint32_t L, ndw;
-    uint32_t tail;        // HALO_RX_TAIL0: first chunk of the tail row (chunks tail + gl)
-    uint32_t buf[R0][4];  // round 0: chunks (u*G + gl) of 16 bytes (TAIL0: row R0-1 = the tail)
+    uint32_t tail;        // HALO_RX_TAIL0 1: first chunk of the tail row; 2: first dword of the last line
+    uint32_t buf[R0 + (HALO_RX_TAIL0 == 2 && G > 1)][4];  // round 0: chunks (u*G + gl) of 16 bytes
 };
 template <int G, int R0>
-constexpr bool kTail0 = HALO_RX_TAIL0 && G > 1 && R0 > 1;
+constexpr bool kTail0 = HALO_RX_TAIL0 == 1 && G > 1 && R0 > 1;
+template <int G, int R0>
+constexpr bool kTail2 = HALO_RX_TAIL0 == 2 && G > 1;
 
 template <int LAYOUT, typename FS>
 __device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool present, FS& st) {
@@ -326,6 +332,15 @@ __device__ __forceinline__ void frame_loads(uint32_t gl, FrameState<G, R0>& st) 
 #pragma unroll
         for (int u = 0; u < R0 - 1; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
         load4(st.frame, (st.tail + gl) * 4, st.ndw, st.buf[R0 - 1]);
+    } else if constexpr (kTail2<G, R0>) {
+        // the frame's last line, from its first byte (S, 128-byte aligned) when S lies past the head
+        // rows; dwords of the frame only (load4 bounds), so the tail row may hold fewer than 16 B
+        const uint64_t fa = reinterpret_cast<uint64_t>(st.frame);
+        const uint32_t s_dw = st.ndw ? (uint32_t)((((fa + 4ull * st.ndw - 1) & ~127ull) - fa) >> 2) : 0u;
+        st.tail = s_dw >= 4u * G * R0 ? s_dw : st.ndw;  // ndw: no tail row
+        load4(st.frame, st.tail + 4 * gl, st.ndw, st.buf[R0]);
+#pragma unroll
+        for (int u = 0; u < R0; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
     } else {
 #pragma unroll
         for (int u = 0; u < R0; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
@@ -440,6 +455,7 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
 #pragma unroll
         for (int u = 1; u < UH; ++u) acc_chunk<L3>(st.buf[u], (u * G + gl) * 4, kIpOff<L3> + tl, hs);
         if constexpr (kTail0<G, R0>) acc_chunk<L3>(st.buf[U0 - 1], (st.tail + gl) * 4, kIpOff<L3> + tl, hs);
+        if constexpr (kTail2<G, R0>) acc_chunk<L3>(st.buf[U0], st.tail + 4 * gl, kIpOff<L3> + tl, hs);
     }
     Verdict v = parse_header<L3>(h, st.L, present, p);
 
@@ -478,10 +494,19 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
             r_first = (U0 - 1) * STEP;
             seg_dw = seg_dw < 4 * st.tail ? seg_dw : 4 * st.tail;
         }
+        if constexpr (kTail2<G, R0>) seg_dw = seg_dw < st.tail ? seg_dw : st.tail;  // the last line is in
         for (uint32_t r0 = r_first; r0 < seg_dw; r0 += U * STEP) {
             uint32_t x[U][4];
 #pragma unroll
-            for (int u = 0; u < U; ++u) load4(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
+            for (int u = 0; u < U; ++u) {
+                // HALO_RX_LATER_NT: 1 = every later-round row non-temporal; 2 = all but the frame's
+                // last row (which may share its line with the next frame's row 0)
+                const uint32_t d = r0 + (u * G + gl) * 4;
+                if (HALO_RX_LATER_NT == 1 || (HALO_RX_LATER_NT == 2 && 4 * (d + 4 * G) < 4 * seg_dw))
+                    load4_nt(st.frame, d, seg_dw, x[u]);
+                else
+                    load4(st.frame, d, seg_dw, x[u]);
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u) acc_chunk<L3>(x[u], r0 + (u * G + gl) * 4, v.seg_end, hs);
         }

@@ -63,6 +63,15 @@ for s in "$@"; do
     vtail) step vtail 600 bash tools/exp/variant_tests.sh "tests/test_gpu_parity.py tests/test_gpu_stream.py -m gpu" tl1 ;;
     krdtail) step krdtail 600 bash tools/exp/with_variant.sh tl1 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krdtail" -o run -- python3 tools/prof_kernels.py 1500B_udp_1M ;;
     krdr12) step krdr12 600 bash tools/exp/with_variant.sh r12 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krdr12" -o run -- python3 tools/prof_kernels.py 1500B_udp_1M ;;
+    plines) step plines 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/plines" -o run -- ./tools/exp/probe_lines ;;
+    abtail2) step ab_tail2 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,570B:4,jumbo9000:16,imix:-1" tl0 tl2 ;;
+    vtail2) step vtail2 600 bash tools/exp/variant_tests.sh "tests/test_gpu_parity.py tests/test_gpu_stream.py -m gpu" tl2 ;;
+    krdtail2) step krdtail2 600 bash tools/exp/with_variant.sh tl2 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krdtail2" -o run -- python3 tools/prof_kernels.py 1500B_udp_1M ;;
+    abov) step ab_ov 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,570B:4,jumbo9000:16,imix:-1,imix:-2,64B:1" tl0 ov1 ;;
+    vov) step vov 600 bash tools/exp/variant_tests.sh "tests/test_gpu_parity.py tests/test_gpu_stream.py tests/test_gpu_tx.py -m gpu" ov1 ;;
+    krdov) step krdov 600 bash tools/exp/with_variant.sh ov1 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krdov" -o run -- python3 tools/prof_kernels.py 1500B_udp_1M config3_imix_16M ;;
+    abnt) step ab_nt 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,570B:4,jumbo9000:16,imix:-1" tl0 nt1 nt2 ;;
+    krdnt) step krdnt 600 bash -c "bash tools/exp/with_variant.sh nt1 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d $OUT/krdnt1 -o run -- python3 tools/prof_kernels.py 1500B_udp_1M && bash tools/exp/with_variant.sh nt2 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d $OUT/krdnt2 -o run -- python3 tools/prof_kernels.py 1500B_udp_1M" ;;
     *) echo "unknown step $s" ;;
   esac
 done
