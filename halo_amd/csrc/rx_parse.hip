@@ -290,29 +290,18 @@ struct Hist {
 template <int G>
 constexpr int kRound0 = G == 8 ? HALO_RX_R0_G8 : 4;
 // One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
-// HALO_RX_TAIL0 (groups, knob): 1 = round 0 takes the frame's last G chunks in place of its
-// R0-th head row; 2 = round 0 also takes the frame's last 128-byte line [S, end) as an extra row,
-// issued just before row 0, so that the line a frame shares with the next one is requested by two
-// consecutive load instructions (the next frame's row 0 follows); later rounds stop at S. Packed
-// 1500 B frames otherwise fetch every shared line twice (profiles/r03/r3l/g8_line_sharing.json).
-#ifndef HALO_RX_TAIL0
-#define HALO_RX_TAIL0 0
-#endif
-#ifndef HALO_RX_LATER_NT
-#define HALO_RX_LATER_NT 0
+// Later-round loads of the widest groups (jumbo frames) are non-temporal: 9000 B frames 6.10-6.33
+// -> 6.00 ms; for 570 B / 1500 B / IMIX the same hint cost 13-16 % (profiles/r03/r3p/ab_nt.log).
+#ifndef HALO_RX_LATER_NT_G
+#define HALO_RX_LATER_NT_G 16
 #endif
 template <int G, int R0 = kRound0<G>>
 struct FrameState {
     static constexpr int kR0 = R0;
     const uint8_t* frame;
     uint32_t L, ndw;
-    uint32_t tail;        // HALO_RX_TAIL0 1: first chunk of the tail row; 2: first dword of the last line
-    uint32_t buf[R0 + (HALO_RX_TAIL0 == 2 && G > 1)][4];  // round 0: chunks (u*G + gl) of 16 bytes
+    uint32_t buf[R0][4];  // round 0: chunks (u*G + gl) of 16 bytes
 };
-template <int G, int R0>
-constexpr bool kTail0 = HALO_RX_TAIL0 == 1 && G > 1 && R0 > 1;
-template <int G, int R0>
-constexpr bool kTail2 = HALO_RX_TAIL0 == 2 && G > 1;
 
 template <int LAYOUT, typename FS>
 __device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool present, FS& st) {
@@ -326,25 +315,8 @@ __device__ __forceinline__ void frame_meta(const RxParams& p, uint64_t i, bool p
 // L4 end is not known before the header is parsed, and never exceeds the frame length).
 template <int G, int R0>
 __device__ __forceinline__ void frame_loads(uint32_t gl, FrameState<G, R0>& st) {
-    if constexpr (kTail0<G, R0>) {
-        const uint32_t chunks = (st.ndw + 3) >> 2, head = (R0 - 1) * G;
-        st.tail = chunks > head + G ? chunks - G : head;
 #pragma unroll
-        for (int u = 0; u < R0 - 1; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
-        load4(st.frame, (st.tail + gl) * 4, st.ndw, st.buf[R0 - 1]);
-    } else if constexpr (kTail2<G, R0>) {
-        // the frame's last line, from its first byte (S, 128-byte aligned) when S lies past the head
-        // rows; dwords of the frame only (load4 bounds), so the tail row may hold fewer than 16 B
-        const uint64_t fa = reinterpret_cast<uint64_t>(st.frame);
-        const uint32_t s_dw = st.ndw ? (uint32_t)((((fa + 4ull * st.ndw - 1) & ~127ull) - fa) >> 2) : 0u;
-        st.tail = s_dw >= 4u * G * R0 ? s_dw : st.ndw;  // ndw: no tail row
-        load4(st.frame, st.tail + 4 * gl, st.ndw, st.buf[R0]);
-#pragma unroll
-        for (int u = 0; u < R0; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
-    } else {
-#pragma unroll
-        for (int u = 0; u < R0; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
-    }
+    for (int u = 0; u < R0; ++u) load4(st.frame, (u * G + gl) * 4, st.ndw, st.buf[u]);
 }
 
 // Header dwords 0..11 of the frame: the lane's own chunks (G = 1) or chunk 0 of group lanes 0..2.
@@ -451,11 +423,8 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
         // for any other frame the sum is never read.
         const uint32_t tl = L3 ? bswap16(h[0] >> 16) : bswap16(h[4] & 0xFFFFu);
         acc_chunk<L3, true>(st.buf[0], gl * 4, kIpOff<L3> + tl, hs);
-        constexpr int UH = kTail0<G, R0> ? U0 - 1 : U0;
 #pragma unroll
-        for (int u = 1; u < UH; ++u) acc_chunk<L3>(st.buf[u], (u * G + gl) * 4, kIpOff<L3> + tl, hs);
-        if constexpr (kTail0<G, R0>) acc_chunk<L3>(st.buf[U0 - 1], (st.tail + gl) * 4, kIpOff<L3> + tl, hs);
-        if constexpr (kTail2<G, R0>) acc_chunk<L3>(st.buf[U0], st.tail + 4 * gl, kIpOff<L3> + tl, hs);
+        for (int u = 1; u < U0; ++u) acc_chunk<L3>(st.buf[u], (u * G + gl) * 4, kIpOff<L3> + tl, hs);
     }
     Verdict v = parse_header<L3>(h, st.L, present, p);
 
@@ -488,24 +457,13 @@ __device__ __forceinline__ void frame_finish(const RxParams& p, uint64_t i, bool
     } else if constexpr (G > 1) {
         // later rounds: the group's loop bound is wave-uniform in practice (one length per batch),
         // and a group with no segment (or a frame not present) loads nothing
-        uint32_t seg_dw = v.seg_end ? (v.seg_end + 3) >> 2 : 0u;
-        uint32_t r_first = U0 * STEP;
-        if constexpr (kTail0<G, R0>) {  // the chunks between the head rows and the tail row
-            r_first = (U0 - 1) * STEP;
-            seg_dw = seg_dw < 4 * st.tail ? seg_dw : 4 * st.tail;
-        }
-        if constexpr (kTail2<G, R0>) seg_dw = seg_dw < st.tail ? seg_dw : st.tail;  // the last line is in
-        for (uint32_t r0 = r_first; r0 < seg_dw; r0 += U * STEP) {
+        const uint32_t seg_dw = v.seg_end ? (v.seg_end + 3) >> 2 : 0u;
+        for (uint32_t r0 = U0 * STEP; r0 < seg_dw; r0 += U * STEP) {
             uint32_t x[U][4];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                // HALO_RX_LATER_NT: 1 = every later-round row non-temporal; 2 = all but the frame's
-                // last row (which may share its line with the next frame's row 0)
-                const uint32_t d = r0 + (u * G + gl) * 4;
-                if (HALO_RX_LATER_NT == 1 || (HALO_RX_LATER_NT == 2 && 4 * (d + 4 * G) < 4 * seg_dw))
-                    load4_nt(st.frame, d, seg_dw, x[u]);
-                else
-                    load4(st.frame, d, seg_dw, x[u]);
+                if constexpr (G >= HALO_RX_LATER_NT_G) load4_nt(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
+                else load4(st.frame, r0 + (u * G + gl) * 4, seg_dw, x[u]);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) acc_chunk<L3>(x[u], r0 + (u * G + gl) * 4, v.seg_end, hs);
