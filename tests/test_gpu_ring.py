@@ -474,3 +474,66 @@ def test_persistent_consumer_idle_exit_and_relaunch(dev, golden, oracle_lib):
         if detach_idle:
             time.sleep(0.05)
         cons.close()
+
+
+def test_persistent_polls_of_changing_sizes(dev, oracle_lib):
+    """HALO_RING_PERSISTENT small polls whose sizes cross 64-frame window edges and change from poll
+    to poll (1 .. 2600 frames, runs of equal lengths and mixed 42..64 B lengths: the host walk's
+    same-length runs), an empty span, a poll cut by max_frames, and records into an array that is
+    neither pinned nor registered: every poll's records, positions, stop and tail == the oracle."""
+    from halo_amd import _lib
+    from halo_amd._lib import RING_SCAN_DTYPE, NetIf
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    O = oracle_lib
+    onetif = O.NetIf.make()
+    rng = np.random.default_rng(29)
+    ring = RingBuffer(1 << 22)
+    _seek(ring, (1 << 36) + 4096)
+    cons = RingConsumer(ring, capacity=1514, persistent=True, max_frames=2000)
+    plain = np.zeros(cons.max_frames, _lib.RESULT_DTYPE)  # neither pinned nor registered
+    before = cons.stats()
+    sizes = [1000, 1, 63, 64, 65, 1900, 2, 640, 0, 1000, 129, 2600, 1000, 1000]
+    served = 0
+    for it, k in enumerate(sizes):
+        small = it % 2 == 1  # mixed 42..64 B lengths; even polls: 64 B frames (one same-length run)
+        lens = (rng.integers(42, 65, size=k) if small else np.full(k, 64)).astype(np.uint16)
+        kinds = rng.integers(0, 3, size=k).astype(np.uint8)
+        offs = np.concatenate([[0], np.cumsum((lens.astype(np.int64) + 3) & ~3)[:-1]]).astype(np.uint32) // 4
+        data = O.synth_batch(1000 + it, 0, lens, kinds, onetif, offsets_dw=offs) if k else np.zeros(4, np.uint8)
+        if k and it % 3 == 2:  # a bit flip in one frame
+            j = int(rng.integers(0, k))
+            data[int(offs[j]) * 4 + int(rng.integers(14, int(lens[j])))] ^= 1 << int(rng.integers(0, 8))
+        start = ring.head
+        if k:
+            assert ring.write_batch(data, offs.astype(np.uint64) * 4, lens) == k
+        want_n = min(k, cons.max_frames)
+        want, _ = O.rx_batch(data, lens[:want_n], onetif, 1, offsets_dw=offs[:want_n]) if want_n else (None, None)
+        served += 0 < min(k, cons.max_frames)
+        if it in (5, 6):  # records into plain memory: the library stages them
+            info = np.zeros(1, RING_SCAN_DTYPE)
+            pos = np.zeros(cons.max_frames, np.uint64)
+            _lib.check("poll", _lib.lib.halo_rx_ring_poll(cons._h, 1, NetIf.make(), plain.ctypes.data, None,
+                                                          pos.ctypes.data, info.ctypes.data))
+            n, stop = int(info["n_frames"][0]), int(info["stop"][0])
+            got, pos = plain[:n], pos[:n]
+        else:
+            got, d, pos = cons.poll(NetIf.make(), positions=True)
+            n, stop = d["n_frames"], {"EMPTY": 0, "MAX": 4}.get(d["stop"], -1)
+        assert n == want_n, (it, k, n)
+        assert stop == (4 if k > cons.max_frames else 0), (it, stop)
+        if n:
+            assert_records_equal(got.copy(), want, None, f"poll {it} ({k} frames)")
+            rec = np.concatenate([[0], np.cumsum(4 + ((lens[:n].astype(np.int64) + 3) & ~3))[:-1]])
+            assert np.array_equal(pos, start + rec)
+        cons.commit()
+        if k > cons.max_frames:  # the rest in the next poll
+            got, d, _ = cons.poll(NetIf.make())
+            rest, _ = O.rx_batch(data, lens[want_n:], onetif, 1, offsets_dw=offs[want_n:])
+            assert d["n_frames"] == k - want_n
+            assert_records_equal(got.copy(), rest, None, f"poll {it} rest")
+            cons.commit()
+        assert ring.tail == ring.head
+    st = cons.stats()
+    assert st["service_requests"] - before["service_requests"] >= served > 10  # every small poll with frames
+    cons.close()

@@ -70,14 +70,16 @@ void fuzz_ring(int iters) {
         for (uint32_t op = 0; op < ops; ++op) {
             const uint64_t kind = below(10);
             if (kind < 5) {  // produce a batch: some empty, some > size/2, some huge
-                const uint32_t n = (uint32_t)below(12);
+                // a third of the batches repeat one length (the walk's same-length runs)
+                const bool same = below(3) == 0;
+                const uint32_t n = (uint32_t)below(same ? 40 : 12);
                 std::vector<uint16_t> lens(n);
                 std::vector<uint64_t> offs(n);
                 uint64_t total = 0;
                 for (uint32_t k = 0; k < n; ++k) {
                     const uint64_t pick = below(8);
-                    lens[k] = (uint16_t)(pick == 0 ? 0 : pick == 1 ? below(65536) : pick == 2 ? size / 2 + below(8)
-                                                                                  : below(size / 2 + 1));
+                    lens[k] = (uint16_t)(same && k ? lens[0] : pick == 0 ? 0 : pick == 1 ? below(65536)
+                                                     : pick == 2 ? size / 2 + below(8) : below(size / 2 + 1));
                     offs[k] = total;
                     total += lens[k];
                 }
