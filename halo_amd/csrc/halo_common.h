@@ -72,15 +72,20 @@ int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 constexpr uint32_t kSvcGroups = HALO_SVC_GROUPS;
 constexpr uint32_t kSvcWaves = HALO_SVC_WAVES;
 struct alignas(64) RingServiceCtl {
-    // The request: one 64-byte line. The host writes the fields, then `check` (svc_check of words
-    // 0..7), then req_seq with release. Each workgroup reads the whole line with one 16-lane load
+    // The request: one 64-byte line. The host writes the fields, then `check` (svc_check of the
+    // fields), then req_seq with release. Each workgroup reads the whole line with one 16-lane load
     // and takes a request whose req_seq is new and whose check matches (a torn read is re-read).
     uint32_t req_seq;        // host: the request number
     uint32_t n, flags, mac_lo, mac_hi, own_ip;
     uint32_t out_lo, out_hi; // device address of the request's records
     uint32_t stop;           // host: 1 = exit now
     uint32_t check;
-    uint32_t pad0[6];
+    // A poll whose frames all have one length and follow each other in the ring (config 1) is
+    // described here instead of by the offset / length arrays: frame i at data + 4 * (uni_off +
+    // i * uni_stride), uni_len bytes (0: use the arrays). It arrives with the request, so the
+    // consumer skips the arrays' PCIe round trip.
+    uint32_t uni_off, uni_stride, uni_len;
+    uint32_t pad0[3];
     // Completion: one slot per workgroup, each written by its group after its records are visible
     // (system-scope release)
     uint32_t done_seq[kSvcGroups];
@@ -90,10 +95,11 @@ struct alignas(64) RingServiceCtl {
 };
 static_assert(offsetof(RingServiceCtl, done_seq) == 64, "request line");
 __host__ __device__ inline uint32_t svc_check(uint32_t seq, uint32_t n, uint32_t flags, uint32_t mac_lo, uint32_t mac_hi,
-                                              uint32_t own_ip, uint32_t out_lo, uint32_t out_hi) {
-    const uint32_t w[8] = {seq, n, flags, mac_lo, mac_hi, own_ip, out_lo, out_hi};
+                                              uint32_t own_ip, uint32_t out_lo, uint32_t out_hi, uint32_t uni_off,
+                                              uint32_t uni_stride, uint32_t uni_len) {
+    const uint32_t w[11] = {seq, n, flags, mac_lo, mac_hi, own_ip, out_lo, out_hi, uni_off, uni_stride, uni_len};
     uint32_t h = 0x811C9DC5u;
-    for (int i = 0; i < 8; ++i) h = (h ^ w[i]) * 0x01000193u;
+    for (int i = 0; i < 11; ++i) h = (h ^ w[i]) * 0x01000193u;
     return h;
 }
 // Launches the consumer on `s`: it serves requests after `last`, and exits when `stop` is set or

@@ -64,6 +64,7 @@ RingWalk ring_walk(const uint8_t* data, uint64_t size, uint64_t cursor, uint64_t
         lens[w.n] = (uint16_t)len;
         if (positions) positions[w.n] = cursor + a;
         w.max_len = std::max(w.max_len, len);
+        w.min_len = std::min(w.min_len, len);
         ++w.n;
         a += bytes;
         // A run of records of this same length (config 1: every frame 64 B). Above, the next

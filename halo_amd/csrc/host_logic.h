@@ -29,7 +29,7 @@ int validate_ring(const uint8_t* mem, int64_t offset, uint64_t* size, uint64_t* 
 // (HALO_RING_STOP_*); `wraps` is set, and the walk stops, at the first frame whose bytes wrap around
 // the data area's end (the caller then linearises the span instead).
 struct RingWalk {
-    uint32_t n = 0, stop = HALO_RING_STOP_EMPTY, max_len = 0;
+    uint32_t n = 0, stop = HALO_RING_STOP_EMPTY, max_len = 0, min_len = 0xFFFFFFFFu;
     uint64_t end_bytes = 0;  // record bytes taken: the tail advance
     bool wraps = false;
 };

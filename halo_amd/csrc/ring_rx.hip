@@ -614,7 +614,7 @@ constexpr uint32_t kSvcIdleUs = 20000;      // the resident consumer exits after
 // consumer that went idle (or exited between its last check and the request) is relaunched: the
 // stream says whether its kernel is still running. Every wait is bounded.
 int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
-                    halo_rx_result_t* dout) {
+                    halo_rx_result_t* dout, uint32_t uni_off, uint32_t uni_stride, uint32_t uni_len) {
     using clk = std::chrono::steady_clock;
     halo::RingServiceCtl* c = r->svc;
     const uint32_t seq = r->svc_seq + 1;
@@ -627,7 +627,11 @@ int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_n
     c->own_ip = netif->ip;
     c->out_lo = (uint32_t)out;
     c->out_hi = (uint32_t)(out >> 32);
-    __atomic_store_n(&c->check, halo::svc_check(seq, n, flags, c->mac_lo, c->mac_hi, c->own_ip, c->out_lo, c->out_hi),
+    c->uni_off = uni_off;
+    c->uni_stride = uni_stride;
+    c->uni_len = uni_len;
+    __atomic_store_n(&c->check, halo::svc_check(seq, n, flags, c->mac_lo, c->mac_hi, c->own_ip, c->out_lo, c->out_hi,
+                                                uni_off, uni_stride, uni_len),
                      __ATOMIC_RELEASE);
     auto launch = [&](uint32_t last) {
         r->svc_launched = halo::launch_ring_service(r->d_svc, r->d_data, r->d_soff, r->d_slen, last, kSvcIdleUs,
@@ -703,12 +707,20 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
             if (hipHostMalloc((void**)&r->h_sres, sb, hipHostMallocDefault) != hipSuccess) return HALO_E_NOMEM;
             if (!(r->d_sres = static_cast<halo_rx_result_t*>(device_view(r->h_sres, sb)))) return HALO_E_NOMEM;
         }
+        // one length and consecutive records (no wrap between the first and the last): frame i at
+        // off_dw[0] + i * stride, passed as the strided layout (no offset / length arrays to read)
+        const uint32_t stride = (4u + max_len + 3u) >> 2;
+        const bool uni = w.min_len == max_len &&
+                         (int64_t)r->h_soff[n - 1] - (int64_t)r->h_soff[0] == (int64_t)(n - 1) * stride;
         int rc;
         if (r->svc && n <= kSvcMaxFrames) {
-            rc = service_request(r, n, flags, netif, dout ? dout : r->d_sres);
+            rc = service_request(r, n, flags, netif, dout ? dout : r->d_sres, uni ? r->h_soff[0] : 0u,
+                                 uni ? stride : 0u, uni ? max_len : 0u);
         } else {
-            rc = halo_rx_parse_batch_device(r->d_data, r->d_soff, r->d_slen, n, flags, netif, max_len,
-                                            dout ? dout : r->d_sres, nullptr, r->s_comp);
+            rc = uni ? halo_rx_parse_strided_device(r->d_data + 4ull * r->h_soff[0], 4ull * stride, nullptr, max_len, n,
+                                                    flags, netif, dout ? dout : r->d_sres, nullptr, r->s_comp)
+                     : halo_rx_parse_batch_device(r->d_data, r->d_soff, r->d_slen, n, flags, netif, max_len,
+                                                  dout ? dout : r->d_sres, nullptr, r->s_comp);
             if (!rc && hipStreamSynchronize(r->s_comp) != hipSuccess) rc = HALO_E_HIP;
         }
         r->stats.wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t1).count();

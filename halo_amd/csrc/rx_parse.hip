@@ -641,7 +641,7 @@ rx_lane_kernel(const RxParams p) {
 __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServiceCtl* ctl, const uint8_t* data,
                                                                       const uint32_t* off, const uint16_t* len,
                                                                       uint32_t last, uint64_t idle_ticks) {
-    __shared__ uint32_t s_cmd[10];  // seq, exit, n, flags, mac_lo, mac_hi, own_ip, out_lo, out_hi
+    __shared__ uint32_t s_cmd[12];  // seq, exit, n, flags, mac_lo, mac_hi, own_ip, out_lo, out_hi, uni_off/stride/len
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     __shared__ uint4 s_rec[kSvcWaves][128];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, g = blockIdx.x;
@@ -659,7 +659,8 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
                     const uint32_t ck = svc_check(seq, __builtin_amdgcn_readlane(v, 1), __builtin_amdgcn_readlane(v, 2),
                                                   __builtin_amdgcn_readlane(v, 3), __builtin_amdgcn_readlane(v, 4),
                                                   __builtin_amdgcn_readlane(v, 5), __builtin_amdgcn_readlane(v, 6),
-                                                  __builtin_amdgcn_readlane(v, 7));
+                                                  __builtin_amdgcn_readlane(v, 7), __builtin_amdgcn_readlane(v, 10),
+                                                  __builtin_amdgcn_readlane(v, 11), __builtin_amdgcn_readlane(v, 12));
                     if (ck == __builtin_amdgcn_readlane(v, 9)) break;
                 }
                 if (__builtin_amdgcn_readlane(v, 8) || __builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
@@ -678,6 +679,9 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
                 s_cmd[6] = __builtin_amdgcn_readlane(v, 5);
                 s_cmd[7] = __builtin_amdgcn_readlane(v, 6);
                 s_cmd[8] = __builtin_amdgcn_readlane(v, 7);
+                s_cmd[9] = __builtin_amdgcn_readlane(v, 10);
+                s_cmd[10] = __builtin_amdgcn_readlane(v, 11);
+                s_cmd[11] = __builtin_amdgcn_readlane(v, 12);
                 if (!quit) ctl->t_seen[g] = __builtin_amdgcn_s_memrealtime();
             }
             // the request's off / len / frames are read after the request was seen
@@ -696,8 +700,16 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
         p.own_ip = s_cmd[6];
         p.out = reinterpret_cast<halo_rx_result_t*>((uint64_t)s_cmd[7] | ((uint64_t)s_cmd[8] << 32));
         Hist hist{s_hist, 0};
-        for (uint32_t base = (w * kSvcGroups + g) * 64; base < p.n; base += kSvcGroups * kSvcWaves * 64)
-            lane_window<0, 0>(p, base, lane, s_rec[w], hist);
+        if (s_cmd[11]) {  // one length, consecutive records: the strided layout, no array reads
+            p.bytes = data + 4ull * s_cmd[9];
+            p.stride = 4ull * s_cmd[10];
+            p.len = s_cmd[11];
+            for (uint32_t base = (w * kSvcGroups + g) * 64; base < p.n; base += kSvcGroups * kSvcWaves * 64)
+                lane_window<2, 0>(p, base, lane, s_rec[w], hist);
+        } else {
+            for (uint32_t base = (w * kSvcGroups + g) * 64; base < p.n; base += kSvcGroups * kSvcWaves * 64)
+                lane_window<0, 0>(p, base, lane, s_rec[w], hist);
+        }
         __syncthreads();  // every record of this group stored
         if (threadIdx.x == 0) {
             ctl->t_done[g] = __builtin_amdgcn_s_memrealtime();
