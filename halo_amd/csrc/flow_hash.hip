@@ -258,6 +258,113 @@ __device__ uint64_t hash_long8(const uint8_t* d, uint32_t len, uint32_t j, const
     return avalanche((uint64_t)len * P64_1 + m);
 }
 
+// hashLong on a group of 4 lanes: lane j owns accumulators 2j and 2j+1 and reads input words 2j
+// and 2j+1 of each stripe (bytes [16j, 16j+16): one 16-byte load), so the i ^ 1 exchange of
+// accumulateStripe (xxh3.go:181-209) stays inside the lane — no DPP swap — and a wave-instruction
+// reads 16 strings' 64-byte stripes. The load is unaligned (gfx9 global loads accept any byte
+// address; the 16 bytes are all string bytes, so no other page is touched).
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ void ld128u(const uint8_t* p, uint64_t& lo, uint64_t& hi) {
+    const u32x4u v = *(const __attribute__((address_space(1))) u32x4u*)p;
+    lo = join64(v.x, v.y);
+    hi = join64(v.z, v.w);
+}
+__device__ __forceinline__ void stripe_acc2(uint64_t& a0, uint64_t& a1, uint64_t in0, uint64_t in1, uint64_t s0,
+                                            uint64_t s1) {
+    const uint64_t k0 = in0 ^ s0, k1 = in1 ^ s1;
+    a0 += in1 + (uint64_t)(uint32_t)k0 * (k0 >> 32);
+    a1 += in0 + (uint64_t)(uint32_t)k1 * (k1 >> 32);
+}
+__device__ uint64_t hash_long4(const uint8_t* d, uint32_t len, uint32_t j, const LongSecrets& sec) {
+    constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+    uint64_t a0 = kInit[0], a1 = kInit[1];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+        a0 = j == (uint32_t)q ? kInit[2 * q] : a0;
+        a1 = j == (uint32_t)q ? kInit[2 * q + 1] : a1;
+    }
+    const uint8_t* q0 = d + 16 * j;
+    constexpr uint32_t B = HALO_XXH3_BATCH;  // stripes whose loads are issued together
+    uint32_t stripe = 0, remaining = len;
+    while (remaining > 1024) {
+#pragma unroll 1
+        for (uint32_t st = 0; st < 16; st += B) {
+            uint64_t lo[B], hi[B];
+#pragma unroll
+            for (uint32_t u = 0; u < B; ++u) ld128u(q0 + 64 * (stripe + st + u), lo[u], hi[u]);
+#pragma unroll
+            for (uint32_t u = 0; u < B; ++u)
+                stripe_acc2(a0, a1, lo[u], hi[u], sec.w8[st + u + 2 * j], sec.w8[st + u + 2 * j + 1]);
+        }
+        stripe += 16;
+        remaining -= 1024;
+        a0 ^= a0 >> 47;  // scramble (xxh3.go:212-218)
+        a1 ^= a1 >> 47;
+        a0 ^= sec.w8[16 + 2 * j];
+        a1 ^= sec.w8[17 + 2 * j];
+        a0 *= P32_1;
+        a1 *= P32_1;
+    }
+    const uint32_t stripes = (remaining - 1) / 64;
+    uint32_t st = 0;
+    for (; st + B <= stripes; st += B) {
+        uint64_t lo[B], hi[B];
+#pragma unroll
+        for (uint32_t u = 0; u < B; ++u) ld128u(q0 + 64 * (stripe + st + u), lo[u], hi[u]);
+#pragma unroll
+        for (uint32_t u = 0; u < B; ++u)
+            stripe_acc2(a0, a1, lo[u], hi[u], sec.w8[st + u + 2 * j], sec.w8[st + u + 2 * j + 1]);
+    }
+    for (; st < stripes; ++st) {
+        uint64_t lo, hi;
+        ld128u(q0 + 64 * (stripe + st), lo, hi);
+        stripe_acc2(a0, a1, lo, hi, sec.w8[st + 2 * j], sec.w8[st + 2 * j + 1]);
+    }
+    {  // last stripe, secret offset 121
+        uint64_t lo, hi;
+        ld128u(d + len - 64 + 16 * j, lo, hi);
+        stripe_acc2(a0, a1, lo, hi, sec.last[2 * j], sec.last[2 * j + 1]);
+    }
+    // merge (xxh3.go:139-145): pair (2j, 2j+1) with secret 11 + 16j on lane j, summed over the quad
+    uint64_t m = mul_fold64(a0 ^ sec.merge[2 * j], a1 ^ sec.merge[2 * j + 1]);
+    m += dpp64<0xB1>(m);  // quad_perm 1,0,3,2
+    m += dpp64<0x4E>(m);  // quad_perm 2,3,0,1
+    return avalanche((uint64_t)len * P64_1 + m);
+}
+
+// hashMedium / hashLarge (xxh3.go:94-129, 17..240 bytes) on a group of 8 lanes. Both are sums of
+// independent mix16 terms (wrapping 64-bit adds: any order), so each lane takes one term — its 16
+// data bytes in one unaligned load, always inside the string — and a butterfly sums them:
+// hashMedium's pairs (16k, len-16-16k) on lanes 2k / 2k+1, hashLarge's first eight terms on
+// lanes 0..7, an avalanche, then its middle terms and the last one the same way.
+__device__ __forceinline__ uint64_t mix16u(const uint8_t* p, uint32_t soff) {
+    uint64_t lo, hi;
+    ld128u(p, lo, hi);
+    return mul_fold64(lo ^ sec64(soff), hi ^ sec64(soff + 8));
+}
+__device__ __forceinline__ uint64_t sum8(uint64_t v) {
+    v += dpp64<0xB1>(v);   // quad_perm 1,0,3,2
+    v += dpp64<0x4E>(v);   // quad_perm 2,3,0,1
+    v += dpp64<0x141>(v);  // row_half_mirror: lane i <-> 7-i within each 8
+    return v;
+}
+__device__ uint64_t hash_mid8(const uint8_t* d, uint32_t len, uint32_t l) {
+    uint64_t v = 0;
+    if (len <= 128) {
+        const uint32_t levels = len > 96 ? 4u : len > 64 ? 3u : len > 32 ? 2u : 1u;
+        const uint32_t k = l >> 1, side = l & 1u;
+        if (k < levels) v = mix16u(d + (side ? len - 16 - 16 * k : 16 * k), 32 * k + 16 * side);
+        return avalanche((uint64_t)len * P64_1 + sum8(v));
+    }
+    v = mix16u(d + 16 * l, 16 * l);
+    const uint64_t acc = avalanche((uint64_t)len * P64_1 + sum8(v));
+    const uint32_t nmid = ((len & ~15u) - 128) / 16;  // 0..7 middle terms, then the last one
+    v = 0;
+    if (l < nmid) v = mix16u(d + 128 + 16 * l, 3 + 16 * l);
+    else if (l == nmid) v = mix16u(d + len - 16, 119);
+    return avalanche(acc + sum8(v));
+}
+
 struct XxhParams {
     const uint8_t* bytes;
     const uint64_t* offsets;
@@ -266,11 +373,12 @@ struct XxhParams {
     uint64_t* out;
 };
 
-// strings <= 240 B, one lane each (the long ones are left to xxh3_long_kernel). A wave scans
-// kShortScan strings and compacts the short ones into LDS — the 129..240 B ones first, then the
-// rest, so a wave-instruction's lanes mostly take the same hashLarge / hashMedium / hashSmall
-// branch — and hashes them 64 at a time: a ragged batch whose short strings are a minority no
-// longer runs the whole short path for a handful of lanes in every wave.
+// strings <= 240 B (the long ones are left to xxh3_long_kernel). A wave scans kShortScan strings
+// and compacts the short ones into LDS by class — 129..240 B, then 17..128 B, then <= 16 B — so a
+// round's groups mostly take the same branch. 17..240 B strings are hashed eight at a time on
+// 8-lane groups (hash_mid8: one 16-byte term per lane), <= 16 B ones a lane each (hash_short).
+// Lane-per-string for 17..240 B (up to 23 dependent mix16 terms, every lane gathering 4-byte words
+// of a different string) ran at ~0.5 TB/s.
 #ifndef HALO_XXH3_SHORT_SCAN
 #define HALO_XXH3_SHORT_SCAN 256
 #endif
@@ -280,6 +388,7 @@ __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t g = lane >> 3, l = lane & 7u;
     for (uint32_t base = wave * kShortScan; base < p.n; base += nwaves * kShortScan) {
         uint32_t len[kShortScan / 64];
 #pragma unroll
@@ -287,12 +396,13 @@ __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
             const uint32_t i = base + 64 * k + lane;
             len[k] = i < p.n ? p.lens[i] : 0xFFFFFFFFu;
         }
-        uint32_t cnt = 0;
+        uint32_t cnt = 0, n_mid = 0;
 #pragma unroll
-        for (int pass = 0; pass < 2; ++pass) {
+        for (int pass = 0; pass < 3; ++pass) {
 #pragma unroll
             for (uint32_t k = 0; k < kShortScan / 64; ++k) {
-                const bool take = pass == 0 ? (len[k] > 128 && len[k] <= 240) : len[k] <= 128;
+                const bool take = pass == 0 ? (len[k] > 128 && len[k] <= 240)
+                                : pass == 1 ? (len[k] > 16 && len[k] <= 128) : len[k] <= 16;
                 const uint64_t b = __ballot(take);
                 if (take)
                     s_idx[w][cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
@@ -300,9 +410,18 @@ __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
                         base + 64 * k + lane;
                 cnt += (uint32_t)__popcll(b);
             }
+            if (pass == 1) n_mid = cnt;
         }
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t e = lane; e < ((cnt + 63) & ~63u); e += 64) {
+        for (uint32_t r = 0; r < n_mid; r += 8) {
+            const uint32_t e = r + g;
+            if (e < n_mid) {  // uniform per group
+                const uint32_t i = s_idx[w][e];
+                const uint64_t h = hash_mid8(p.bytes + p.offsets[i], p.lens[i], l);
+                if (l == 0) p.out[i] = h;
+            }
+        }
+        for (uint32_t e = n_mid + lane; e < ((cnt - n_mid + 63) & ~63u) + n_mid; e += 64) {
             if (e < cnt) {
                 const uint32_t i = s_idx[w][e];
                 p.out[i] = hash_short(p.bytes + p.offsets[i], p.lens[i]);
@@ -313,16 +432,28 @@ __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
 }
 
 // strings > 240 B: each wave scans 64 strings, ranks its long ones by length (longest first) and
-// hashes them eight at a time, one per 8-lane group — rank order keeps the eight strings of a
-// round about equally long, so groups do not idle behind the round's longest string
-__global__ void __launch_bounds__(HALO_XXH3_LONG_BLOCK) xxh3_long_kernel(const XxhParams p) {
+// hashes them sixteen at a time, one per 4-lane group (eight per 8-lane group with
+// HALO_XXH3_LANES=8) — rank order keeps the strings of a round about equally long, so groups do
+// not idle behind the round's longest string
+#ifndef HALO_XXH3_LANES
+#define HALO_XXH3_LANES 4  // lanes per long string: 4 (hash_long4) or 8 (hash_long8)
+#endif
+#ifndef HALO_XXH3_LONG_WAVES
+#define HALO_XXH3_LONG_WAVES 0  // amdgpu_waves_per_eu for the long kernel (0: the compiler's choice)
+#endif
+__global__ void __launch_bounds__(HALO_XXH3_LONG_BLOCK)
+#if HALO_XXH3_LONG_WAVES
+__attribute__((amdgpu_waves_per_eu(HALO_XXH3_LONG_WAVES)))
+#endif
+xxh3_long_kernel(const XxhParams p) {
+    constexpr uint32_t LN = HALO_XXH3_LANES, GPW = 64 / LN;  // strings per round
     __shared__ LongSecrets s_sec;
     __shared__ uint8_t s_order[HALO_XXH3_LONG_BLOCK / 64][64];  // per wave: lane holding the string of each rank
     load_secrets(s_sec);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = threadIdx.x >> 6;
-    const uint32_t g = lane >> 3, j = lane & 7u;
+    const uint32_t g = lane / LN, j = lane & (LN - 1);
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t base = wave * 64; base < p.n; base += nwaves * 64) {
@@ -340,12 +471,13 @@ __global__ void __launch_bounds__(HALO_XXH3_LONG_BLOCK) xxh3_long_kernel(const X
         }
         if (len) s_order[w][rank] = (uint8_t)lane;
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t r0 = 0; r0 < nlong; r0 += 8) {
+        for (uint32_t r0 = 0; r0 < nlong; r0 += GPW) {
             const uint32_t rk = r0 + g;
             if (rk < nlong) {  // uniform per group
                 const uint32_t owner = s_order[w][rk];
                 const uint32_t idx = base + owner;
-                const uint64_t h = hash_long8(p.bytes + p.offsets[idx], p.lens[idx], j, s_sec);
+                const uint64_t h = LN == 4 ? hash_long4(p.bytes + p.offsets[idx], p.lens[idx], j, s_sec)
+                                           : hash_long8(p.bytes + p.offsets[idx], p.lens[idx], j, s_sec);
                 if (j == 0) p.out[idx] = h;
             }
         }

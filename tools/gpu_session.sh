@@ -72,6 +72,8 @@ for s in "$@"; do
     krdov) step krdov 600 bash tools/exp/with_variant.sh ov1 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krdov" -o run -- python3 tools/prof_kernels.py 1500B_udp_1M config3_imix_16M ;;
     abnt) step ab_nt 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,570B:4,jumbo9000:16,imix:-1" tl0 nt1 nt2 ;;
     krdnt) step krdnt 600 bash -c "bash tools/exp/with_variant.sh nt1 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d $OUT/krdnt1 -o run -- python3 tools/prof_kernels.py 1500B_udp_1M && bash tools/exp/with_variant.sh nt2 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d $OUT/krdnt2 -o run -- python3 tools/prof_kernels.py 1500B_udp_1M" ;;
+    abxx) step ab_xxh3 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_xxh3.py" ${AB_XX:-xx8 xx4} ;;
+    abg8) step ab_g8 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,imix:-1,570B:8" ${AB_G8:-g8shfl g8dpp} ;;
     *) echo "unknown step $s" ;;
   esac
 done
