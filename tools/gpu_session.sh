@@ -74,6 +74,9 @@ for s in "$@"; do
     krdnt) step krdnt 600 bash -c "bash tools/exp/with_variant.sh nt1 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d $OUT/krdnt1 -o run -- python3 tools/prof_kernels.py 1500B_udp_1M && bash tools/exp/with_variant.sh nt2 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d $OUT/krdnt2 -o run -- python3 tools/prof_kernels.py 1500B_udp_1M" ;;
     abxx) step ab_xxh3 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_xxh3.py" ${AB_XX:-xx8 xx4} ;;
     abg8) step ab_g8 900 bash tools/exp/ab_variants.sh "python tools/tune.py --spec 1500B:8,imix:-1,570B:8" ${AB_G8:-g8shfl g8dpp} ;;
+    ktxx)  step ktxx 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ktxx" -o run -- python3 tools/exp/bench_xxh3.py ;;
+    sqxx)  step sqxx 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/sqxx" -o run -- python3 tools/exp/bench_xxh3.py ;;
+    rdxx)  step rdxx 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/rdxx" -o run -- python3 tools/exp/bench_xxh3.py ;;
     *) echo "unknown step $s" ;;
   esac
 done
