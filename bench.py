@@ -48,8 +48,8 @@ def log(*a):
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=1000)  # 22 ms timed region at N=1: launch jitter < 1 %
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--frames", type=int, default=1 << 20, help="frames per batch per GPU")
     p.add_argument("--rotate", type=int, default=16,
                    help="distinct batches cycled through (frames x rotate = one GPU's shard: 16M = config 4 / 8)")
