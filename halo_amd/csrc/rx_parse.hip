@@ -290,8 +290,9 @@ struct Hist {
 template <int G>
 constexpr int kRound0 = G == 8 ? HALO_RX_R0_G8 : 4;
 // One frame's state between "fetch" (addresses + round-0 loads issued) and "finish".
-// Later-round loads of the widest groups (jumbo frames) are non-temporal: 9000 B frames 6.10-6.33
-// -> 6.00 ms; for 570 B / 1500 B / IMIX the same hint cost 13-16 % (profiles/r03/r3p/ab_nt.log).
+// Later-round loads of the widest groups (jumbo frames) are non-temporal: 9000 B frames 6.08-6.10
+// -> 5.76 ms; for 1500 B on 8 lanes the same hint costs 12 % (290-296 -> 332 us), IMIX 2 %
+// (profiles/r03/r3y/ab_nt.log: HALO_RX_LATER_NT_G 16 / off / 8, two rounds on one box).
 #ifndef HALO_RX_LATER_NT_G
 #define HALO_RX_LATER_NT_G 16
 #endif
