@@ -78,6 +78,7 @@ for s in "$@"; do
     sqxx)  step sqxx 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/sqxx" -o run -- python3 tools/exp/bench_xxh3.py ;;
     rdxx)  step rdxx 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/rdxx" -o run -- python3 tools/exp/bench_xxh3.py ;;
     abgen) step ${AB_NAME:-ab_gen} 900 bash tools/exp/ab_variants.sh "$AB_CMD" $AB_V ;;
+    krdv)  step krd_$KV 600 bash tools/exp/with_variant.sh $KV rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krd_$KV" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
     *) echo "unknown step $s" ;;
   esac
 done
