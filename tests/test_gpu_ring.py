@@ -476,11 +476,14 @@ def test_persistent_consumer_idle_exit_and_relaunch(dev, golden, oracle_lib):
         cons.close()
 
 
-def test_persistent_polls_of_changing_sizes(dev, oracle_lib):
-    """HALO_RING_PERSISTENT small polls whose sizes cross 64-frame window edges and change from poll
-    to poll (1 .. 2600 frames, runs of equal lengths and mixed 42..64 B lengths: the host walk's
-    same-length runs), an empty span, a poll cut by max_frames, and records into an array that is
-    neither pinned nor registered: every poll's records, positions, stop and tail == the oracle."""
+@pytest.mark.parametrize("persistent", [True, False], ids=["persistent", "launch"])
+def test_small_polls_of_changing_sizes(dev, oracle_lib, persistent):
+    """Small polls (served by the resident consumer, or one launch each) whose sizes cross 64-frame
+    window edges and change from poll to poll (1 .. 2600 frames): polls of one frame length
+    (64 B: the host walk's same-length run, and the uniform request / strided launch that needs no
+    offset arrays) and of mixed 42..64 B lengths, an empty span, a poll cut by max_frames, and
+    records into an array that is neither pinned nor registered: every poll's records, positions,
+    stop and tail == the oracle."""
     from halo_amd import _lib
     from halo_amd._lib import RING_SCAN_DTYPE, NetIf
     from halo_amd.ring import RingBuffer, RingConsumer
@@ -490,7 +493,7 @@ def test_persistent_polls_of_changing_sizes(dev, oracle_lib):
     rng = np.random.default_rng(29)
     ring = RingBuffer(1 << 22)
     _seek(ring, (1 << 36) + 4096)
-    cons = RingConsumer(ring, capacity=1514, persistent=True, max_frames=2000)
+    cons = RingConsumer(ring, capacity=1514, persistent=persistent, max_frames=2000, small_poll=16 << 20)
     plain = np.zeros(cons.max_frames, _lib.RESULT_DTYPE)  # neither pinned nor registered
     before = cons.stats()
     sizes = [1000, 1, 63, 64, 65, 1900, 2, 640, 0, 1000, 129, 2600, 1000, 1000]
@@ -535,5 +538,8 @@ def test_persistent_polls_of_changing_sizes(dev, oracle_lib):
             cons.commit()
         assert ring.tail == ring.head
     st = cons.stats()
-    assert st["service_requests"] - before["service_requests"] >= served > 10  # every small poll with frames
+    got_small = st["small_polls"] - before["small_polls"]
+    assert got_small >= served > 10  # every poll with frames took the small path
+    if persistent:
+        assert st["service_requests"] - before["service_requests"] >= served
     cons.close()
