@@ -207,18 +207,29 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
                 if (4 * c + i < ndw) o[i] = w[i];
         }
     };
+    // Groups (G >= 4) visit the chunks in the order 4, 5, ..., C-1, 0, 1, 2, 3 (C = the frame's
+    // chunks): the header chunks and the frame's last, partial chunk — the only ones taking the
+    // masked path — then sit next to each other in one row of U * G, so the other rows of the round
+    // run the unmasked path on every lane (a row with one masked lane runs both paths). 1514 B
+    // frames: one masked row per frame instead of two.
+    const uint32_t nch = (ndw + 3u) >> 2;
+    auto chunk_of = [&](uint32_t v) -> uint32_t {
+        if constexpr (G >= 4) return nch <= 4u ? v : v + 4u < nch ? v + 4u : v + 4u - nch;  // (a LoChan packet can be < 64 B)
+        return v;
+    };
+    uint32_t kc = 4;  // the header chunk this lane keeps (G >= 4: at most one), 4 = none
     for (uint32_t c0 = j; 4 * c0 < ndw; c0 += U * G) {
         uint32_t raw[U][5];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t c = c0 + u * G;
-            if (chunk_has_payload(f, c, ndw)) payload_raw(f, c, raw[u]);
+            const uint32_t c = chunk_of(c0 + u * G);
+            if (c0 + u * G < nch && chunk_has_payload(f, c, ndw)) payload_raw(f, c, raw[u]);
             else raw[u][0] = raw[u][1] = raw[u][2] = raw[u][3] = raw[u][4] = 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t c = c0 + u * G;
-            if (4 * c >= ndw) break;
+            if (c0 + u * G >= nch) break;
+            const uint32_t c = chunk_of(c0 + u * G);
             uint32_t w[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(raw[u][i + 1], raw[u][i], sh);
@@ -239,6 +250,7 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
                 } else {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) keep[0][i] = w[i];
+                    kc = c;
                 }
             } else {
                 store(c, w);
@@ -260,7 +272,7 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
     const uint32_t ck_dw = ck_at >> 2, ck_sh = (ck_at & 2u) * 8u;
 #pragma unroll
     for (int q = 0; q < kDefer; ++q) {
-        const uint32_t c = kDefer == 4 ? (uint32_t)q : j;
+        const uint32_t c = kDefer == 4 ? (uint32_t)q : kc;
         if (c >= 4 || 4 * c >= ndw) continue;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
