@@ -20,6 +20,10 @@
 #include "flow_key.h"
 #include "halo_common.h"
 
+#ifndef HALO_XXH3_FUSED_SHORT
+#define HALO_XXH3_FUSED_SHORT 1  // the long kernel also hashes its windows' short strings (no short launch)
+#endif
+
 namespace halo {
 namespace {
 
@@ -90,7 +94,7 @@ __device__ __forceinline__ uint64_t rrmxmx(uint64_t v, uint64_t len) {  // xxh3.
     v ^= v >> 28;
     return v;
 }
-__device__ __forceinline__ uint64_t mix16(const uint8_t* d, uint32_t doff, uint32_t soff) {  // :221-225
+[[maybe_unused]] __device__ __forceinline__ uint64_t mix16(const uint8_t* d, uint32_t doff, uint32_t soff) {  // :221-225
     return mul_fold64(ld64(d + doff) ^ sec64(soff), ld64(d + doff + 8) ^ sec64(soff + 8));
 }
 
@@ -101,22 +105,26 @@ __device__ __forceinline__ uint64_t hash_9to16(uint64_t w_lo, uint64_t w_hi, uin
     return avalanche((uint64_t)len + __builtin_bswap64(lo) + hi + mul_fold64(lo, hi));
 }
 
+// hashSmall (xxh3.go:59-91), len <= 16, one lane
+__device__ __forceinline__ uint64_t hash_upto16(const uint8_t* d, uint32_t len) {
+    if (len > 8) return hash_9to16(ld64(d), ld64(d + len - 8), len);
+    if (len > 3) {
+        const uint64_t in = (uint64_t)ld32(d + len - 4) + ((uint64_t)ld32(d) << 32);
+        return rrmxmx(in ^ (sec64(8) ^ sec64(16)), len);
+    }
+    uint64_t acc;
+    if (len == 3) acc = ((uint64_t)(ld8(d) | ld8(d + 1) << 8) << 16) + ld8(d + 2) + (3u << 8);
+    else if (len == 2) acc = ((uint64_t)(ld8(d) | ld8(d + 1) << 8) * ((1u << 24) + 1) >> 8) + (2u << 8);
+    else if (len == 1) acc = (uint64_t)ld8(d) * ((1u << 24) + (1u << 16) + 1) + (1u << 8);
+    else return 0x2d06800538d394c2ull;
+    acc ^= (uint64_t)(sec32(0) ^ sec32(4));
+    return avalanche_small(acc);
+}
+
+#if !HALO_XXH3_FUSED_SHORT
 // xxh3HashCode for len <= 240 (xxh3.go:43-129), one lane
 __device__ uint64_t hash_short(const uint8_t* d, uint32_t len) {
-    if (len <= 16) {
-        if (len > 8) return hash_9to16(ld64(d), ld64(d + len - 8), len);
-        if (len > 3) {
-            const uint64_t in = (uint64_t)ld32(d + len - 4) + ((uint64_t)ld32(d) << 32);
-            return rrmxmx(in ^ (sec64(8) ^ sec64(16)), len);
-        }
-        uint64_t acc;
-        if (len == 3) acc = ((uint64_t)(ld8(d) | ld8(d + 1) << 8) << 16) + ld8(d + 2) + (3u << 8);
-        else if (len == 2) acc = ((uint64_t)(ld8(d) | ld8(d + 1) << 8) * ((1u << 24) + 1) >> 8) + (2u << 8);
-        else if (len == 1) acc = (uint64_t)ld8(d) * ((1u << 24) + (1u << 16) + 1) + (1u << 8);
-        else return 0x2d06800538d394c2ull;
-        acc ^= (uint64_t)(sec32(0) ^ sec32(4));
-        return avalanche_small(acc);
-    }
+    if (len <= 16) return hash_upto16(d, len);
     uint64_t acc = (uint64_t)len * P64_1;
     if (len <= 128) {  // hashMedium (xxh3.go:94-113)
         if (len > 32) {
@@ -143,6 +151,7 @@ __device__ uint64_t hash_short(const uint8_t* d, uint32_t len) {
     acc += mix16(d, len - 16, 119);
     return avalanche(acc);
 }
+#endif
 
 // a 64-bit DPP move (both halves with the same control)
 template <int CTRL>
@@ -379,6 +388,7 @@ struct XxhParams {
 // 8-lane groups (hash_mid8: one 16-byte term per lane), <= 16 B ones a lane each (hash_short).
 // Lane-per-string for 17..240 B (up to 23 dependent mix16 terms, every lane gathering 4-byte words
 // of a different string) ran at ~0.5 TB/s.
+#if !HALO_XXH3_FUSED_SHORT
 #ifndef HALO_XXH3_SHORT_SCAN
 #define HALO_XXH3_SHORT_SCAN 256
 #endif
@@ -430,6 +440,7 @@ __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
         __builtin_amdgcn_wave_barrier();
     }
 }
+#endif
 
 // strings > 240 B: each wave scans 64 strings, ranks its long ones by length (longest first) and
 // hashes them sixteen at a time, one per 4-lane group (eight per 8-lane group with
@@ -461,27 +472,56 @@ xxh3_long_kernel(const XxhParams p) {
         const uint32_t raw = i < p.n ? p.lens[i] : 0u;
         const uint32_t len = raw > 240 ? raw : 0u;
         const uint32_t nlong = (uint32_t)__popcll(__ballot(len != 0));
-        if (nlong == 0) continue;
-        // rank = number of lanes with a longer string, ties by lane
-        uint32_t rank = 0;
+        if (!HALO_XXH3_FUSED_SHORT && nlong == 0) continue;
+        if (nlong) {
+            // rank = number of lanes with a longer string, ties by lane
+            uint32_t rank = 0;
 #pragma unroll
-        for (int k = 0; k < 64; ++k) {
-            const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
-            rank += (lk > len || (lk == len && (uint32_t)k < lane)) ? 1u : 0u;
+            for (int k = 0; k < 64; ++k) {
+                const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)len, k);
+                rank += (lk > len || (lk == len && (uint32_t)k < lane)) ? 1u : 0u;
+            }
+            if (len) s_order[w][rank] = (uint8_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t r0 = 0; r0 < nlong; r0 += GPW) {
+                const uint32_t rk = r0 + g;
+                if (rk < nlong) {  // uniform per group
+                    const uint32_t owner = s_order[w][rk];
+                    const uint32_t idx = base + owner;
+                    const uint64_t h = LN == 4 ? hash_long4(p.bytes + p.offsets[idx], p.lens[idx], j, s_sec)
+                                               : hash_long8(p.bytes + p.offsets[idx], p.lens[idx], j, s_sec);
+                    if (j == 0) p.out[idx] = h;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
         }
-        if (len) s_order[w][rank] = (uint8_t)lane;
+#if HALO_XXH3_FUSED_SHORT
+        // the window's short strings in the same wave: lines they share with the long strings just
+        // hashed are still in the L2, and the window's 64 hashes are written by one wave.
+        // 129..240 B, then 17..128 B on 8-lane groups (hash_mid8; classes kept apart so that a
+        // round's groups take one branch), <= 16 B a lane each.
+        const bool in = i < p.n;
+        const uint64_t b_large = __ballot(in && raw > 128 && raw <= 240);
+        const uint64_t b_med = __ballot(in && raw > 16 && raw <= 128);
+        const uint32_t n_large = (uint32_t)__popcll(b_large), n_mid = n_large + (uint32_t)__popcll(b_med);
+        if (in && raw > 128 && raw <= 240)
+            s_order[w][__builtin_amdgcn_mbcnt_hi((uint32_t)(b_large >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)b_large, 0u))] = (uint8_t)lane;
+        if (in && raw > 16 && raw <= 128)
+            s_order[w][n_large + __builtin_amdgcn_mbcnt_hi((uint32_t)(b_med >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)b_med, 0u))] = (uint8_t)lane;
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t r0 = 0; r0 < nlong; r0 += GPW) {
-            const uint32_t rk = r0 + g;
-            if (rk < nlong) {  // uniform per group
-                const uint32_t owner = s_order[w][rk];
-                const uint32_t idx = base + owner;
-                const uint64_t h = LN == 4 ? hash_long4(p.bytes + p.offsets[idx], p.lens[idx], j, s_sec)
-                                           : hash_long8(p.bytes + p.offsets[idx], p.lens[idx], j, s_sec);
-                if (j == 0) p.out[idx] = h;
+        for (uint32_t r0 = 0; r0 < n_mid; r0 += 8) {
+            const uint32_t e = r0 + (lane >> 3);
+            if (e < n_mid) {  // uniform per 8-lane group
+                const uint32_t idx = base + s_order[w][e];
+                const uint64_t h = hash_mid8(p.bytes + p.offsets[idx], p.lens[idx], lane & 7u);
+                if ((lane & 7u) == 0) p.out[idx] = h;
             }
         }
+        if (in && raw <= 16) p.out[i] = hash_upto16(p.bytes + p.offsets[i], raw);
         __builtin_amdgcn_wave_barrier();
+#endif
     }
 }
 
@@ -525,9 +565,11 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
     if (rc) return rc;
     halo::XxhParams p{d_bytes, d_offsets, d_lens, n, d_hash};
     const hipStream_t s = static_cast<hipStream_t>(stream);
+#if !HALO_XXH3_FUSED_SHORT
     hipLaunchKernelGGL(halo::xxh3_short_kernel, dim3(halo::blocks_for((n + halo::kShortScan / 64 - 1) /
                                                                        (halo::kShortScan / 64))),
                        dim3(256), 0, s, p);
+#endif
     constexpr uint32_t wpb = HALO_XXH3_LONG_BLOCK / 64;
     const uint32_t long_blocks = (uint32_t)(((uint64_t)halo::blocks_for(n) * 4 + wpb - 1) / wpb);
     hipLaunchKernelGGL(halo::xxh3_long_kernel, dim3(long_blocks), dim3(HALO_XXH3_LONG_BLOCK), 0, s, p);
