@@ -80,6 +80,7 @@ for s in "$@"; do
     abgen) step ${AB_NAME:-ab_gen} 900 bash tools/exp/ab_variants.sh "$AB_CMD" $AB_V ;;
     krdv)  step krd_$KV 600 bash tools/exp/with_variant.sh $KV rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krd_$KV" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
     wrxx)  step wrxx 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/wrxx" -o run -- python3 tools/exp/bench_xxh3.py ;;
+    vgen)  step vtest_$VT 600 bash tools/exp/variant_tests.sh "$VT_TESTS" $VT ;;
     *) echo "unknown step $s" ;;
   esac
 done
