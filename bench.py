@@ -229,14 +229,15 @@ def device_identity(gpu: int) -> dict:
             "name": torch.cuda.get_device_name(gpu)}
 
 
-def make_batches(dev, netif, *, n, rotate, rank, length=64, size_mode=0, proto_mode=0, strided=False):
+def make_batches(dev, netif, *, n, rotate, rank, length=64, size_mode=0, proto_mode=0, strided=False,
+                 mutate_shift=0):
     from halo_amd import synth
 
     batches = []
     for b in range(rotate):
         first = shard_first_index(rank, b, n, rotate)
         lay = synth.layout(n, length=length, size_mode=size_mode, proto_mode=proto_mode, first_index=first,
-                           ragged=not strided)
+                           ragged=not strided, mutate_shift=mutate_shift)
         fr = synth.frames_device(lay, netif, device=dev, stride=length if strided else 0)
         fr["layout"] = lay
         batches.append(fr)
@@ -266,7 +267,7 @@ def bench_lib():
         vp = ctypes.c_void_p
         L.halo_bench_steps.restype = ctypes.c_int
         L.halo_bench_steps.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
-                                       ctypes.c_uint32, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp,
+                                       ctypes.c_uint32, vp, ctypes.c_uint32, vp, vp, ctypes.c_int, ctypes.c_int, vp,
                                        ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
         L.halo_bench_tx_steps.restype = ctypes.c_int
         L.halo_bench_tx_steps.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_uint32,
@@ -283,6 +284,10 @@ def bench_lib():
         u64 = ctypes.c_uint64
         L.halo_bench_read_peak.restype = ctypes.c_int
         L.halo_bench_read_peak.argtypes = [vp, u64, vp] + tail
+        L.halo_bench_read_probe.restype = ctypes.c_int
+        L.halo_bench_read_probe.argtypes = [vp, u64, vp, i32] + tail
+        L.halo_bench_read_probe_name.restype = ctypes.c_char_p
+        L.halo_bench_read_probe_name.argtypes = [i32]
         L.halo_bench_rx_flow_steps.restype = ctypes.c_int
         L.halo_bench_rx_flow_steps.argtypes = [i32, vp, vp, vp, u32, u32, vp, u32, vp, u32, u32, vp, u32, vp] + tail
         L.halo_bench_stream_rw.restype = ctypes.c_int
@@ -294,11 +299,16 @@ def bench_lib():
         L.halo_bench_ring_polls.restype = ctypes.c_int
         L.halo_bench_ring_polls.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, i32, i32, vp,
                                             ctypes.POINTER(ctypes.c_uint32)]
+        L.halo_bench_multi_steps.restype = ctypes.c_int
+        L.halo_bench_multi_steps.argtypes = [i32, vp, vp, vp, u32, u32, u32, vp, u32, vp, vp] + tail
+        L.halo_bench_host_calls.restype = ctypes.c_int
+        L.halo_bench_host_calls.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, i32, i32, vp,
+                                            ctypes.POINTER(ctypes.c_uint32)]
         _BENCH_LIB = L
     return _BENCH_LIB
 
 
-def time_steps(batches, out, netif, *, flags, hint, steps, warmup, d: Dist, strided_len: int = 0):
+def time_steps(batches, out, netif, *, flags, hint, steps, warmup, d: Dist, strided_len: int = 0, hist=None):
     """`steps` hot-path launches, one per batch (cycling), issued back to back by the native loop
     on torch's current stream. Barrier + device sync on both sides. One HIP event pair on that
     stream brackets the timed region. Returns (max-over-ranks wall seconds, average launch
@@ -319,8 +329,8 @@ def time_steps(batches, out, netif, *, flags, hint, steps, warmup, d: Dist, stri
     torch.cuda.synchronize()
     d.barrier()
     rc = bench_lib().halo_bench_steps(nb, b_bytes, b_offs, b_lens, batches[0]["layout"]["n"], strided_len,
-                                      strided_len, flags, ctypes.addressof(netif), hint, out.data_ptr(), warmup,
-                                      steps, torch.cuda.current_stream().cuda_stream, ctypes.byref(region),
+                                      strided_len, flags, ctypes.addressof(netif), hint, out.data_ptr(),
+                                      None if hist is None else hist.data_ptr(), warmup, steps, torch.cuda.current_stream().cuda_stream, ctypes.byref(region),
                                       ctypes.byref(wall))
     _lib.check("halo_bench_steps", rc)
     torch.cuda.synchronize()
@@ -853,22 +863,152 @@ def ring_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = False):
     return res
 
 
+DROPIN_SIZES = (1, 32, 99, 256, 1024, 4096)  # frames per call: single-frame Parse*, .., PacketHandle's 99
+
+
+def dropin_small_batch(dev, netif, with_cpu: bool = True) -> dict:
+    """The drop-in surface at the reference's own cadence. go/gpurx Ctx.ParseBatch —
+    what the batched PacketHandle (go/engine, DrainEvery 99 caps a batch at 99 polls) and, with one
+    frame, the single-frame Parse* wrappers call — is halo_rx_parse_batch_host + halo_rx_dispatch over
+    frames in pageable host memory (Go slices). Timed per call from native code
+    (tools/bench_loop.hip halo_bench_host_calls) at 1..4096 config-2 frames per call, on the
+    launched path (chunked DMA + kernel + D2H + stream synchronisation) and on the resident path
+    (halo_rx_host_ctx_set_resident: frames packed into pinned staging, one request to a resident
+    consumer). Beside it, the reference's cost for the same frames: the one-core C port's per-frame
+    time x frames (the Go loop has no per-batch cost), and the batch size where the GPU call
+    becomes cheaper (crossover)."""
+    import ctypes
+
+    import numpy as np
+
+    from halo_amd import synth
+    from halo_amd._lib import RESULT_DTYPE
+    from halo_amd.engine import HostBatcher
+
+    mmax = max(DROPIN_SIZES)
+    lay = synth.layout(mmax, length=64)
+    host = synth.frames_device(lay, netif, device=dev)["bytes"].cpu().numpy().copy()  # pageable, like Go's heap
+    offs = lay["offsets_dw"].astype(np.uint64) * 4
+    lens = np.ascontiguousarray(lay["lens"])
+    out = np.zeros(mmax, RESULT_DTYPE)
+    acts = np.zeros(mmax, np.uint8)
+    res = {"what": "halo_rx_parse_batch_host + halo_rx_dispatch per call over m pageable 64 B frames "
+                   "(go/gpurx Ctx.ParseBatch; m = 1 is the single-frame Parse* path), native loop, "
+                   "per-call wall time (median / p10 / p90 of the calls)"}
+    for path in ("launched", "resident"):
+        hb = HostBatcher(dev.index or 0)
+        if path == "resident":
+            hb.set_resident(mmax)
+        curve = {}
+        for m in DROPIN_SIZES:
+            iters = 2000 if m <= 256 else 400
+            us = np.zeros(iters, np.float64)
+            bad = ctypes.c_uint32()
+            st0 = hb.stats()
+            from halo_amd import _lib
+
+            _lib.check("halo_bench_host_calls", bench_lib().halo_bench_host_calls(
+                hb._ctx, host.ctypes.data, offs.ctypes.data, lens.ctypes.data, m, 1, ctypes.addressof(netif),
+                out.ctypes.data, acts.ctypes.data, 50, iters, us.ctypes.data, ctypes.byref(bad)))
+            st1 = hb.stats()
+            med = float(np.median(us))
+            pt = {"us_median": round(med, 2), "us_p10": round(float(np.percentile(us, 10)), 2),
+                  "us_p90": round(float(np.percentile(us, 90)), 2), "mpps": round(m / med, 3),
+                  "bad_calls": int(bad.value)}
+            if path == "resident":
+                calls = max(1, st1["resident_calls"] - st0["resident_calls"])
+                pt["per_call_us"] = {k: round((st1[k + "_ns"] - st0[k + "_ns"]) / calls / 1e3, 2)
+                                     for k in ("pack", "wait", "service_gpu")}
+                pt["resident_calls"] = st1["resident_calls"] - st0["resident_calls"]
+            curve[str(m)] = pt
+        hb.close()
+        res[path] = curve
+    if with_cpu:
+        from oracle import oracle as O
+
+        O.build()
+        onet = O.NetIf.make()
+        O.rx_batch(host, lens, onet, 1, offsets_dw=lay["offsets_dw"])  # warm
+        passes, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 2.0:
+            O.rx_batch(host, lens, onet, 1, offsets_dw=lay["offsets_dw"])
+            passes += 1
+        ns = (time.perf_counter() - t0) / (passes * mmax) * 1e9
+        res["cpu_port_ns_per_frame"] = round(ns, 2)
+        res["cpu_port_us_per_call"] = {str(m): round(m * ns / 1e3, 3) for m in DROPIN_SIZES}
+        res["cpu_note"] = ("oracle/halo_rx_oracle.c -O2 on one core over the same frames (the reference is Go, "
+                           "one goroutine per NetIf; its loop has no per-batch cost, so a call of m frames costs "
+                           "m x the per-frame time)")
+        # crossover: fit the resident curve t(m) = a + b m and solve a + b m = c m (c = CPU per frame)
+        ms = np.array(DROPIN_SIZES, np.float64)
+        t = np.array([res["resident"][str(m)]["us_median"] for m in DROPIN_SIZES])
+        b, a = np.polyfit(ms, t, 1)
+        c = ns / 1e3
+        res["resident_fit_us"] = {"fixed": round(float(a), 3), "per_frame": round(float(b), 5)}
+        res["crossover_frames"] = round(float(a / (c - b)), 1) if c > b else None
+        beats = [m for m in DROPIN_SIZES if res["resident"][str(m)]["us_median"] < m * c]
+        res["smallest_measured_batch_faster_than_cpu"] = min(beats) if beats else None
+    return res
+
+
+STATUS_NAMES = ("OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_PROTO", "IP_HDR_CKSUM",
+                "IP_TOTLEN_UNDERFLOW", "IP_TOTLEN_OVERRUN", "L4_LEN", "ICMP_TYPE", "ICMP_CODE", "L4_CKSUM")
+
+
+def batch_stream_secondary(batches, netif, steps: int, warmup: int, d: Dist, headline_ms: float, k: int = 8) -> dict:
+    """The headline's batch stream, k batches per launch (halo_rx_parse_batches_device): each
+    batch keeps its own records (k record arrays), the batches rotate as in the headline."""
+    import ctypes
+
+    import torch
+
+    n = batches[0]["layout"]["n"]
+    nb = len(batches)
+    arr = lambda xs: (ctypes.c_void_p * len(xs))(*xs)  # noqa: E731
+    outs = [torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=batches[0]["bytes"].device) for _ in range(k)]
+    st = max(10, steps // k)
+    w, km = time_native(bench_lib().halo_bench_multi_steps, nb, arr([b["bytes"].data_ptr() for b in batches]),
+                        arr([b["offsets_dw"].data_ptr() for b in batches]), arr([b["lens"].data_ptr() for b in batches]),
+                        n, k, 1, ctypes.addressof(netif), 64, arr([o.data_ptr() for o in outs]), None, steps=st,
+                        warmup=max(2, warmup // k), d=d)
+    fb = frame_bytes(batches[0])
+    alg = k * (fb + n * (4 + 2 + RESULT_BYTES))
+    res = {"batches_per_launch": k, "frames_per_launch": k * n, "launches": st, "mpps": round(k * n * st / w / 1e6, 1),
+           "kernel_ms": round(km, 5), "ms_per_batch": round(km / k, 5),
+           "vs_headline_per_batch": round(headline_ms / (km / k), 4),
+           "roofline": roofline(alg, km, frame_bytes=k * fb), "alg_bytes_per_launch": alg,
+           "kernel": "rx_lane_multi_kernel<0> (the lane kernel's window code, k batches' windows in one grid)",
+           "what": f"config 2's rotating 1M-frame batches handed over {k} per call (halo_rx_parse_batches_device); "
+                   "records per batch identical to the headline's one-launch-per-batch steps"}
+    del outs
+    return res
+
+
 MEASURED_READ_GBS = None  # set by measure_read_peak() on this box
+MEASURED_READ_PROBES = {}  # every probe shape's GB/s
 
 
-def measure_read_peak(dev, d: Dist, gib: int = 2):
-    """A read-only streaming kernel over `gib` GiB (8x the Infinity Cache): this box's achievable
-    HBM read bandwidth, the second peak SURVEY.md §8d asks the roofline to be reported against."""
+def measure_read_peak(dev, d: Dist, gib: int = 4):
+    """Read-only streaming kernels over `gib` GiB (16x the Infinity Cache): this box's achievable
+    HBM read bandwidth, the second peak SURVEY.md §8d asks the roofline to be reported against —
+    the fastest of a family of probe shapes (one 64 KB tile per block or persistent blocks; 64 to
+    1024 threads; 4 to 16 16-byte loads in flight per lane; plain and non-temporal loads), each
+    timed over 20 launches."""
     import torch
 
     global MEASURED_READ_GBS
     nbytes = gib << 30
     buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     buf.fill_(1)
-    sink = torch.zeros(256 * 16, dtype=torch.int32, device=dev)
-    w, k = time_native(bench_lib().halo_bench_read_peak, buf.data_ptr(), nbytes, sink.data_ptr(), steps=20,
-                       warmup=3, d=d)
-    MEASURED_READ_GBS = round(nbytes / (k * 1e-3) / 1e9, 1)
+    sink = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+    L = bench_lib()
+    v = 0
+    while L.halo_bench_read_probe_name(v) is not None:
+        w, k = time_native(L.halo_bench_read_probe, buf.data_ptr(), nbytes, sink.data_ptr(), v, steps=20, warmup=3,
+                           d=d)
+        MEASURED_READ_PROBES[L.halo_bench_read_probe_name(v).decode()] = round(nbytes / (k * 1e-3) / 1e9, 1)
+        v += 1
+    MEASURED_READ_GBS = max(MEASURED_READ_PROBES.values())
     del buf
     torch.cuda.empty_cache()
     return MEASURED_READ_GBS
@@ -901,10 +1041,14 @@ def with_probe(r: dict, probe_ms: float, kernel_ms: float) -> dict:
     return r
 
 
-def roofline(alg_bytes_per_launch, kernel_ms, traffic=None):
+def roofline(alg_bytes_per_launch, kernel_ms, traffic=None, frame_bytes=None):
+    """`frame_bytes` (the frames' own bytes per launch, SURVEY §8d's primary R): also report the
+    R-only fraction beside the (R + M + W) one."""
     achieved = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+    if frame_bytes:
+        r["frac_frames_only"] = round(frame_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if MEASURED_READ_GBS:
         r["peak_measured_read"] = MEASURED_READ_GBS
         r["frac_of_measured"] = round(achieved / MEASURED_READ_GBS, 4)
@@ -1086,7 +1230,7 @@ def main():
         "kernel_ms": round(max(per_rank_kms), 5),
         "per_rank_kernel_ms": [round(k, 5) for k in per_rank_kms],
         "kernel": "rx_lane_kernel<0, 0> (lane per frame, ragged, no fused pass)",
-        "roofline": roofline(alg, kern_ms, load_traffic("config2")),
+        "roofline": roofline(alg, kern_ms, load_traffic("config2"), frame_bytes=fbytes),
         "alg_bytes_per_launch": alg,
         "per_rank": ranks,
         "distinct_devices": distinct,
@@ -1120,6 +1264,7 @@ def main():
                                 "size_matched_probe_ms = a no-work kernel streaming "
                                 "the same bytes in and out with perfect access patterns over the same number of "
                                 "rotating buffers (frac_of_size_matched = probe / kernel time)")
+    line["roofline"]["peak_measured_read_probes"] = MEASURED_READ_PROBES
     if d.world == 1 and not args.no_secondary:
         with_probe(line["roofline"], size_matched_probe(dev, fbytes + 6 * n, RESULT_BYTES * n, d, nbuf=args.rotate),
                    kern_ms)
@@ -1138,6 +1283,20 @@ def main():
         algc = fbytes + n * (4 + 2 + 16)
         sec["config2_compact_record16"] = {"mpps": round(n * args.steps / wc / 1e6, 1), "kernel_ms": round(kc, 5),
                                            "roofline": roofline(algc, kc)}
+        # the headline with the §5 metrics output on: every launch counts into a status histogram
+        hist = torch.zeros(14, dtype=torch.int32, device=dev)
+        wh, kh = time_steps(batches, out, netif, flags=1, hint=64, steps=args.steps, warmup=args.warmup, d=d,
+                            hist=hist)
+        hsum = int(hist.sum().item())
+        sec["config2_status_histogram"] = {
+            "mpps": round(n * args.steps / wh / 1e6, 1), "kernel_ms": round(kh, 5), "roofline": roofline(alg, kh),
+            "vs_headline": round(kern_ms / kh, 4), "hist_frames": hsum, "hist_ok": int(hist[0].item()),
+            "what": "the headline step with d_status_hist (block-aggregated in LDS, one atomic per status per block)"}
+        assert hsum == n * (args.steps + args.warmup) and int(hist[0].item()) == hsum
+        # the batch stream handed over 8 batches per launch (halo_rx_parse_batches_device): the ramp
+        # and tail of a 1M-frame launch paid once per 8M frames
+        sec["config2_batch_stream"] = batch_stream_secondary(batches, netif, args.steps, args.warmup, d, kern_ms)
+
         # forward / transmit rewrite (§8f row f2) on the headline frames: DNAT + SNAT + DPDK fill
         import numpy as np
 
@@ -1178,6 +1337,22 @@ def main():
         sec["route_lpm_500k_prefixes"] = route_secondary(dev, max(10, args.steps // 4), 3, d, with_cpu=not args.no_cpu)
         torch.cuda.empty_cache()
         line["config4_128M_one_gpu"] = config4_one_gpu(dev, netif, d, max(20, args.steps // 4), 3)
+        # SURVEY §8d's mutation set: 1/64 of the frames with one bit flipped in [14, L)
+        bm = make_batches(dev, netif, n=n, rotate=8, rank=0, mutate_shift=6)
+        om = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
+        hm = torch.zeros(14, dtype=torch.int32, device=dev)
+        wm, km = time_steps(bm, om, netif, flags=1, hint=64, steps=args.steps, warmup=args.warmup, d=d, hist=hm)
+        fbm = frame_bytes(bm[0])
+        hmn = hm.cpu().numpy().astype(np.int64)
+        sec["config2_mutated_1in64"] = {
+            "mpps": round(n * args.steps / wm / 1e6, 1), "kernel_ms": round(km, 5),
+            "roofline": roofline(fbm + n * (6 + RESULT_BYTES), km, frame_bytes=fbm),
+            "failing_frac": round(float(hmn[1:].sum() / hmn.sum()), 5),
+            "status_hist": {STATUS_NAMES[i]: int(hmn[i]) for i in range(14) if hmn[i]},
+            "what": "config 2 with 1/64 of the frames mutated (one random bit flipped in [14, L) after the checksums "
+                    "were filled, SURVEY §8d), 8 rotating batches, status histogram on"}
+        del bm, om
+        torch.cuda.empty_cache()
         for name, kw, hint, strided_len, flags in [
             ("config4_shard_16M_64B", dict(length=64), 64, 0, 1),
             ("1500B_udp_1M", dict(length=1500), 1500, 0, 1 | _lib.HALO_RX_UNIFORM_LEN),
@@ -1198,7 +1373,10 @@ def main():
             a2 = fb + nn * (meta + RESULT_BYTES)
             sec[name] = {"frames": nn, "mpps": round(nn * steps / w2 / 1e6, 1),
                          "gbit_s": round(fb * steps * 8 / w2 / 1e9, 1), "kernel_ms": round(k2, 4),
-                         "roofline": roofline(a2, k2, load_traffic(name))}
+                         "roofline": roofline(a2, k2, load_traffic(name), frame_bytes=fb)}
+            if "imix" in name:
+                sec[name]["mix"] = ("sizes 64/570/1500 B at 7:4:1; protocols UDP 50 / TCP 40 / ICMP 10 % "
+                                    "(synth proto_mode 3, per frame from the seed)")
             if "config4" in name:
                 sec[name]["what"] = ("one GPU's shard of BASELINE config 4 (128M x 64 B over 8 GPUs = 16M per GPU, "
                                      "index-sharded, no collective); the scaling run itself is bench.py --gpus N")
@@ -1211,6 +1389,8 @@ def main():
         # buffered in 64 MB chunks by halo_rx_parse_batch_host; the frame buffer is registered
         # (pinned in place) so each chunk is one DMA straight from it
         sec.update(e2e_host(dev, netif, steps=max(3, args.steps // 40)))
+        # the drop-in surface at small batch sizes (go/gpurx ParseBatch, single-frame Parse*)
+        sec["dropin_small_batch"] = dropin_small_batch(dev, netif, with_cpu=not args.no_cpu)
         # halo's SPSC packet ring as the source (BASELINE config 1 over a Wire)
         sec.update(ring_secondary(dev, netif, max(10, args.steps // 4), 3, d, with_cpu=not args.no_cpu))
         torch.cuda.empty_cache()

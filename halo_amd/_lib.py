@@ -114,6 +114,9 @@ assert RING_SCAN_DTYPE.itemsize == 24
 # halo_rx_ring_stats_t (8 x u64)
 RING_STATS_DTYPE = np.dtype([(k, "<u8") for k in ("polls", "frames", "small_polls", "service_requests",
                                                   "service_launches", "walk_ns", "wait_ns", "service_gpu_ns")])
+# halo_rx_host_stats_t (8 x u64)
+HOST_STATS_DTYPE = np.dtype([(k, "<u8") for k in ("calls", "frames", "resident_calls", "resident_parked",
+                                                  "service_launches", "pack_ns", "wait_ns", "service_gpu_ns")])
 RING_STOP_NAMES = ("EMPTY", "BAD_LEN", "PARTIAL", "CAPACITY", "MAX", "BAD_CURSOR")
 RING_STOP = {name: code for code, name in enumerate(RING_STOP_NAMES)}
 RING_REGISTER = 0x1
@@ -206,6 +209,15 @@ class NetIf(ctypes.Structure):
         return n
 
 
+class BatchDesc(ctypes.Structure):
+    """halo_rx_batch_desc_t — one batch of halo_rx_parse_batches_device."""
+
+    _fields_ = [("d_bytes", ctypes.c_void_p), ("d_offsets_dw", ctypes.c_void_p), ("d_lens", ctypes.c_void_p),
+                ("d_out", ctypes.c_void_p), ("n", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(BatchDesc) == 40
+
 _u8p = ctypes.c_void_p
 _PROTOS = {
     "halo_rx_version": (ctypes.c_char_p, []),
@@ -218,10 +230,16 @@ _PROTOS = {
     "halo_rx_parse_strided_device": (ctypes.c_int, [
         _u8p, ctypes.c_uint64, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
         ctypes.POINTER(NetIf), _u8p, _u8p, ctypes.c_void_p]),
+    "halo_rx_parse_batches_device": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf), ctypes.c_uint32, _u8p,
+        ctypes.c_void_p]),
     "halo_rx_host_ctx_create": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "halo_rx_host_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "halo_rx_host_ctx_set_zero_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "halo_rx_host_ctx_set_resident": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64]),
+    "halo_rx_host_ctx_set_service_timeout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "halo_rx_host_ctx_get_stats": (ctypes.c_int, [ctypes.c_void_p, _u8p]),
     "halo_rx_parse_batch_host": (ctypes.c_int, [
         ctypes.c_void_p, _u8p, _u8p, _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(NetIf),
         _u8p, _u8p]),
@@ -269,6 +287,7 @@ _PROTOS = {
     "halo_rx_ring_commit": (ctypes.c_int, [ctypes.c_void_p]),
     "halo_rx_ring_get_stats": (ctypes.c_int, [ctypes.c_void_p, _u8p]),
     "halo_rx_ring_set_small_poll": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    "halo_rx_ring_set_service_timeout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     "halo_rx_ring_scan_workspace": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32]),
     "halo_rx_ring_scan_device": (ctypes.c_int, [
         _u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, _u8p, _u8p,

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "halo_amd", "csrc")
 OUT = os.path.join(ROOT, "halo_amd", "lib", "libhalo_rx.so")
 SOURCES = ["rx_parse.hip", "tx_fixup.hip", "tx_build.hip", "deep_nat.hip", "flow_hash.hip", "route_lpm.hip", "synth.hip", "host_path.hip",
-           "ring_rx.hip", "host_logic.cc"]
+           "ring_rx.hip", "resident.hip", "host_logic.cc"]
 # measurement tooling (bench.py's native step loop), linked against the product library
 BENCH_SRC = os.path.join(ROOT, "tools", "bench_loop.hip")
 BENCH_OUT = os.path.join(ROOT, "tools", "libhalo_bench.so")
@@ -32,9 +32,28 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-fvisibility=hidden", "-Wall", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
-           *srcs, "-o", OUT + ".tmp"]
+    obj_dir = os.path.join(ROOT, "build", "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+             "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+    headers_mtime = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), headers_mtime):
+            cmd = [_hipcc(), *flags, "-c", src, "-o", obj + ".tmp"]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+            os.replace(obj + ".tmp", obj)
+        return obj
+
+    from concurrent.futures import ThreadPoolExecutor
+
+    jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS") or os.cpu_count() or 1), 8))
+    with ThreadPoolExecutor(jobs) as ex:  # one hipcc per source file, then one link
+        objs = list(ex.map(compile_one, srcs))
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", *objs, "-o", OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

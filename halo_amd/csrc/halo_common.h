@@ -102,10 +102,57 @@ __host__ __device__ inline uint32_t svc_check(uint32_t seq, uint32_t n, uint32_t
     for (int i = 0; i < 11; ++i) h = (h ^ w[i]) * 0x01000193u;
     return h;
 }
-// Launches the consumer on `s`: it serves requests after `last`, and exits when `stop` is set or
-// after idle_us microseconds without a request.
+// Launches the consumer on `s`: it serves requests after `last`, and exits when `stop` is set, when
+// another of its workgroups has left (*d_quit, device memory, zeroed before the launch), or after
+// idle_us microseconds without a request (the first group to time out sets *d_quit, so the whole
+// grid leaves together instead of one group at a time).
 int launch_ring_service(RingServiceCtl* d_ctl, const uint8_t* d_data, const uint32_t* d_off,
-                        const uint16_t* d_len, uint32_t last, uint32_t idle_us, hipStream_t s);
+                        const uint16_t* d_len, uint32_t* d_quit, uint32_t last, uint32_t idle_us, hipStream_t s);
+
+// ---- resident consumers (resident.hip): one RingServiceCtl + its kernel, driven from the host ----
+// Used by rings attached with HALO_RING_PERSISTENT and by host contexts with a resident consumer
+// (halo_rx_host_ctx_set_resident). The frames of a request live at d_data (+ the u32 dword offsets /
+// u16 lengths at d_off / d_len, or the uniform layout carried in the request line).
+constexpr uint32_t kSvcMaxFrames = 16384;  // larger requests take a full-grid launch
+constexpr uint32_t kSvcIdleUs = 20000;      // the consumer exits after 20 ms without a request
+constexpr int kResidentParked = 1;          // resident_request: not served, launch instead
+struct Resident;
+struct ResidentStats {
+    uint64_t requests;  // requests served
+    uint64_t launches;  // kernel launches (first use, after idle exits, after parks)
+    uint64_t gpu_ns;    // the consumer's own time per request (first group in, last group out), summed
+    uint64_t parked;    // requests refused while a device drain had the consumers parked
+};
+int resident_create(int device, const uint8_t* d_data, const uint32_t* d_off, const uint16_t* d_len,
+                    Resident** out);
+void resident_destroy(Resident* s);
+// Serves n <= kSvcMaxFrames frames into dout (device address). HALO_OK when every group published;
+// kResidentParked when a drain is in progress (nothing was requested: the caller launches); HALO_E_HIP
+// when the wait passed the timeout — the request is retired first (the consumer is stopped and its
+// kernel has ended), so nothing is written to dout after the call returns.
+int resident_request(Resident* s, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif, halo_rx_result_t* dout,
+                     uint32_t uni_off, uint32_t uni_stride, uint32_t uni_len);
+void resident_set_timeout(Resident* s, uint64_t us);  // 0: the default (2 s)
+ResidentStats resident_stats(const Resident* s);
+// While one lives, the resident consumers of `device` are stopped (their kernels have ended) and new
+// requests take the launch path. Every library call that frees device or pinned memory or
+// synchronises the whole device runs under one: hipFree / hipHostFree / hipDeviceSynchronize wait
+// for every kernel on the device, and a resident kernel ends only 20 ms after its last request —
+// never, while another thread keeps polling it.
+class ParkResidents {
+  public:
+    explicit ParkResidents(int device);
+    ~ParkResidents();
+    ParkResidents(const ParkResidents&) = delete;
+    ParkResidents& operator=(const ParkResidents&) = delete;
+
+  private:
+    int device_;
+};
+// hipDeviceSynchronize on `device` under a ParkResidents.
+int drain_device(int device);
+// The calling thread's current device (0 if none).
+int current_device();
 
 // Live host registrations made through this library (halo_rx_host_register and
 // halo_rx_ring_attach(HALO_RING_REGISTER)), over RegMap (host_logic.h): page-aligned whole pages,

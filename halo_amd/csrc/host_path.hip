@@ -6,8 +6,10 @@
 
 #include <unistd.h>
 
-#include <atomic>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <utility>
@@ -45,18 +47,27 @@ int check_device() {
 namespace {
 // Waits for all work this library queued on any device: a DMA or kernel still reading or
 // writing the range must finish before its pages are unpinned.
+// Resident consumers are stopped first (ParkResidents, held by the caller): their kernels would
+// otherwise keep the device busy until they idle out, or forever while another thread keeps polling
+// (ADVICE r3).
 int sync_used_devices() {
     const uint64_t used = g_devices_used.load(std::memory_order_relaxed);
-    if (!used) return HALO_OK;
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess) return HALO_E_HIP;
     int rc = HALO_OK;
     for (int d = 0; d < 64; ++d)
         if ((used >> d) & 1)
-            if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = HALO_E_HIP;
-    (void)hipSetDevice(cur);
+            if (drain_device(d) != HALO_OK) rc = HALO_E_HIP;
     return rc;
 }
+
+// The resident consumers of every device this library launched on, parked for a scope.
+struct ParkUsed {
+    std::vector<std::unique_ptr<ParkResidents>> parks;
+    ParkUsed() {
+        const uint64_t used = g_devices_used.load(std::memory_order_relaxed);
+        for (int d = 0; d < 64; ++d)
+            if ((used >> d) & 1) parks.emplace_back(new ParkResidents(d));
+    }
+};
 
 // True while the runtime still maps host address p for the device.
 bool runtime_maps(void* p) {
@@ -81,6 +92,7 @@ int host_reg_add(void* base, uint64_t bytes, HostRegKind kind) {
     const uintptr_t b = reinterpret_cast<uintptr_t>(base);
     int rc = registry().reserve(b, bytes, host_page_size(), kind);
     if (rc) return rc;
+    ParkUsed park;  // hipHostRegister may wait for the device
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
         (void)hipGetLastError();
@@ -114,6 +126,7 @@ void* host_reg_device_view(const void* p, uint64_t bytes) {
 int host_reg_remove(void* base, HostRegKind kind) {
     const uintptr_t b = reinterpret_cast<uintptr_t>(base);
     if (!registry().begin_remove(b, kind)) return HALO_E_INVAL;  // not a live base of this kind
+    ParkUsed park;                                                // through the unregistration
     int rc = sync_used_devices();                                 // the pages stay pinned on failure
     if (rc == HALO_OK && hipHostUnregister(base) != hipSuccess) {
         (void)hipGetLastError();
@@ -136,6 +149,22 @@ extern "C" HALO_API int halo_rx_init(int device) {
 
 // ---- host-memory batch path ---------------------------------------------------------------
 struct halo_rx_host_ctx {
+    // halo_rx_host_ctx_set_resident: batches of up to max_frames frames / max_bytes bytes are packed
+    // into pinned staging and served by a resident consumer (no launch, no stream synchronisation)
+    struct Resident {
+        halo::Resident* svc = nullptr;
+        uint32_t max_frames = 0;
+        uint64_t max_bytes = 0;
+        uint8_t* h_bytes = nullptr;  // pinned; d_* are the device's addresses of the same memory
+        uint8_t* d_bytes = nullptr;
+        uint32_t* h_off = nullptr;
+        uint32_t* d_off = nullptr;
+        uint16_t* h_len = nullptr;
+        uint16_t* d_len = nullptr;
+        halo_rx_result_t* h_res = nullptr;
+        halo_rx_result_t* d_res = nullptr;
+    } res;
+    halo_rx_host_stats_t stats{};
     int device;
     uint32_t chunk_frames;
     uint32_t zc_frames;  // chunk of the zero-copy path with GPU-converted metadata (no host staging)
@@ -163,7 +192,31 @@ struct halo_rx_host_ctx {
 };
 
 namespace {
+void free_resident(halo_rx_host_ctx::Resident& r) {
+    halo::resident_destroy(r.svc);  // stops the consumer and waits for its kernel to end
+    if (r.h_bytes) (void)hipHostFree(r.h_bytes);
+    if (r.h_off) (void)hipHostFree(r.h_off);
+    if (r.h_len) (void)hipHostFree(r.h_len);
+    if (r.h_res) (void)hipHostFree(r.h_res);
+    r = halo_rx_host_ctx::Resident{};
+}
+
+template <typename T>
+bool pinned_mapped(T** h, T** d, uint64_t bytes) {
+    void* p = nullptr;
+    void* dv = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocMapped) != hipSuccess) return false;
+    *h = static_cast<T*>(p);
+    if (hipHostGetDevicePointer(&dv, p, 0) != hipSuccess || !dv) {
+        (void)hipGetLastError();
+        return false;
+    }
+    *d = static_cast<T*>(dv);
+    return true;
+}
+
 void free_ctx(halo_rx_host_ctx* c) {
+    free_resident(c->res);
     for (auto& s : c->slot) {
         if (s.stream) (void)hipStreamDestroy(s.stream);
         if (s.h_bytes) (void)hipHostFree(s.h_bytes);
@@ -220,6 +273,7 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
     if (chunk_bytes < 65536) return HALO_E_INVAL;
     auto* c = new (std::nothrow) halo_rx_host_ctx;
     if (!c) return HALO_E_NOMEM;
+    halo::ParkResidents park(device);  // pinned allocations (and a failed create's frees)
     c->device = device;
     c->chunk_frames = chunk_frames;
     // zero-copy chunks with GPU-converted metadata stage nothing on the host, so they can be
@@ -257,11 +311,64 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
 extern "C" HALO_API int halo_rx_host_ctx_destroy(halo_rx_host_ctx_t* ctx) {
     if (!ctx) return HALO_E_INVAL;
     (void)hipSetDevice(ctx->device);
+    halo::ParkResidents park(ctx->device);  // hipFree / hipHostFree wait for every kernel on the device
     for (auto& s : ctx->slot)
         if (s.stream) (void)hipStreamSynchronize(s.stream);
     free_ctx(ctx);
     return HALO_OK;
 }
+
+namespace {
+using clk = std::chrono::steady_clock;
+uint64_t ns_between(clk::time_point a, clk::time_point b) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+}
+
+// The resident path of halo_rx_parse_batch_host: the frames are packed into the context's pinned
+// staging (4-byte aligned starts; frames over the length cap are not copied, their verdict needs no
+// byte), and one request to the resident consumer parses them there over PCIe and writes the records
+// into `out` directly when it is registered, else into pinned staging that is copied out. A batch
+// whose frames all have one length travels as the uniform layout (frame i at i * stride: the consumer
+// reads no offset / length arrays). Returns 1 when the frames do not fit the staging area (the caller
+// takes the chunked path). With the consumer parked by a device drain, the same staging is parsed by
+// one launch instead.
+int resident_batch(halo_rx_host_ctx* c, const uint8_t* bytes, const uint64_t* offsets, const uint16_t* lens,
+                   uint32_t n, uint32_t flags, uint32_t cap, const halo_rx_netif_t* netif, halo_rx_result_t* out,
+                   uint32_t* status_hist) {
+    auto& R = c->res;
+    const auto t0 = clk::now();
+    uint64_t used = 0;
+    if (halo::pack_chunk(bytes, offsets, lens, n, 0, n, R.max_bytes, cap, R.h_bytes, R.h_off, R.h_len, &used) != n)
+        return 1;
+    uint32_t ulen = lens[0], ustride = 0;
+    for (uint32_t i = 1; i < n && ulen; ++i) ulen = lens[i] == ulen ? ulen : 0u;
+    if (ulen > cap || (flags & HALO_RX_L3_START)) ulen = 0;  // the strided layout has no L3 form
+    if (ulen) ustride = (ulen + 3u) >> 2;                      // pack_chunk laid them i * stride apart
+    const uint64_t rb = sizeof(halo_rx_result_t) * (uint64_t)n;
+    auto* dout = static_cast<halo_rx_result_t*>(halo::host_reg_device_view(out, rb));
+    if (reinterpret_cast<uintptr_t>(dout) & 15u) dout = nullptr;
+    halo_rx_result_t* dst = dout ? dout : R.d_res;
+    const auto t1 = clk::now();
+    int rc = halo::resident_request(R.svc, n, flags & ~HALO_RX_VARIANT_MASK, netif, dst, 0u, ustride, ulen);
+    if (rc == halo::kResidentParked) {
+        hipStream_t st = c->slot[0].stream;  // idle between calls: the API is synchronous
+        rc = ulen ? halo_rx_parse_strided_device(R.d_bytes, 4ull * ustride, nullptr, ulen, n, flags, netif, dst,
+                                                 nullptr, st)
+                  : halo_rx_parse_batch_device(R.d_bytes, R.d_off, R.d_len, n, flags, netif, 0, dst, nullptr, st);
+        if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = HALO_E_HIP;
+        ++c->stats.resident_parked;
+    }
+    const auto t2 = clk::now();
+    c->stats.pack_ns += ns_between(t0, t1);
+    c->stats.wait_ns += ns_between(t1, t2);
+    if (rc) return rc;
+    ++c->stats.resident_calls;
+    if (!dout) memcpy(out, R.h_res, rb);
+    if (status_hist)
+        for (uint32_t i = 0; i < n; ++i) ++status_hist[out[i].status];  // the statuses the kernel wrote
+    return HALO_OK;
+}
+}  // namespace
 
 extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* bytes,
                                                  const uint64_t* offsets, const uint16_t* lens, uint32_t n,
@@ -271,9 +378,18 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
     if (n == 0) return HALO_OK;
     if (!bytes || !offsets || !lens || !out) return HALO_E_INVAL;
     if (flags & HALO_RX_RECORD_COMPACT) return HALO_E_INVAL;  // host path returns full records
+    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_UNIFORM_LEN | HALO_RX_L3_START |
+                  HALO_RX_VARIANT_MASK))
+        return HALO_E_INVAL;
     if (hipSetDevice(ctx->device) != hipSuccess) return HALO_E_NODEV;
     const uint32_t cap = (flags & HALO_RX_L3_START) ? ((flags & HALO_RX_JUMBO_EXT) ? halo::kIpMaxJumbo : halo::kIpMax)
                                                     : ((flags & HALO_RX_JUMBO_EXT) ? halo::kEthMaxJumbo : halo::kEthMax);
+    ++ctx->stats.calls;
+    ctx->stats.frames += n;
+    if (ctx->res.svc && n <= ctx->res.max_frames) {
+        const int r = resident_batch(ctx, bytes, offsets, lens, n, flags, cap, netif, out, status_hist);
+        if (r <= 0) return r;  // 1: larger than the staging area -> the chunked path below
+    }
     int rc = HALO_OK;
     std::vector<std::pair<uint64_t, uint32_t>> redo;  // zero-copy chunks to re-parse on the DMA path
     auto drain = [&](halo_rx_host_ctx::Slot& s) -> int {
@@ -433,6 +549,48 @@ extern "C" HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const 
         ctx->zero_copy = true;
     }
     return rc;
+}
+
+extern "C" HALO_API int halo_rx_host_ctx_set_resident(halo_rx_host_ctx_t* ctx, uint32_t max_frames,
+                                                      uint64_t max_bytes) {
+    if (!ctx) return HALO_E_INVAL;
+    if (max_frames > halo::kSvcMaxFrames || max_bytes > (64ull << 20)) return HALO_E_INVAL;
+    if (hipSetDevice(ctx->device) != hipSuccess) return HALO_E_NODEV;
+    halo::ParkResidents park(ctx->device);  // frees and pinned allocations below
+    free_resident(ctx->res);
+    if (max_frames == 0) return HALO_OK;
+    if (max_bytes == 0) max_bytes = std::min<uint64_t>(1516ull * max_frames, 4ull << 20);
+    max_bytes = (max_bytes + 3) & ~3ull;
+    auto& R = ctx->res;
+    bool ok = pinned_mapped(&R.h_bytes, &R.d_bytes, max_bytes + 64) &&  // + a dword tail any load may cover
+              pinned_mapped(&R.h_off, &R.d_off, 4ull * max_frames) && pinned_mapped(&R.h_len, &R.d_len, 2ull * max_frames) &&
+              pinned_mapped(&R.h_res, &R.d_res, sizeof(halo_rx_result_t) * (uint64_t)max_frames);
+    ok = ok && halo::resident_create(ctx->device, R.d_bytes, R.d_off, R.d_len, &R.svc) == HALO_OK;
+    if (!ok) {
+        free_resident(R);
+        return HALO_E_NOMEM;
+    }
+    memset(R.h_bytes, 0, max_bytes + 64);
+    R.max_frames = max_frames;
+    R.max_bytes = max_bytes;
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_host_ctx_set_service_timeout(halo_rx_host_ctx_t* ctx, uint64_t us) {
+    if (!ctx || !ctx->res.svc) return HALO_E_INVAL;
+    halo::resident_set_timeout(ctx->res.svc, us);
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_host_ctx_get_stats(const halo_rx_host_ctx_t* ctx, halo_rx_host_stats_t* out) {
+    if (!ctx || !out) return HALO_E_INVAL;
+    *out = ctx->stats;
+    if (ctx->res.svc) {
+        const halo::ResidentStats s = halo::resident_stats(ctx->res.svc);
+        out->service_launches = s.launches;
+        out->service_gpu_ns = s.gpu_ns;
+    }
+    return HALO_OK;
 }
 
 extern "C" HALO_API int halo_rx_host_ctx_set_zero_copy(halo_rx_host_ctx_t* ctx, int enable) {

@@ -520,31 +520,18 @@ struct halo_rx_ring {
     uint32_t* d_soff = nullptr;
     uint16_t* d_slen = nullptr;
     halo_rx_result_t* d_sres = nullptr;
-    // HALO_RING_PERSISTENT: the resident small-poll consumer (rx_parse.hip ring_service_kernel)
-    halo::RingServiceCtl* svc = nullptr;    // pinned, coherent
-    halo::RingServiceCtl* d_svc = nullptr;  // its device address
-    hipStream_t s_svc = nullptr;
-    uint32_t svc_seq = 0;                   // the last request made
-    bool svc_launched = false;
-    std::chrono::steady_clock::time_point svc_last{};  // when the last request completed
+    // HALO_RING_PERSISTENT: the resident small-poll consumer (resident.hip, rx_parse.hip
+    // ring_service_kernel) over the ring's data area and the pinned offset / length arrays
+    halo::Resident* svc = nullptr;
     halo_rx_ring_stats_t stats{};
 };
 
 namespace {
 // Returns false when the ring memory could not be unregistered (the caller must not free it then:
 // the pages stay mapped for the device).
-// Stops the resident consumer (if any) and waits for its kernel to end.
-void stop_service(halo_rx_ring* r) {
-    if (!r->svc) return;
-    __atomic_store_n(&r->svc->stop, 1u, __ATOMIC_RELEASE);
-    if (r->s_svc) (void)hipStreamSynchronize(r->s_svc);
-    r->svc_launched = false;
-}
-
 bool free_ring(halo_rx_ring* r) {
-    stop_service(r);
-    if (r->s_svc) (void)hipStreamDestroy(r->s_svc);
-    if (r->svc) (void)hipHostFree(r->svc);
+    halo::ParkResidents park(r->device);  // hipFree / hipHostFree wait for every kernel on the device
+    halo::resident_destroy(r->svc);      // stops the consumer and waits for its kernel to end
     for (hipEvent_t e : r->ev)
         if (e) (void)hipEventDestroy(e);
     if (r->s_copy) (void)hipStreamDestroy(r->s_copy);
@@ -585,6 +572,7 @@ void* device_view(const void* p, uint64_t bytes) {
 int alloc_small(halo_rx_ring* r, uint64_t bytes) {
     const uint32_t frames = (uint32_t)std::min<uint64_t>(bytes / 8, r->max_frames);
     if (frames > r->small_frames) {
+        halo::ParkResidents park(r->device);
         if (r->h_soff) (void)hipHostFree(r->h_soff);
         if (r->h_slen) (void)hipHostFree(r->h_slen);
         if (r->h_sres) (void)hipHostFree(r->h_sres);
@@ -602,75 +590,6 @@ int alloc_small(halo_rx_ring* r, uint64_t bytes) {
         r->small_frames = frames;
     }
     r->small = bytes;
-    return HALO_OK;
-}
-
-constexpr uint32_t kSvcMaxFrames = 16384;  // larger small polls take a full-grid launch
-constexpr uint32_t kSvcIdleUs = 20000;      // the resident consumer exits after 20 ms without a request
-
-// One request to the resident consumer: the frames' offsets / lengths are already in the pinned
-// arrays it reads (d_soff / d_slen). Fields and their check first, then req_seq with release; spin
-// until every group's done_seq slot holds it. A
-// consumer that went idle (or exited between its last check and the request) is relaunched: the
-// stream says whether its kernel is still running. Every wait is bounded.
-int service_request(halo_rx_ring* r, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
-                    halo_rx_result_t* dout, uint32_t uni_off, uint32_t uni_stride, uint32_t uni_len) {
-    using clk = std::chrono::steady_clock;
-    halo::RingServiceCtl* c = r->svc;
-    const uint32_t seq = r->svc_seq + 1;
-    const uint64_t out = reinterpret_cast<uint64_t>(dout);
-    c->n = n;
-    c->flags = flags;
-    c->mac_lo = (uint32_t)netif->mac[0] | ((uint32_t)netif->mac[1] << 8) | ((uint32_t)netif->mac[2] << 16) |
-                ((uint32_t)netif->mac[3] << 24);
-    c->mac_hi = (uint32_t)netif->mac[4] | ((uint32_t)netif->mac[5] << 8);
-    c->own_ip = netif->ip;
-    c->out_lo = (uint32_t)out;
-    c->out_hi = (uint32_t)(out >> 32);
-    c->uni_off = uni_off;
-    c->uni_stride = uni_stride;
-    c->uni_len = uni_len;
-    __atomic_store_n(&c->check, halo::svc_check(seq, n, flags, c->mac_lo, c->mac_hi, c->own_ip, c->out_lo, c->out_hi,
-                                                uni_off, uni_stride, uni_len),
-                     __ATOMIC_RELEASE);
-    auto launch = [&](uint32_t last) {
-        r->svc_launched = halo::launch_ring_service(r->d_svc, r->d_data, r->d_soff, r->d_slen, last, kSvcIdleUs,
-                                                    r->s_svc) == HALO_OK;
-        r->stats.service_launches += r->svc_launched;
-        return r->svc_launched;
-    };
-    // idle past half the timeout: the kernel may have exited; ask the stream (cheap, rare)
-    if (!r->svc_launched ||
-        (clk::now() - r->svc_last > std::chrono::microseconds(kSvcIdleUs / 2) && hipStreamQuery(r->s_svc) == hipSuccess)) {
-        if (!launch(r->svc_seq)) return HALO_E_HIP;
-    }
-    r->svc_seq = seq;
-    __atomic_store_n(&c->req_seq, seq, __ATOMIC_RELEASE);
-    const auto t0 = clk::now();
-    auto t_check = t0;
-    for (uint32_t k = 1;; ++k) {
-        uint32_t done = 0;
-        for (uint32_t g = 0; g < halo::kSvcGroups; ++g) done += __atomic_load_n(&c->done_seq[g], __ATOMIC_ACQUIRE) == seq;
-        if (done == halo::kSvcGroups) break;
-        __builtin_ia32_pause();
-        if ((k & 255u) == 0) {
-            const auto now = clk::now();
-            if (now - t_check > std::chrono::milliseconds(2)) {
-                t_check = now;
-                // the kernel ended before it saw this request (idle exit racing it): start another
-                if (hipStreamQuery(r->s_svc) == hipSuccess && !launch(seq - 1)) return HALO_E_HIP;
-            }
-            if (now - t0 > std::chrono::seconds(2)) return HALO_E_HIP;  // never wait forever
-        }
-    }
-    r->svc_last = clk::now();
-    ++r->stats.service_requests;
-    uint64_t seen = c->t_seen[0], fin = c->t_done[0];
-    for (uint32_t g = 1; g < halo::kSvcGroups; ++g) {
-        seen = std::min(seen, c->t_seen[g]);
-        fin = std::max(fin, c->t_done[g]);
-    }
-    r->stats.service_gpu_ns += (fin - seen) * 10u;  // 100 MHz ticks: first group in to last group out
     return HALO_OK;
 }
 
@@ -712,11 +631,11 @@ int small_poll(halo_rx_ring* r, uint64_t used, uint32_t flags, const halo_rx_net
         const uint32_t stride = (4u + max_len + 3u) >> 2;
         const bool uni = w.min_len == max_len &&
                          (int64_t)r->h_soff[n - 1] - (int64_t)r->h_soff[0] == (int64_t)(n - 1) * stride;
-        int rc;
-        if (r->svc && n <= kSvcMaxFrames) {
-            rc = service_request(r, n, flags, netif, dout ? dout : r->d_sres, uni ? r->h_soff[0] : 0u,
-                                 uni ? stride : 0u, uni ? max_len : 0u);
-        } else {
+        int rc = halo::kResidentParked;
+        if (r->svc && n <= halo::kSvcMaxFrames)
+            rc = halo::resident_request(r->svc, n, flags, netif, dout ? dout : r->d_sres, uni ? r->h_soff[0] : 0u,
+                                        uni ? stride : 0u, uni ? max_len : 0u);
+        if (rc == halo::kResidentParked) {  // no resident consumer, or a device drain has it parked
             rc = uni ? halo_rx_parse_strided_device(r->d_data + 4ull * r->h_soff[0], 4ull * stride, nullptr, max_len, n,
                                                     flags, netif, dout ? dout : r->d_sres, nullptr, r->s_comp)
                      : halo_rx_parse_batch_device(r->d_data, r->d_soff, r->d_slen, n, flags, netif, max_len,
@@ -800,6 +719,7 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     if (max_bytes < 8) return HALO_E_INVAL;
     if (max_frames == 0 || max_frames > max_bytes / 8) max_frames = (uint32_t)std::min<uint64_t>(max_bytes / 8, 0xFFFFFFFFull);
     if ((rc = halo_rx_init(device))) return rc;
+    halo::ParkResidents park(device);  // allocations, registration (and a failed attach's frees)
     auto* r = new (std::nothrow) halo_rx_ring;
     if (!r) return HALO_E_NOMEM;
     r->device = device;
@@ -822,8 +742,10 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     ok = ok && hipMalloc((void**)&r->d_len, 2ull * max_frames) == hipSuccess;
     ok = ok && hipMalloc((void**)&r->d_res, sizeof(halo_rx_result_t) * (uint64_t)max_frames) == hipSuccess;
     ok = ok && hipMalloc((void**)&r->d_hist, 4 * HALO_RX_STATUS_COUNT) == hipSuccess;
-    ok = ok && hipMemset(r->d_hist, 0, 4 * HALO_RX_STATUS_COUNT) == hipSuccess &&
-         hipDeviceSynchronize() == hipSuccess;  // complete before any non-blocking stream counts into it
+    // complete before any non-blocking stream counts into it (a stream wait, not a device drain: a
+    // resident consumer elsewhere on the device would hold a device synchronisation for 20 ms)
+    ok = ok && hipMemsetAsync(r->d_hist, 0, 4 * HALO_RX_STATUS_COUNT, r->s_comp) == hipSuccess &&
+         hipStreamSynchronize(r->s_comp) == hipSuccess;
     ok = ok && hipMalloc((void**)&r->d_info, sizeof(halo_rx_ring_scan_t)) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&r->h_info, sizeof(halo_rx_ring_scan_t), hipHostMallocDefault) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&r->h_off, 4ull * max_frames, hipHostMallocDefault) == hipSuccess;
@@ -836,18 +758,8 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
             r->d_data = static_cast<uint8_t*>(device_view(r->data, size));
             ok = !r->d_data || alloc_small(r, halo::kSmallPoll) == HALO_OK;
         }
-        if (ok && (attach_flags & HALO_RING_PERSISTENT) && r->d_data) {
-            void* cp = nullptr;
-            ok = hipHostMalloc(&cp, sizeof(halo::RingServiceCtl), hipHostMallocCoherent | hipHostMallocMapped) ==
-                     hipSuccess &&
-                 hipStreamCreateWithFlags(&r->s_svc, hipStreamNonBlocking) == hipSuccess;
-            r->svc = static_cast<halo::RingServiceCtl*>(cp);
-            if (ok) {
-                memset(cp, 0, sizeof(halo::RingServiceCtl));
-                r->d_svc = static_cast<halo::RingServiceCtl*>(device_view(cp, sizeof(halo::RingServiceCtl)));
-                ok = r->d_svc != nullptr;
-            }
-        }
+        if (ok && (attach_flags & HALO_RING_PERSISTENT) && r->d_data)
+            ok = halo::resident_create(device, r->d_data, r->d_soff, r->d_slen, &r->svc) == HALO_OK;
     }
     if (!ok) {
         free_ring(r);
@@ -975,6 +887,18 @@ extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, con
 extern "C" HALO_API int halo_rx_ring_get_stats(const halo_rx_ring_t* r, halo_rx_ring_stats_t* out) {
     if (!r || !out) return HALO_E_INVAL;
     *out = r->stats;
+    if (r->svc) {
+        const halo::ResidentStats s = halo::resident_stats(r->svc);
+        out->service_requests = s.requests;
+        out->service_launches = s.launches;
+        out->service_gpu_ns = s.gpu_ns;
+    }
+    return HALO_OK;
+}
+
+extern "C" HALO_API int halo_rx_ring_set_service_timeout(halo_rx_ring_t* r, uint64_t us) {
+    if (!r || !r->svc) return HALO_E_INVAL;
+    halo::resident_set_timeout(r->svc, us);
     return HALO_OK;
 }
 

@@ -198,7 +198,8 @@ extern "C" HALO_API int halo_route_table_destroy(halo_route_table_t* t) {
     if (!t) return HALO_E_INVAL;
     if (t->device >= 0) {
         halo::DeviceScope ds(t->device);
-        (void)hipDeviceSynchronize();  // no lookup may still read the tables
+        halo::ParkResidents park(t->device);  // through the frees: hipFree waits for every kernel
+        (void)halo::drain_device(t->device);  // no lookup may still read the tables
         for (auto& g : t->gen) {
             if (g.d_tbl24) (void)hipFree(g.d_tbl24);
             if (g.d_tbl8) (void)hipFree(g.d_tbl8);
@@ -263,6 +264,7 @@ extern "C" HALO_API int halo_route_sync_device(halo_route_table_t* t, int device
     }
     halo::DeviceScope ds(device);
     if ((rc = halo::check_device())) return rc;
+    halo::ParkResidents park(device);  // the drains, table growth (hipFree) and copies below
     std::vector<uint32_t> tbl24(1u << 24, 0u), tbl8, ids;
     std::vector<uint2> lists;
     {
@@ -275,7 +277,9 @@ extern "C" HALO_API int halo_route_sync_device(halo_route_table_t* t, int device
     const int cur = t->active.load(std::memory_order_acquire);
     // the generation written now was last published before `cur`: lookups launched while it was
     // active may still be running on any stream of the device, so drain the device first
-    if (cur >= 0 && hipDeviceSynchronize() != hipSuccess) return HALO_E_HIP;
+    // (resident consumers are stopped for it, so a persistent ring's kernel cannot hold the write
+    // lock, and the lookups behind it, for its 20 ms idle window: ADVICE r3)
+    if (cur >= 0 && halo::drain_device(device) != HALO_OK) return HALO_E_HIP;
     auto& g = t->gen[cur < 0 ? 0 : 1 - cur];
     if (!g.d_tbl24 && hipMalloc(&g.d_tbl24, tbl24.size() * sizeof(uint32_t)) != hipSuccess) return HALO_E_NOMEM;
     t->device = device;
@@ -291,7 +295,7 @@ extern "C" HALO_API int halo_route_sync_device(halo_route_table_t* t, int device
         return HALO_E_HIP;
     // hipMemcpy from pageable memory returns once the host buffer is consumed, not when the copy
     // has landed: wait for it before publishing
-    if (hipDeviceSynchronize() != hipSuccess) return HALO_E_HIP;
+    if (halo::drain_device(device) != HALO_OK) return HALO_E_HIP;
     t->active.store(cur < 0 ? 0 : 1 - cur, std::memory_order_release);
     return HALO_OK;
 }

@@ -625,6 +625,52 @@ rx_lane_kernel(const RxParams p) {
     flush_hist(p, hist);
 }
 
+// Several batches in one launch (halo_rx_parse_batches_device): the batch stream of the reference's
+// unbounded poll loop (engine/engine.go:344-351) handed over K batches at a time. A 1M-frame launch
+// spends a fixed ramp and tail filling and draining 256 CUs — config 2 ran at 0.62 of 8 TB/s while
+// the same kernel reached 0.74 on 16M frames — so the K batches' 64-frame windows are
+// one grid: window w belongs to the batch whose cumulative window count first exceeds w (a
+// wave-uniform scan over <= kMultiMax kernel arguments), and each wave runs the lane kernel's window
+// code on that batch's arrays. Records, histogram and read contract are those of K separate launches.
+constexpr uint32_t kMultiMax = 32;
+struct MultiParams {
+    RxParams p;  // the shared fields (flags, netif, histogram); per-batch arrays below
+    uint32_t k;
+    uint32_t win_end[kMultiMax];  // windows of batches 0..b
+    uint32_t n[kMultiMax];
+    const uint8_t* bytes[kMultiMax];
+    const uint32_t* offsets_dw[kMultiMax];
+    const uint16_t* lens[kMultiMax];
+    halo_rx_result_t* out[kMultiMax];
+};
+
+template <int LAYOUT>
+__global__ void __launch_bounds__(HALO_RX_LANE_BLOCK) rx_lane_multi_kernel(const MultiParams mp) {
+    __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
+    __shared__ uint4 s_rec[HALO_RX_LANE_BLOCK / 64][128];
+    if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    Hist hist{s_hist, 0};
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t total = mp.win_end[mp.k - 1];
+    for (uint32_t win = wave; win < total; win += nwaves) {
+        uint32_t b = 0;
+        while (win >= mp.win_end[b]) ++b;  // k <= 32, uniform across the wave
+        RxParams p = mp.p;
+        p.bytes = mp.bytes[b];
+        p.offsets_dw = mp.offsets_dw[b];
+        p.lens = mp.lens[b];
+        p.out = mp.out[b];
+        p.n = mp.n[b];
+        const uint32_t base = (win - (b ? mp.win_end[b - 1] : 0u)) * 64u;
+        lane_window<LAYOUT, 0>(p, base, lane, s_rec[w], hist);
+    }
+    flush_hist(mp.p, hist);
+}
+
 // The resident small-poll consumer (RingServiceCtl, halo_common.h), kSvcGroups workgroups of
 // kSvcWaves waves. In each group wave 0 waits for a request: all its lanes load the request line
 // (one 64-byte read of pinned host memory, system scope), s_sleep between tries, bounded by the
@@ -639,9 +685,15 @@ rx_lane_kernel(const RxParams p) {
 // with the request (offsets derived in-wave, no metadata read after the request: 11.5 / 13.3-13.6,
 // the wider poll read cost more than the read it saved), and four poll reads in flight per group
 // (profiles/r03/r3h: 25.9 us at 1000: the reads queued ahead of the frame reads).
+// Idle exit is one decision for the grid: the first group whose timer runs out sets *quit (device
+// memory) and every other group leaves at its next empty read of the request line, so a request
+// that races the exit finds the whole kernel gone (the host relaunches within microseconds) rather
+// than some groups alive for another 20 ms. Requests whose flags carry
+// HALO_RX_L3_START (a LoChan drain through a host context) take the L3 layout.
 __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServiceCtl* ctl, const uint8_t* data,
                                                                       const uint32_t* off, const uint16_t* len,
-                                                                      uint32_t last, uint64_t idle_ticks) {
+                                                                      uint32_t* quit_all, uint32_t last,
+                                                                      uint64_t idle_ticks) {
     __shared__ uint32_t s_cmd[12];  // seq, exit, n, flags, mac_lo, mac_hi, own_ip, out_lo, out_hi, uni_off/stride/len
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     __shared__ uint4 s_rec[kSvcWaves][128];
@@ -664,7 +716,13 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
                                                   __builtin_amdgcn_readlane(v, 11), __builtin_amdgcn_readlane(v, 12));
                     if (ck == __builtin_amdgcn_readlane(v, 9)) break;
                 }
-                if (__builtin_amdgcn_readlane(v, 8) || __builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
+                const uint32_t others = __hip_atomic_load(quit_all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readlane(v, 8) || others) {
+                    quit = 1;
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
+                    if (lane == 0) __hip_atomic_store(quit_all, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     quit = 1;
                     break;
                 }
@@ -707,6 +765,9 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
             p.len = s_cmd[11];
             for (uint32_t base = (w * kSvcGroups + g) * 64; base < p.n; base += kSvcGroups * kSvcWaves * 64)
                 lane_window<2, 0>(p, base, lane, s_rec[w], hist);
+        } else if (p.flags & HALO_RX_L3_START) {
+            for (uint32_t base = (w * kSvcGroups + g) * 64; base < p.n; base += kSvcGroups * kSvcWaves * 64)
+                lane_window<3, 0>(p, base, lane, s_rec[w], hist);
         } else {
             for (uint32_t base = (w * kSvcGroups + g) * 64; base < p.n; base += kSvcGroups * kSvcWaves * 64)
                 lane_window<0, 0>(p, base, lane, s_rec[w], hist);
@@ -1450,11 +1511,62 @@ extern "C" HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uin
     return halo::launch_parse(p, d_lens ? 1 : 2, max_len, d_lens == nullptr, static_cast<hipStream_t>(stream));
 }
 
+extern "C" HALO_API int halo_rx_parse_batches_device(const halo_rx_batch_desc_t* batches, uint32_t k, uint32_t flags,
+                                                     const halo_rx_netif_t* netif, uint32_t max_len_hint,
+                                                     uint32_t* d_status_hist, halo_stream_t stream) {
+    if (!batches || k == 0 || k > halo::kMultiMax) return HALO_E_INVAL;
+    halo::MultiParams mp{};
+    uint64_t windows = 0;
+    uint32_t live = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+        const halo_rx_batch_desc_t& d = batches[j];
+        if (d.n == 0) {
+            mp.win_end[j] = (uint32_t)windows;
+            continue;
+        }
+        int rc = halo::fill_common(mp.p, d.n, flags, netif, d.d_out, d_status_hist);
+        if (rc) return rc;
+        if (!d.d_bytes || !d.d_offsets_dw || !d.d_lens) return HALO_E_INVAL;
+        windows += (d.n + 63u) / 64u;
+        mp.win_end[j] = (uint32_t)windows;
+        mp.n[j] = d.n;
+        mp.bytes[j] = d.d_bytes;
+        mp.offsets_dw[j] = d.d_offsets_dw;
+        mp.lens[j] = d.d_lens;
+        mp.out[j] = d.d_out;
+        ++live;
+    }
+    if (!live) return netif ? HALO_OK : HALO_E_INVAL;
+    int rc = halo::check_device();
+    if (rc) return rc;
+    const uint32_t v = (flags & HALO_RX_VARIANT_MASK) >> HALO_RX_VARIANT_SHIFT;
+    const bool lane = v == HALO_RX_VARIANT_LANE || (v == HALO_RX_VARIANT_AUTO && max_len_hint && max_len_hint <= 64);
+    if (!lane) {  // the larger-frame kernels are per batch: one launch each, in order, on `stream`
+        for (uint32_t j = 0; j < k && rc == HALO_OK; ++j)
+            if (batches[j].n)
+                rc = halo_rx_parse_batch_device(batches[j].d_bytes, batches[j].d_offsets_dw, batches[j].d_lens,
+                                                batches[j].n, flags, netif, max_len_hint, batches[j].d_out,
+                                                d_status_hist, stream);
+        return rc;
+    }
+    mp.k = k;
+    mp.p.n = 0;
+    constexpr uint32_t wpb = HALO_RX_LANE_BLOCK / 64;
+    const dim3 grid(halo::grid_for(windows * 64u, 64, HALO_RX_LANE_MAX_BLOCKS * 4 / wpb, wpb));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (flags & HALO_RX_L3_START)
+        hipLaunchKernelGGL(halo::rx_lane_multi_kernel<3>, grid, dim3(HALO_RX_LANE_BLOCK), HALO_RX_LANE_LDS_PAD, s, mp);
+    else
+        hipLaunchKernelGGL(halo::rx_lane_multi_kernel<0>, grid, dim3(HALO_RX_LANE_BLOCK), HALO_RX_LANE_LDS_PAD, s, mp);
+    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+
 namespace halo {
 int launch_ring_service(RingServiceCtl* d_ctl, const uint8_t* d_data, const uint32_t* d_off, const uint16_t* d_len,
-                        uint32_t last, uint32_t idle_us, hipStream_t s) {
-    hipLaunchKernelGGL(ring_service_kernel, dim3(kSvcGroups), dim3(64 * kSvcWaves), 0, s, d_ctl, d_data, d_off, d_len, last,
-                       (uint64_t)idle_us * 100u);  // s_memrealtime: 100 MHz
+                        uint32_t* d_quit, uint32_t last, uint32_t idle_us, hipStream_t s) {
+    if (hipMemsetAsync(d_quit, 0, sizeof(uint32_t), s) != hipSuccess) return HALO_E_HIP;
+    hipLaunchKernelGGL(ring_service_kernel, dim3(kSvcGroups), dim3(64 * kSvcWaves), 0, s, d_ctl, d_data, d_off, d_len,
+                       d_quit, last, (uint64_t)idle_us * 100u);  // s_memrealtime: 100 MHz
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 }  // namespace halo

@@ -73,6 +73,24 @@ class HostBatcher:
         """Registered batches parsed in place over PCIe (default) or DMA'd in chunks."""
         _lib.check("halo_rx_host_ctx_set_zero_copy", _lib.lib.halo_rx_host_ctx_set_zero_copy(self._ctx, int(enable)))
 
+    def set_resident(self, max_frames: int, max_bytes: int = 0):
+        """Batches of up to ``max_frames`` frames (and ``max_bytes`` of staging; 0 = the library's
+        default) go to a resident consumer kernel: no launch or stream synchronisation per call
+        (halo_rx_host_ctx_set_resident). 0 turns it off."""
+        _lib.check("halo_rx_host_ctx_set_resident",
+                   _lib.lib.halo_rx_host_ctx_set_resident(self._ctx, max_frames, max_bytes))
+
+    def set_service_timeout(self, us: int):
+        """Bound on one resident request's wait (0 = the default 2 s; fault injection)."""
+        _lib.check("halo_rx_host_ctx_set_service_timeout",
+                   _lib.lib.halo_rx_host_ctx_set_service_timeout(self._ctx, us))
+
+    def stats(self) -> dict:
+        """halo_rx_host_ctx_get_stats: call counts and where the resident path's time went."""
+        st = np.zeros(1, _lib.HOST_STATS_DTYPE)
+        _lib.check("halo_rx_host_ctx_get_stats", _lib.lib.halo_rx_host_ctx_get_stats(self._ctx, st.ctypes.data))
+        return {k: int(st[k][0]) for k in _lib.HOST_STATS_DTYPE.names}
+
     def close(self):
         if self._ctx:
             _lib.lib.halo_rx_host_ctx_destroy(self._ctx)
@@ -112,6 +130,9 @@ class NetIf:
     TcpServiceMap: dict = field(default_factory=dict)
     LoChan: collections.deque = field(default_factory=collections.deque)  # NetIf.LoChan (engine/engine.go:106, cap 1024 :209)
     device: int = 0
+    # batches of up to this many frames go to the host context's resident consumer (no launch per
+    # batch: PacketHandle-sized batches, e.g. drain_every=99, are latency-bound); 0 = launches only
+    resident_frames: int = 4096
 
     def __post_init__(self):
         self.abi = NetIfAbi.make(self.MacAddr, self.IpAddr, self.NatEnable)
@@ -151,9 +172,7 @@ class NetIf:
             offsets = np.zeros(len(frames), dtype=np.uint64)
             np.cumsum(lens[:-1], out=offsets[1:])
             data = np.frombuffer(b"".join(frames), dtype=np.uint8)
-            if self._batcher is None:
-                self._batcher = HostBatcher(self.device)
-            res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable))
+            res = self._host().parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable))
             actions = dispatch(res, self.abi)
             self._deliver(frames, res, actions)
         if not drain_every or self._polls >= drain_every:
@@ -179,9 +198,7 @@ class NetIf:
             data = np.zeros(int(sizes.sum()) + 4, dtype=np.uint8)
             for o, p in zip(offsets, pkts):
                 data[int(o):int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
-            if self._batcher is None:
-                self._batcher = HostBatcher(self.device)
-            res = self._batcher.parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable, l3_start=True))
+            res = self._host().parse(data, offsets, lens, self.abi, flags_word(self.CheckSumEnable, l3_start=True))
             actions = dispatch_loopback(res, self.abi)
             self._deliver(pkts, res, actions)
             all_res.append(res)
@@ -189,6 +206,13 @@ class NetIf:
         if not all_res:
             return np.empty(0, RESULT_DTYPE), np.empty(0, np.uint8)
         return np.concatenate(all_res), np.concatenate(all_act)
+
+    def _host(self) -> HostBatcher:
+        if self._batcher is None:
+            self._batcher = HostBatcher(self.device)
+            if self.resident_frames:
+                self._batcher.set_resident(self.resident_frames)
+        return self._batcher
 
     def _deliver(self, bufs, res, actions):
         """Invoke the UDP / TCP service handlers for the LOCAL_UDP / LOCAL_TCP records, in order."""

@@ -129,6 +129,27 @@ def parse_frames_batch(frames, offsets_dw, lens, *, netif: NetIf, check_sum_enab
     return out
 
 
+def parse_frames_batches(batches, *, netif: NetIf, check_sum_enable: bool = True, jumbo: bool = False,
+                         max_len_hint: int = 0, variant: int = 0, compact: bool = False, l3_start: bool = False,
+                         hist=None, stream=None):
+    """Several ragged device-resident batches in one call (halo_rx_parse_batches_device): each of
+    ``batches`` is (frames, offsets_dw, lens, out) with the tensors of parse_frames_batch; frames of
+    at most 64 B (max_len_hint <= 64 or variant 1) run as one launch. Returns the outs."""
+    import ctypes
+
+    k = len(batches)
+    descs = (_lib.BatchDesc * max(k, 1))()
+    for j, (fr, offs, ln, out) in enumerate(batches):
+        n = int(ln.numel())
+        assert out.is_cuda and out.numel() * out.element_size() >= (16 if compact else 32) * n, "out too small"
+        descs[j] = _lib.BatchDesc(_lib.ptr(fr), _lib.ptr(offs), _lib.ptr(ln), _lib.ptr(out), n, 0)
+    fl = flags_word(check_sum_enable, jumbo, variant, False, l3_start) | (_lib.HALO_RX_RECORD_COMPACT if compact else 0)
+    rc = _lib.lib.halo_rx_parse_batches_device(ctypes.cast(descs, ctypes.c_void_p), k, fl, netif, max_len_hint,
+                                               _lib.ptr(hist), _stream_handle(stream))
+    _lib.check("halo_rx_parse_batches_device", rc)
+    return [b[3] for b in batches]
+
+
 def parse_ipv4_packets_batch(packets, offsets_dw, lens, *, netif: NetIf, **kw):
     """ParseIpv4Pkt + local L4 parse of a batch of LoChan packets (buffers that start at their
     IPv4 header: engine/engine.go:353-381), HALO_RX_L3_START. Same arguments and record as
@@ -276,7 +297,7 @@ def icmp_ttl_deep_nat_batch(frames, offsets_dw, lens, *, nat=None, check_sum_ena
 # example/example.go:162-168) or code ported from the reference — each wrapper returns exactly the
 # tuple its Go function returns, with `err` the reference's error string (None on success). The
 # frame goes through the GPU like a batch of one (halo_rx_parse_batch_host, a per-process host
-# context): there is no CPU path. Batches of frames belong on parse_frames_batch / engine.
+# context whose resident consumer serves it: one request, no launch): there is no CPU path. Batches of frames belong on parse_frames_batch / engine.
 CheckSumEnable = True  # protocol.CheckSumEnable (protocol/utils.go:8) for the wrappers below
 DEVICE = 0             # the device the wrappers' host context uses
 
@@ -299,6 +320,8 @@ def _parse_one(buf: bytes, l3: bool) -> np.void:
     if DEVICE not in _ctx:
         h = ctypes.c_void_p()
         _lib.check("halo_rx_host_ctx_create", _lib.lib.halo_rx_host_ctx_create(DEVICE, 64, 1 << 16, ctypes.byref(h)))
+        # one frame per call: the resident consumer serves it (no launch or synchronisation per frame)
+        _lib.check("halo_rx_host_ctx_set_resident", _lib.lib.halo_rx_host_ctx_set_resident(h, 64, 1 << 16))
         _ctx[DEVICE] = h
     n = min(len(buf), 0xFFFF)
     data = np.zeros(max(4, n), np.uint8)

@@ -145,6 +145,10 @@ class RingConsumer:
     def commit(self):
         _lib.check("halo_rx_ring_commit", _lib.lib.halo_rx_ring_commit(self._h))
 
+    def set_service_timeout(self, us: int):
+        """Bound on one resident request's wait (0 = the default 2 s; fault injection)."""
+        _lib.check("halo_rx_ring_set_service_timeout", _lib.lib.halo_rx_ring_set_service_timeout(self._h, us))
+
     def stats(self) -> dict:
         """halo_rx_ring_get_stats: poll counters and where the small polls' time went."""
         st = np.zeros(1, RING_STATS_DTYPE)

@@ -222,6 +222,28 @@ HALO_API int halo_rx_parse_strided_device(const uint8_t* d_bytes, uint64_t strid
                                           halo_rx_result_t* d_out, uint32_t* d_status_hist,
                                           halo_stream_t stream);
 
+/* ---- several device-resident batches in one launch ------------------------------------
+ * The reference's receive loop is an unbounded stream of polls (engine/engine.go:344-351); a
+ * caller holding K ragged batches at once (consecutive batches of one queue, or the batches of
+ * several NetIf queues) hands them over together. Each batch keeps its own arrays and records,
+ * exactly as K halo_rx_parse_batch_device calls on `stream` would produce them; the status
+ * histogram (optional) counts all of them. With frames of at most 64 B (max_len_hint 1..64, or
+ * HALO_RX_VARIANT_LANE) the K batches run as ONE grid of lane-per-frame waves, so the launch ramp
+ * and tail are paid once per K batches instead of once per batch; larger frames take one launch
+ * per batch. k <= 32; `batches` is a host array read during the call; batches with n = 0 are
+ * skipped. Flags as halo_rx_parse_batch_device (HALO_RX_L3_START included). Asynchronous.   */
+typedef struct halo_rx_batch_desc {
+    const uint8_t* d_bytes;
+    const uint32_t* d_offsets_dw;
+    const uint16_t* d_lens;
+    halo_rx_result_t* d_out; /* n records (or halo_rx_record16_t), 16-byte aligned */
+    uint32_t n;
+    uint32_t pad;
+} halo_rx_batch_desc_t;    /* 40 B */
+HALO_API int halo_rx_parse_batches_device(const halo_rx_batch_desc_t* batches, uint32_t k, uint32_t flags,
+                                          const halo_rx_netif_t* netif, uint32_t max_len_hint,
+                                          uint32_t* d_status_hist, halo_stream_t stream);
+
 /* ---- host-memory batch parse -----------------------------------
  * Frames in HOST memory (any alignment, ragged byte offsets). Stages them into pinned
  * buffers, copies H2D, runs the kernel and copies results D2H, double-buffered in chunks
@@ -243,6 +265,34 @@ HALO_API int halo_rx_parse_batch_host(halo_rx_host_ctx_t* ctx, const uint8_t* by
  * pinned staging by the CPU. halo_rx_host_ctx_set_zero_copy(ctx, 0) keeps registered batches
  * on the DMA path. Registered memory must stay registered until the call returns.         */
 HALO_API int halo_rx_host_ctx_set_zero_copy(halo_rx_host_ctx_t* ctx, int enable);
+/* Resident consumer for small batches (the latency path of a batched PacketHandle: EthRxFunc polls
+ * gathered into batches of a few frames to a few thousand, engine/engine.go:339-385, and of the
+ * single-frame Parse* wrappers an Ipv4PktFwdHook calls, engine/engine.go:132). Batches of at most
+ * `max_frames` frames (<= 16384; 0 turns the path off) whose frames fit `max_bytes` of staging
+ * (0: min(1516 * max_frames, 4 MiB); at most 64 MiB) are copied into pinned staging this context
+ * owns, and a kernel resident on 8 CUs — waiting on a control block in pinned memory — parses them
+ * there and writes the records into `out` (directly when `out` lies in a live registration): no
+ * launch and no stream synchronisation per call. The kernel leaves 20 ms after its last request and
+ * the next call relaunches it; a device drain (halo_rx_host_unregister, a ring detach, a route sync)
+ * stops it first and serves calls by launches until the drain is over. Same records as the chunked
+ * path. Larger batches take the chunked path. */
+HALO_API int halo_rx_host_ctx_set_resident(halo_rx_host_ctx_t* ctx, uint32_t max_frames, uint64_t max_bytes);
+/* Bounds the wait for one resident request (default 2 s; 0 restores it). A request that times out
+ * is retired before the call returns HALO_E_HIP: the consumer is stopped and its kernel has ended,
+ * so nothing is written into the caller's arrays afterwards. (Diagnostics and fault injection.) */
+HALO_API int halo_rx_host_ctx_set_service_timeout(halo_rx_host_ctx_t* ctx, uint64_t us);
+typedef struct halo_rx_host_stats {
+    uint64_t calls;            /* halo_rx_parse_batch_host calls with frames                     */
+    uint64_t frames;           /* frames parsed                                                   */
+    uint64_t resident_calls;   /* calls served on the resident path                              */
+    uint64_t resident_parked;  /* resident calls served by a launch while a device drain ran     */
+    uint64_t service_launches; /* resident consumer launches (first use, after idle exits)       */
+    uint64_t pack_ns;          /* resident path: host time packing frames into pinned staging    */
+    uint64_t wait_ns;          /* resident path: request to completion                            */
+    uint64_t service_gpu_ns;   /* resident consumer: GPU time per request (first group in to last
+                                  group out), summed                                              */
+} halo_rx_host_stats_t;
+HALO_API int halo_rx_host_ctx_get_stats(const halo_rx_host_ctx_t* ctx, halo_rx_host_stats_t* out);
 /*
  * Registration pins whole pages, so the library enforces: `ptr` page-aligned and `bytes` a
  * multiple of the page size (hugepages, mmap regions; halo_amd._lib.host_array in Python), and
@@ -356,6 +406,11 @@ typedef struct halo_rx_ring_stats {
     uint64_t service_gpu_ns;   /* resident consumer: GPU time per request, summed                 */
 } halo_rx_ring_stats_t;
 HALO_API int halo_rx_ring_get_stats(const halo_rx_ring_t* ring, halo_rx_ring_stats_t* out);
+/* HALO_RING_PERSISTENT rings: bounds the wait for one resident request (default 2 s; 0 restores
+ * it). A poll whose request times out retires it before returning HALO_E_HIP (the consumer is
+ * stopped and its kernel has ended: nothing is written into `out` afterwards) and leaves the cursor
+ * where it was, so the next poll parses the same frames. (Diagnostics and fault injection.)    */
+HALO_API int halo_rx_ring_set_service_timeout(halo_rx_ring_t* ring, uint64_t us);
 
 /* The record walk alone, device-resident: `used` bytes of ring data in stream order at d_span
  * (4-byte aligned; used a multiple of 4, <= ring_size), ring_size = RingBuffer.size. Writes

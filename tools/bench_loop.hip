@@ -13,19 +13,20 @@
 
 #include "halo_rx.h"
 
+// `hist` (optional, device): the status histogram every launch counts into (the §5 metrics output).
 extern "C" __attribute__((visibility("default"))) int halo_bench_steps(
     int nbatch, const uint8_t* const* bytes, const uint32_t* const* offsets_dw, const uint16_t* const* lens,
     uint32_t n, uint64_t stride, uint32_t len, uint32_t flags, const halo_rx_netif_t* netif, uint32_t hint,
-    halo_rx_result_t* out, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    halo_rx_result_t* out, uint32_t* hist, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
     if (nbatch <= 0 || steps <= 0 || !region_ms || !wall_s) return HALO_E_INVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto launch = [&](int k) -> int {
         const int b = k % nbatch;
         if (offsets_dw)
-            return halo_rx_parse_batch_device(bytes[b], offsets_dw[b], lens[b], n, flags, netif, hint, out, nullptr,
+            return halo_rx_parse_batch_device(bytes[b], offsets_dw[b], lens[b], n, flags, netif, hint, out, hist,
                                               stream);
         return halo_rx_parse_strided_device(bytes[b], stride, lens ? lens[b] : nullptr, len, n, flags, netif, out,
-                                            nullptr, stream);
+                                            hist, stream);
     };
     int rc = HALO_OK;
     for (int k = 0; k < warmup && rc == HALO_OK; ++k) rc = launch(k);
@@ -171,6 +172,33 @@ __global__ void __launch_bounds__(256) read_peak_kernel(const uint4* __restrict_
     if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;  // practically never: keeps the loads live
 }
 
+// The read probe family (halo_bench_read_probe): block b reads tile b once — BLOCK threads x U
+// chunks of 16 B, all U loads in flight per lane, consecutive lanes on consecutive chunks — with
+// plain or non-temporal loads. No grid-stride loop: like the rx kernels, one wave never loops, the
+// dispatcher refills CUs. bench.py takes the fastest of the family and of read_peak_kernel as the
+// box's measured read peak (a single probe shape was beaten by the jumbo kernel).
+template <int BLOCK, int U, bool NT>
+__global__ void __launch_bounds__(BLOCK) read_tile_kernel(const uint4* __restrict__ src, uint64_t n16,
+                                                          uint32_t* __restrict__ sink) {
+    const uint64_t base = (uint64_t)blockIdx.x * U * BLOCK + threadIdx.x;
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t k = base + (uint64_t)u * BLOCK;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        if (k < n16 && NT) {
+            const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + k);
+            v[u] = make_uint4(t.x, t.y, t.z, t.w);
+        } else {
+            v[u] = k < n16 ? src[k] : make_uint4(0, 0, 0, 0);
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    if (acc == 0x9E3779B9u) sink[blockIdx.x & 4095u] = acc;  // practically never: keeps the loads live
+}
+
 // Size-matched speed-of-light probe: block t reads 16 KB tile t of `src` (four 16-byte loads per
 // thread in flight) and writes its share of `dst` with coalesced 16-byte stores — the rx kernel's
 // bytes (frames + metadata in, records out) with perfect access patterns and no work.
@@ -204,6 +232,48 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_read_peak(const
     auto launch = [&](int) {
         hipLaunchKernelGGL(read_peak_kernel, dim3(grid_blocks), dim3(256), 0, s, static_cast<const uint4*>(buf),
                            bytes / 16, sink);
+        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+    };
+    return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
+}
+
+// Read probe `variant` over `bytes` (a multiple of 64 KiB): 0 = read_peak_kernel (8192 blocks of
+// 256 threads streaming 64 KB tiles), 1.. = read_tile_kernel shapes (see kReadProbes). Returns
+// HALO_E_RANGE past the last variant.
+namespace {
+struct ReadProbe {
+    const char* name;
+    void (*launch)(const uint4*, uint64_t, uint32_t*, hipStream_t);
+};
+template <int BLOCK, int U, bool NT>
+void launch_tile(const uint4* src, uint64_t n16, uint32_t* sink, hipStream_t s) {
+    const uint64_t blocks = (n16 + (uint64_t)U * BLOCK - 1) / ((uint64_t)U * BLOCK);
+    hipLaunchKernelGGL((read_tile_kernel<BLOCK, U, NT>), dim3((uint32_t)blocks), dim3(BLOCK), 0, s, src, n16, sink);
+}
+const ReadProbe kReadProbes[] = {
+    {"tile256_u4", launch_tile<256, 4, false>},   {"tile256_u8", launch_tile<256, 8, false>},
+    {"tile256_u16", launch_tile<256, 16, false>}, {"tile256_u8_nt", launch_tile<256, 8, true>},
+    {"tile256_u16_nt", launch_tile<256, 16, true>}, {"tile64_u8", launch_tile<64, 8, false>},
+    {"tile64_u16", launch_tile<64, 16, false>},   {"tile1024_u4", launch_tile<1024, 4, false>},
+};
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) const char* halo_bench_read_probe_name(int variant) {
+    if (variant == 0) return "persistent256_64KB";
+    if (variant < 1 || variant > (int)(sizeof kReadProbes / sizeof kReadProbes[0])) return nullptr;
+    return kReadProbes[variant - 1].name;
+}
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_read_probe(const void* buf, uint64_t bytes,
+                                                                             uint32_t* sink, int variant,
+                                                                             int warmup, int steps, void* stream,
+                                                                             float* region_ms, double* wall_s) {
+    if (variant == 0) return halo_bench_read_peak(buf, bytes, sink, warmup, steps, stream, region_ms, wall_s);
+    if (variant < 1 || variant > (int)(sizeof kReadProbes / sizeof kReadProbes[0])) return HALO_E_RANGE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const ReadProbe& p = kReadProbes[variant - 1];
+    auto launch = [&](int) {
+        p.launch(static_cast<const uint4*>(buf), bytes / 16, sink, s);
         return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
     };
     return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
@@ -279,4 +349,46 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_ring_polls(
         if (k >= warmup) us[k - warmup] = std::chrono::duration<double, std::micro>(t1 - t0).count();
     }
     return HALO_OK;
+}
+
+// The drop-in surface as a cgo caller drives it (go/gpurx Ctx.ParseBatch, the batched PacketHandle
+// of go/engine at its 99-poll cadence, and — m = 1 — the single-frame Parse* wrappers): per call
+// halo_rx_parse_batch_host over m frames in pageable host memory (Go slices) + halo_rx_dispatch over
+// the records. us[k] = call k's time; *bad counts calls whose records were not all OK / LOCAL_UDP.
+extern "C" __attribute__((visibility("default"))) int halo_bench_host_calls(
+    halo_rx_host_ctx_t* ctx, const uint8_t* bytes, const uint64_t* offs, const uint16_t* lens, uint32_t m,
+    uint32_t flags, const halo_rx_netif_t* netif, halo_rx_result_t* out, uint8_t* acts, int warmup, int iters,
+    double* us, uint32_t* bad) {
+    if (!ctx || !netif || !out || !acts || !us || !bad || iters <= 0) return HALO_E_INVAL;
+    *bad = 0;
+    for (int k = 0; k < warmup + iters; ++k) {
+        const auto t0 = std::chrono::steady_clock::now();
+        int rc = halo_rx_parse_batch_host(ctx, bytes, offs, lens, m, flags, netif, out, nullptr);
+        if (!rc) rc = halo_rx_dispatch(out, m, netif, acts, nullptr);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc) return rc;
+        bool ok = true;
+        for (uint32_t i = 0; ok && i < m; ++i) ok = out[i].status == HALO_RX_OK && acts[i] == HALO_RX_ACT_LOCAL_UDP;
+        if (!ok) ++*bad;
+        if (k >= warmup) us[k - warmup] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+    }
+    return HALO_OK;
+}
+
+// The batch stream handed over k batches per launch (halo_rx_parse_batches_device): step t parses
+// batches (t * k + j) % nbatch, j < k, into outs[j].
+extern "C" __attribute__((visibility("default"))) int halo_bench_multi_steps(
+    int nbatch, const uint8_t* const* bytes, const uint32_t* const* offsets_dw, const uint16_t* const* lens, uint32_t n,
+    uint32_t k, uint32_t flags, const halo_rx_netif_t* netif, uint32_t hint, halo_rx_result_t* const* outs,
+    uint32_t* hist, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0 || k == 0 || k > 32) return HALO_E_INVAL;
+    auto launch = [&](int t) {
+        halo_rx_batch_desc_t d[32];
+        for (uint32_t j = 0; j < k; ++j) {
+            const int b = (int)(((uint64_t)t * k + j) % (uint64_t)nbatch);
+            d[j] = halo_rx_batch_desc_t{bytes[b], offsets_dw[b], lens[b], outs[j], n, 0};
+        }
+        return halo_rx_parse_batches_device(d, k, flags, netif, hint, hist, stream);
+    };
+    return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
 }

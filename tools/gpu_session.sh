@@ -81,6 +81,10 @@ for s in "$@"; do
     krdv)  step krd_$KV 600 bash tools/exp/with_variant.sh $KV rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krd_$KV" -o run -- python3 tools/prof_kernels.py ${PK_ARGS:-} ;;
     wrxx)  step wrxx 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/wrxx" -o run -- python3 tools/exp/bench_xxh3.py ;;
     vgen)  step vtest_$VT 600 bash tools/exp/variant_tests.sh "$VT_TESTS" $VT ;;
+    tres)  step pytest_resident 600 python -u -m pytest tests/test_gpu_host_resident.py tests/test_gpu_ring.py tests/test_gpu_single_frame.py tests/test_gpu_engine_cadence.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    dropin) step dropin 600 python tools/bench_dropin.py ;;
+    tmulti) step pytest_multi 600 python -u -m pytest tests/test_gpu_multi_batch.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    tnew)  step pytest_new 900 python -u -m pytest tests/test_gpu_host_resident.py tests/test_gpu_multi_batch.py tests/test_gpu_ring.py tests/test_gpu_single_frame.py tests/test_gpu_engine_cadence.py tests/test_gpu_route.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
   esac
 done
