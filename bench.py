@@ -277,6 +277,8 @@ def bench_lib():
         tail = [i32, i32, vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double)]
         L.halo_bench_flow_steps.restype = ctypes.c_int
         L.halo_bench_flow_steps.argtypes = [i32, vp, u32, u32, u32, vp, u32, vp] + tail
+        L.halo_bench_flow_compact_steps.restype = ctypes.c_int
+        L.halo_bench_flow_compact_steps.argtypes = [i32, vp, u32, u32, u32, vp, u32, vp] + tail
         L.halo_bench_route_steps.restype = ctypes.c_int
         L.halo_bench_route_steps.argtypes = [i32, vp, vp, u32, vp] + tail
         L.halo_bench_xxh3_steps.restype = ctypes.c_int
@@ -548,22 +550,26 @@ def lo_drain_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = Fals
     pk, ln, _ = b.build(torch.from_numpy(desc.view(np.uint8)).to(dev),
                         torch.randint(0, 256, (n * plen,), dtype=torch.uint8, device=dev), netif=netif,
                         out_stride=64)  # 50 B packets in 64 B slots (out_stride >= 60)
-    offs = torch.arange(n, dtype=torch.int32, device=dev) * 16
+    # packed back to back at 4-byte aligned starts, as the batched drain packs LoChan's slices
+    # (go/gpurx PackAligned, halo_amd.engine lo_drain): 52-byte pitch for the 50 B packets
+    pk = pk.reshape(n, 64)[:, :52].contiguous().reshape(-1)
+    offs = torch.arange(n, dtype=torch.int32, device=dev) * 13
     out = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=dev)
-    w, k = time_torch_loop(lambda: protocol.parse_ipv4_packets_batch(pk.reshape(-1), offs, ln, netif=netif,
+    w, k = time_torch_loop(lambda: protocol.parse_ipv4_packets_batch(pk, offs, ln, netif=netif,
                                                                      max_len_hint=64, out=out), steps, warmup, d)
     recs = protocol.records(out)
     assert np.all(recs["status"] == 0) and np.all(recs["flags"] & 4)
     alg = n * (50 + 6 + RESULT_BYTES)
     r = {"frames": n, "mpps": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 5),
          "roofline": roofline(alg, k, load_traffic("lo_drain_1M_50B")), "alg_bytes_per_launch": alg,
-         "what": "LoChan drain: ParseIpv4Pkt -> own-address filter -> RxUdp verify (engine/engine.go:353-381)"}
+         "what": "LoChan drain: ParseIpv4Pkt -> own-address filter -> RxUdp verify (engine/engine.go:353-381); "
+                 "packets packed at a 52-byte pitch (4-byte aligned starts, as PackAligned lays them out)"}
     if with_cpu:
         from oracle import oracle as O
 
         m = 1 << 18
-        host = pk.reshape(-1)[:m * 64].cpu().numpy()
-        hoffs = np.arange(m, dtype=np.uint32) * 16
+        host = pk[:m * 52].cpu().numpy()
+        hoffs = np.arange(m, dtype=np.uint32) * 13
         hl = ln[:m].cpu().numpy().view(np.uint16)
         r["cpu_baseline"] = cpu_rate(lambda: O.rx_batch(host, hl, O.NetIf.make(), 1 | 0x10, offsets_dw=hoffs), m, 2.0,
                                      "Mpps", f"{m} packets of the batch (oracle/halo_rx_oracle.c, HALO_RX_L3_START)")
@@ -594,6 +600,26 @@ def flow_hash_secondary(batches, out_records, netif, steps, warmup, d: Dist, wit
     res = {"mpps": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 5),
            "roofline": roofline(alg, k, load_traffic("flow_hash_config2")), "alg_bytes_per_launch": alg,
            "what": "NatWanFlowHash (13 B key) XXH3-64 + hash % 2^20 per record"}
+    # the same keys from compact 16 B records (halo_flow_hash_compact_device): every fetched byte used
+    from halo_amd import _lib
+    from halo_amd._lib import HALO_RX_RECORD_COMPACT
+
+    crecs = []
+    for b in batches:
+        o = torch.empty((n, 16), dtype=torch.uint8, device=out_records.device)
+        _lib.check("halo_rx_parse_batch_device", _lib.lib.halo_rx_parse_batch_device(
+            b["bytes"].data_ptr(), b["offsets_dw"].data_ptr(), b["lens"].data_ptr(), n, 1 | HALO_RX_RECORD_COMPACT,
+            ctypes.byref(netif), 64, o.data_ptr(), None, torch.cuda.current_stream().cuda_stream))
+        crecs.append(o)
+    carr = (ctypes.c_void_p * len(crecs))(*[r.data_ptr() for r in crecs])
+    wc, kc = time_native(bench_lib().halo_bench_flow_compact_steps, len(crecs), carr, n, 1, 0, h.data_ptr(), 1 << 20,
+                         bk.data_ptr(), steps=steps, warmup=warmup, d=d)
+    algc = n * (16 + 8 + 4)
+    res["compact_records"] = {"mpps": round(n * steps / wc / 1e6, 1), "kernel_ms": round(kc, 5),
+                              "roofline": roofline(algc, kc, load_traffic("flow_hash_config2_compact")),
+                              "alg_bytes_per_launch": algc,
+                              "what": "the same keys from HALO_RX_RECORD_COMPACT records (16 B: the key fields only)"}
+    del crecs
     if with_cpu:
         from oracle import oracle as O
 

@@ -27,16 +27,33 @@ type BatchConfig struct {
 	// there, so handlers, drains and their TX see exactly the reference's order. 0 drains after
 	// every batch, and a batch also ends at the first poll that returns nil.
 	DrainEvery int
+	// Launched turns the resident consumer off: every batch is then a launch + synchronisation
+	// (~33-37 us for <= 256 frames instead of ~8 us, DESIGN.md §13.1), and no kernel stays on the
+	// GPU between batches.
+	Launched bool
 }
 
 // PacketHandleBatched replaces `go netIf.PacketHandle()` (engine.go:299) for a NetIf whose frames
 // are parsed on the GPU by x.
+//
+// One difference in timing, not in results for unchanged configuration: the reference parses and
+// acts on each frame before it polls the next, while a batch is parsed as a whole before its
+// handlers run, with the NetIf's MAC / IP / NatEnable as they were at the start of the batch. A
+// handler that changes them (RxDhcp storing a leased address, engine/dhcp_engine.go) takes effect
+// from the next batch; the frames after it in the same batch were judged (DST_IS_OWN, MAC_MATCH)
+// against the old address. With DrainEvery 99 a batch spans at most 99 polls. A failed GPU call
+// drops its whole batch with one log line where the reference would have handled each frame.
 func (i *NetIf) PacketHandleBatched(x *gpurx.Ctx, cfg BatchConfig) {
 	if i.Config.BindCpuCore >= 0 {
 		cpu.BindCpuCore(i.Config.BindCpuCore)
 	}
 	if cfg.Batch <= 0 {
 		cfg.Batch = 4096
+	}
+	if !cfg.Launched && cfg.Batch <= 16384 {
+		if err := x.SetResident(cfg.Batch, 0); err != nil {
+			Log(fmt.Sprintf("gpurx resident consumer unavailable, batches are launched: %v\n", err))
+		}
 	}
 	netif := &gpurx.NetIfCfg{MacAddr: i.MacAddr, IpAddr: i.IpAddr, NatEnable: i.Config.NatEnable}
 	b := gpurx.NewBatch(cfg.Batch)

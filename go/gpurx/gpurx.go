@@ -185,6 +185,17 @@ func NewCtx(device int) (*Ctx, error) {
 	return &Ctx{c: c}, nil
 }
 
+// SetResident serves batches of up to maxFrames frames (<= 16384; 0 turns it off) with a kernel
+// resident on the GPU instead of a launch per batch (halo_rx_host_ctx_set_resident): the frames are
+// packed into pinned staging and one request line is written, so a PacketHandle-sized batch costs
+// ~8 us instead of ~33-37 us (DESIGN.md §13.1). The kernel keeps 8 CUs while batches keep coming
+// and leaves 20 ms after the last one. maxBytes bounds the staging (0: min(1516 * maxFrames, 4 MiB)).
+func (x *Ctx) SetResident(maxFrames int, maxBytes uint64) error {
+	x.mu.Lock()
+	defer x.mu.Unlock()
+	return halo(C.halo_rx_host_ctx_set_resident(x.c, C.uint32_t(maxFrames), C.uint64_t(maxBytes)))
+}
+
 // Close frees the context.
 func (x *Ctx) Close() {
 	x.mu.Lock()
@@ -288,8 +299,9 @@ func (b *Batch) Len() int { return len(b.Lens) }
 
 // Add copies one frame in (EthRxFunc's slice aliases a reused buffer: dpdk/dpdk.go:184-194,
 // engine/engine.go:544, so it must be copied before the next poll — the one copy the reference
-// already makes out of the ring). Frames longer than 65535 bytes are cut to 65535 (every length
-// past 1514 gets the same ETH_LEN verdict).
+// already makes out of the ring). Frames longer than 65535 bytes are cut to 65535: the record's
+// length field is a u16, and every length past 1514 (9014 with the jumbo extension) gets the same
+// ETH_LEN verdict, so the verdicts are unchanged; Frame(k) then returns the first 65535 bytes.
 func (b *Batch) Add(frame []byte) {
 	if len(frame) > 0xFFFF {
 		frame = frame[:0xFFFF]

@@ -15,9 +15,13 @@ import (
 // Single-frame Parse* with the reference's signatures and results (protocol/{ethernet,ipv4,udp,
 // tcp,icmp}.go), for callers that hold one frame or packet at a time: an Ipv4PktFwdHook
 // (engine/engine.go:132, example/example.go:162-168) or code written against package protocol.
-// Each frame goes through the GPU as a batch of one on a package-level context (Device); there is
-// no CPU path. A batch of frames belongs on Ctx.ParseFramesBatch, which is ~1000x cheaper per
-// frame. protocol.CheckSumEnable is read at every call, as the reference reads it.
+// Each frame goes through the GPU as a batch of one on a package-level context (Device) whose
+// resident consumer serves it: ~7.6 us per frame (DESIGN.md §13.1), against ~22 ns for the one-core
+// C port of the reference's own parse — a GPU round trip per packet is ~350x slower than parsing it
+// on the calling core. These wrappers exist for ported code that needs the reference's signatures;
+// a forward hook that parses every forwarded packet belongs on Ctx.ParseFramesBatch over batches of
+// a few hundred frames or more (the crossover, §13.1). There is no CPU path. protocol.CheckSumEnable
+// is read at every call, as the reference reads it.
 
 // Device is the GPU the single-frame wrappers use (set before the first call).
 var Device = 0
@@ -33,6 +37,11 @@ func parseOne(buf []byte, l3 bool) (Result, error) {
 	if oneCtx == nil {
 		x, err := NewCtx(Device)
 		if err != nil {
+			return Result{}, err
+		}
+		// one frame per call: served by the resident consumer (~8 us, no launch or synchronisation)
+		if err := x.SetResident(64, 1<<16); err != nil {
+			x.Close()
 			return Result{}, err
 		}
 		oneCtx = x

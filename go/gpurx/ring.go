@@ -61,12 +61,29 @@ func (x *RingRx) Poll(netif *NetIfCfg, out []Result, pos []uint64) (int, error) 
 // Commit hands the polled records back to the producer (ReadPacket's tail store).
 func (x *RingRx) Commit() error { return halo(C.halo_rx_ring_commit(x.r)) }
 
+// RingStats mirrors halo_rx_ring_stats_t as a Go type callers outside this package can name (cgo
+// types are private to the package that declares them).
+type RingStats struct {
+	Polls           uint64 // polls that found records
+	Frames          uint64 // frames returned
+	SmallPolls      uint64 // polls on the small path (one launch, or a resident request)
+	ServiceRequests uint64 // small polls served by the resident consumer
+	ServiceLaunches uint64 // resident consumer launches (first use, after idle exits and device drains)
+	WalkNs          uint64 // small polls: the host's ReadPacket walk of the length fields
+	WaitNs          uint64 // small polls: launch + synchronisation, or request to completion
+	ServiceGpuNs    uint64 // resident consumer: GPU time per request, summed
+}
+
 // Stats reports the consumer's poll counters and where small polls spent their time
 // (halo_rx_ring_get_stats).
-func (x *RingRx) Stats() (C.halo_rx_ring_stats_t, error) {
+func (x *RingRx) Stats() (RingStats, error) {
 	var st C.halo_rx_ring_stats_t
-	err := halo(C.halo_rx_ring_get_stats(x.r, &st))
-	return st, err
+	if err := halo(C.halo_rx_ring_get_stats(x.r, &st)); err != nil {
+		return RingStats{}, err
+	}
+	return RingStats{Polls: uint64(st.polls), Frames: uint64(st.frames), SmallPolls: uint64(st.small_polls),
+		ServiceRequests: uint64(st.service_requests), ServiceLaunches: uint64(st.service_launches),
+		WalkNs: uint64(st.walk_ns), WaitNs: uint64(st.wait_ns), ServiceGpuNs: uint64(st.service_gpu_ns)}, nil
 }
 
 // Detach synchronises and frees the consumer (the ring memory must outlive it).

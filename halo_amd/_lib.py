@@ -267,6 +267,8 @@ _PROTOS = {
         ctypes.c_void_p, _u8p, ctypes.c_void_p]),
     "halo_flow_hash_device": (ctypes.c_int, [
         _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
+    "halo_flow_hash_compact_device": (ctypes.c_int, [
+        _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p, ctypes.c_void_p]),
     "halo_route_table_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
     "halo_route_table_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "halo_route_update": (ctypes.c_int, [ctypes.c_void_p, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint32)]),

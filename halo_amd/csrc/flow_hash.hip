@@ -171,13 +171,17 @@ struct LongSecrets {
     uint64_t w8[24];
     uint64_t last[8];
     uint64_t merge[8];
+    uint64_t mid3[16];  // hashLarge's middle terms: the word at 3 + 8k (xxh3.go:124-126)
+    uint64_t mlast[2];  // hashLarge's last term: the words at 119 and 127 (:127)
 };
 
-__device__ __forceinline__ void load_secrets(LongSecrets& s) {
+__device__ __forceinline__ void load_secrets(LongSecrets& s) {  // needs >= 58 threads
     const uint32_t t = threadIdx.x;
     if (t < 24) s.w8[t] = sec64(8 * t);
     else if (t < 32) s.last[t - 24] = sec64(121 + 8 * (t - 24));
     else if (t < 40) s.merge[t - 32] = sec64(11 + 8 * (t - 32));
+    else if (t < 56) s.mid3[t - 40] = sec64(3 + 8 * (t - 40));
+    else if (t < 58) s.mlast[t - 56] = sec64(119 + 8 * (t - 56));
 }
 
 // accumulateStripe (xxh3.go:181-209) for accumulator j on lane j: `in` = input word j of the stripe
@@ -201,7 +205,7 @@ __device__ __forceinline__ void stripe_acc(uint64_t& acc, uint64_t in, uint64_t 
 // hashLong (xxh3.go:132-178) on a group of 8 lanes; lane j = accumulator j. Result in every lane.
 // Stripe words are read as aligned dwords (three when the string is not 4-byte aligned) four
 // stripes at a time, so a lane has up to 12 loads in flight.
-__device__ uint64_t hash_long8(const uint8_t* d, uint32_t len, uint32_t j, const LongSecrets& sec) {
+[[maybe_unused]] __device__ uint64_t hash_long8(const uint8_t* d, uint32_t len, uint32_t j, const LongSecrets& sec) {
     constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
     uint64_t acc = kInit[0];
 #pragma unroll
@@ -284,7 +288,7 @@ __device__ __forceinline__ void stripe_acc2(uint64_t& a0, uint64_t& a1, uint64_t
     a0 += in1 + (uint64_t)(uint32_t)k0 * (k0 >> 32);
     a1 += in0 + (uint64_t)(uint32_t)k1 * (k1 >> 32);
 }
-__device__ uint64_t hash_long4(const uint8_t* d, uint32_t len, uint32_t j, const LongSecrets& sec) {
+[[maybe_unused]] __device__ uint64_t hash_long4(const uint8_t* d, uint32_t len, uint32_t j, const LongSecrets& sec) {
     constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
     uint64_t a0 = kInit[0], a1 = kInit[1];
 #pragma unroll
@@ -357,7 +361,7 @@ __device__ __forceinline__ uint64_t sum8(uint64_t v) {
     v += dpp64<0x141>(v);  // row_half_mirror: lane i <-> 7-i within each 8
     return v;
 }
-__device__ uint64_t hash_mid8(const uint8_t* d, uint32_t len, uint32_t l) {
+[[maybe_unused]] __device__ uint64_t hash_mid8(const uint8_t* d, uint32_t len, uint32_t l) {
     uint64_t v = 0;
     if (len <= 128) {
         const uint32_t levels = len > 96 ? 4u : len > 64 ? 3u : len > 32 ? 2u : 1u;
@@ -446,6 +450,10 @@ __global__ void __launch_bounds__(256) xxh3_short_kernel(const XxhParams p) {
 // hashes them sixteen at a time, one per 4-lane group (eight per 8-lane group with
 // HALO_XXH3_LANES=8) — rank order keeps the strings of a round about equally long, so groups do
 // not idle behind the round's longest string
+#ifndef HALO_XXH3_RUNS
+#define HALO_XXH3_RUNS 1  // the run kernel below (0: this round-3 kernel, kept for A/B)
+#endif
+#if !HALO_XXH3_RUNS
 #ifndef HALO_XXH3_LANES
 #define HALO_XXH3_LANES 4  // lanes per long string: 4 (hash_long4) or 8 (hash_long8)
 #endif
@@ -524,22 +532,224 @@ xxh3_long_kernel(const XxhParams p) {
 #endif
     }
 }
+#endif  // !HALO_XXH3_RUNS
+
+
+// ---- the run kernel (HALO_XXH3_RUNS, the default) ---------------------------------------------
+// the per-class kernels fetched 1.29x the algorithmic bytes — strings packed one byte
+// apart share their first and last 128-byte lines with their neighbours, and a neighbour was hashed
+// at another time (a length-ranked round, or the short-string pass), by then evicted from the L2 —
+// and wrote every 8-byte hash on its own (3.2x the hash bytes).
+//
+// Shape. A wave owns a window of kRunWin consecutive strings and splits it into 16 contiguous RUNS
+// of strings, one per 4-lane group, balanced by their cost in loop iterations (a long string: one
+// iteration per 4 stripes, counting the last stripe; a string <= 240 B: one). Each group hashes its
+// run in index order, so the line a string shares with the next one is read twice in a row by the
+// same group (an L2 hit, often a TCP one), and only the 15 boundaries between runs can miss. Every
+// iteration a group issues up to four 16-byte loads for whatever its current string needs: four
+// stripes of a long string (hashLong, xxh3.go:132-209; accumulateStripe's terms do not depend on the
+// accumulators, so the last stripe is simply one more term of the final block), or the mix16 terms of
+// hashMedium / hashLarge (:94-129, two or four per lane), so all groups share one memory round trip
+// per iteration whatever mix of strings they hold. Strings of <= 16 B take hashSmall (:59-91). The
+// window's hashes collect in LDS and leave as whole lines in string order.
+#ifndef HALO_XXH3_WIN
+#define HALO_XXH3_WIN 256
+#endif
+constexpr uint32_t kRunWin = HALO_XXH3_WIN;  // strings per wave (a multiple of 64)
+[[maybe_unused]] constexpr uint32_t kRunPer = kRunWin / 64;
+struct RunLds {
+    uint64_t off[kRunWin];
+    uint64_t hash[kRunWin];
+    uint32_t len[kRunWin];
+    uint32_t pref[kRunWin];  // exclusive prefix of the strings' iteration counts
+};
+
+[[maybe_unused]] __device__ __forceinline__ uint32_t run_cost(uint32_t len) {
+    return len > 240 ? ((len - 1) / 64 + 4) / 4 : 1u;  // ceil((T + 1) / 4), T = loop stripes
+}
+
+[[maybe_unused]] __device__ __forceinline__ uint64_t quad_sum(uint64_t v) {
+    v += dpp64<0xB1>(v);  // quad_perm 1,0,3,2
+    v += dpp64<0x4E>(v);  // quad_perm 2,3,0,1
+    return v;
+}
+
+#if HALO_XXH3_RUNS
+__global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
+    __shared__ LongSecrets sec;
+    __shared__ RunLds s;
+    load_secrets(sec);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t base = blockIdx.x * kRunWin;
+    const uint32_t cnt = p.n - base < kRunWin ? p.n - base : kRunWin;
+    uint32_t total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kRunPer; ++k) {  // stage the window's metadata; weights' exclusive prefix
+        const uint32_t r = 64 * k + lane;
+        const bool in = r < cnt;
+        const uint32_t len = in ? p.lens[base + r] : 0u;
+        s.len[r] = len;
+        s.off[r] = in ? p.offsets[base + r] : 0ull;
+        const uint32_t w = in ? run_cost(len) : 0u;
+        uint32_t incl = w;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if (lane >= (uint32_t)d) incl += o;
+        }
+        s.pref[r] = total + incl - w;
+        total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    __syncthreads();
+    const uint32_t g = lane >> 2, j = lane & 3u;
+    // run of group g: the strings whose cost starts in [ceil(g * total / 16), ceil((g + 1) * total / 16))
+    auto first_at = [&](uint32_t t) {
+        uint32_t lo = 0, hi = cnt;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (s.pref[m] < t) lo = m + 1;
+            else hi = m;
+        }
+        return lo;
+    };
+    uint32_t idx = first_at((uint32_t)(((uint64_t)g * total + 15) / 16));
+    const uint32_t end = g == 15 ? cnt : first_at((uint32_t)(((uint64_t)(g + 1) * total + 15) / 16));
+    constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+    const uint64_t init0 = j == 0 ? kInit[0] : j == 1 ? kInit[2] : j == 2 ? kInit[4] : kInit[6];
+    const uint64_t init1 = j == 0 ? kInit[1] : j == 1 ? kInit[3] : j == 2 ? kInit[5] : kInit[7];
+    uint32_t len = 0, T = 0, nb = 0, st = 0;
+    const uint8_t* d = p.bytes;
+    uint64_t a0 = init0, a1 = init1;
+    auto begin = [&]() {
+        len = s.len[idx];
+        d = p.bytes + s.off[idx];
+        T = len > 240 ? (len - 1) / 64 : 0u;
+        nb = len > 240 ? (len - 1) / 1024 : 0u;
+        st = 0;
+        a0 = init0;
+        a1 = init1;
+    };
+    if (idx < end) begin();
+    for (;;) {
+        const bool act = idx < end;
+        if (!__builtin_amdgcn_ballot_w64(act)) break;
+        const bool lng = act && len > 240, mid = act && len > 16 && len <= 240, sml = act && len <= 16;
+        const bool large = len > 128;
+        const uint32_t lv = len > 96 ? 4u : len > 64 ? 3u : len > 32 ? 2u : 1u;  // hashMedium's pairs
+        const uint32_t nmid = large ? ((len & ~15u) - 128) / 16 : 0u;           // hashLarge's middle terms
+        uint64_t lo[4], hi[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint8_t* a = d;
+            bool v = false;
+            if (lng) {
+                const uint32_t x = st + u;
+                v = x <= T;
+                a = x < T ? d + 64 * x + 16 * j : d + len - 64 + 16 * j;
+            } else if (mid && !large) {
+                v = u < 2 && j < lv;
+                a = u == 0 ? d + 16 * j : d + len - 16 - 16 * j;
+            } else if (mid) {
+                const uint32_t t = 2 * j + (u & 1u);
+                v = u < 2 || t <= nmid;
+                a = u < 2 ? d + 16 * t : t < nmid ? d + 128 + 16 * t : d + len - 16;
+            }
+            lo[u] = hi[u] = 0;
+            if (v) ld128u(a, lo[u], hi[u]);
+        }
+        uint64_t h = 0;
+        bool have = false;
+        if (lng) {
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t x = st + u;
+                if (x < T) stripe_acc2(a0, a1, lo[u], hi[u], sec.w8[(x & 15u) + 2 * j], sec.w8[(x & 15u) + 2 * j + 1]);
+                else if (x == T) stripe_acc2(a0, a1, lo[u], hi[u], sec.last[2 * j], sec.last[2 * j + 1]);
+            }
+            st += 4;
+            if ((st & 15u) == 0 && (st >> 4) <= nb) {  // a full block ended: scramble (xxh3.go:212-218)
+                a0 ^= a0 >> 47;
+                a1 ^= a1 >> 47;
+                a0 ^= sec.w8[16 + 2 * j];
+                a1 ^= sec.w8[17 + 2 * j];
+                a0 *= P32_1;
+                a1 *= P32_1;
+            }
+            if (st > T) {  // merge (xxh3.go:139-145): pair (2j, 2j+1) with secret 11 + 16j, summed over the quad
+                const uint64_t m = quad_sum(mul_fold64(a0 ^ sec.merge[2 * j], a1 ^ sec.merge[2 * j + 1]));
+                h = avalanche((uint64_t)len * P64_1 + m);
+                have = true;
+            }
+        }
+        if (mid) {
+            uint64_t t01 = 0, t23 = 0;
+            if (!large) {  // hashMedium: pair j = terms (16j, secret 32j) and (len-16-16j, secret 32j+16)
+                if (j < lv)
+                    t01 = mul_fold64(lo[0] ^ sec.w8[4 * j], hi[0] ^ sec.w8[4 * j + 1]) +
+                          mul_fold64(lo[1] ^ sec.w8[4 * j + 2], hi[1] ^ sec.w8[4 * j + 3]);
+                h = avalanche((uint64_t)len * P64_1 + quad_sum(t01));
+            } else {       // hashLarge: terms 2j, 2j+1 of the first eight, then of the middle + last
+                t01 = mul_fold64(lo[0] ^ sec.w8[4 * j], hi[0] ^ sec.w8[4 * j + 1]) +
+                      mul_fold64(lo[1] ^ sec.w8[4 * j + 2], hi[1] ^ sec.w8[4 * j + 3]);
+                const uint64_t acc = avalanche((uint64_t)len * P64_1 + quad_sum(t01));
+#pragma unroll
+                for (uint32_t u = 2; u < 4; ++u) {
+                    const uint32_t t = 2 * j + (u & 1u);
+                    if (t < nmid) t23 += mul_fold64(lo[u] ^ sec.mid3[2 * t], hi[u] ^ sec.mid3[2 * t + 1]);
+                    else if (t == nmid) t23 += mul_fold64(lo[u] ^ sec.mlast[0], hi[u] ^ sec.mlast[1]);
+                }
+                h = avalanche(acc + quad_sum(t23));
+            }
+            have = true;
+        }
+        if (sml) {  // hashSmall: every lane of the group computes it
+            h = hash_upto16(d, len);
+            have = true;
+        }
+        if (have) {
+            if (j == 0) s.hash[idx] = h;
+            ++idx;
+            if (idx < end) begin();
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kRunPer; ++k) {  // the window's hashes as whole lines, in string order
+        const uint32_t r = 64 * k + lane;
+        if (r < cnt) p.out[base + r] = s.hash[r];
+    }
+}
+#endif  // HALO_XXH3_RUNS
 
 // ---- NAT flow keys from parsed records ------------------------------------------------------
 struct FlowParams {
-    const halo_rx_result_t* recs;
+    const void* recs;  // halo_rx_result_t (32 B) or, COMPACT, halo_rx_record16_t (16 B)
     uint32_t n, kind, nat_type, buckets;
     uint64_t* hash;
     uint32_t* bucket;
 };
 
+// Full records: bytes 0..15 (status..dst_ip) and 16..19 (sport, dport) of each 32-byte record —
+// 20 of every 32 bytes, so the memory system delivers the whole record (1.6x the bytes used,
+// VERDICT r3). Compact records carry the same five fields in 16 bytes: one load, nothing unused.
+template <bool COMPACT>
 __global__ void __launch_bounds__(256) flow_hash_kernel(const FlowParams p) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += stride) {
-        // record bytes 0..15 (status..dst_ip) and 16..19 (sport, dport)
-        const uint4 a = reinterpret_cast<const uint4*>(p.recs)[2ull * i];
-        const uint32_t ports = reinterpret_cast<const uint32_t*>(p.recs)[8ull * i + 4];
-        const uint32_t proto = a.y & 0xFFu, src = a.z, dst = a.w;
+        uint32_t proto, src, dst, ports;
+        if constexpr (COMPACT) {  // status, flags, ip_proto, l4_aux | src | dst | sport, dport
+            const uint4 a = reinterpret_cast<const uint4*>(p.recs)[i];
+            proto = (a.x >> 16) & 0xFFu;
+            src = a.y;
+            dst = a.z;
+            ports = a.w;
+        } else {
+            const uint4 a = reinterpret_cast<const uint4*>(p.recs)[2ull * i];
+            ports = reinterpret_cast<const uint32_t*>(p.recs)[8ull * i + 4];
+            proto = a.y & 0xFFu;
+            src = a.z;
+            dst = a.w;
+        }
         const uint64_t h = flowkey::nat_hash(proto, src, dst, ports & 0xFFFFu, ports >> 16, p.kind, p.nat_type);
         p.hash[i] = h;
         if (p.bucket) p.bucket[i] = (uint32_t)(h % p.buckets);  // hashmap/hashmap.go:64
@@ -570,15 +780,19 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
                                                                        (halo::kShortScan / 64))),
                        dim3(256), 0, s, p);
 #endif
+#if HALO_XXH3_RUNS
+    hipLaunchKernelGGL(halo::xxh3_run_kernel, dim3((n + halo::kRunWin - 1) / halo::kRunWin), dim3(64), 0, s, p);
+#else
     constexpr uint32_t wpb = HALO_XXH3_LONG_BLOCK / 64;
     const uint32_t long_blocks = (uint32_t)(((uint64_t)halo::blocks_for(n) * 4 + wpb - 1) / wpb);
     hipLaunchKernelGGL(halo::xxh3_long_kernel, dim3(long_blocks), dim3(HALO_XXH3_LONG_BLOCK), 0, s, p);
+#endif
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 
-extern "C" HALO_API int halo_flow_hash_device(const halo_rx_result_t* d_records, uint32_t n, uint32_t kind,
-                                              uint32_t nat_type, uint64_t* d_hash, uint32_t bucket_count,
-                                              uint32_t* d_bucket, halo_stream_t stream) {
+namespace {
+int flow_hash(const void* d_records, bool compact, uint32_t n, uint32_t kind, uint32_t nat_type, uint64_t* d_hash,
+              uint32_t bucket_count, uint32_t* d_bucket, halo_stream_t stream) {
     if (kind > HALO_FLOW_NAT_WAN) return HALO_E_INVAL;
     if (d_bucket && bucket_count == 0) return HALO_E_INVAL;
     if (n == 0) return HALO_OK;
@@ -588,7 +802,24 @@ extern "C" HALO_API int halo_flow_hash_device(const halo_rx_result_t* d_records,
     int rc = halo::check_device();
     if (rc) return rc;
     halo::FlowParams p{d_records, n, kind, nat_type, bucket_count, d_hash, d_bucket};
-    hipLaunchKernelGGL(halo::flow_hash_kernel, dim3(halo::blocks_for(n)), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), p);
+    if (compact)
+        hipLaunchKernelGGL(halo::flow_hash_kernel<true>, dim3(halo::blocks_for(n)), dim3(256), 0,
+                           static_cast<hipStream_t>(stream), p);
+    else
+        hipLaunchKernelGGL(halo::flow_hash_kernel<false>, dim3(halo::blocks_for(n)), dim3(256), 0,
+                           static_cast<hipStream_t>(stream), p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+}  // namespace
+
+extern "C" HALO_API int halo_flow_hash_device(const halo_rx_result_t* d_records, uint32_t n, uint32_t kind,
+                                              uint32_t nat_type, uint64_t* d_hash, uint32_t bucket_count,
+                                              uint32_t* d_bucket, halo_stream_t stream) {
+    return flow_hash(d_records, false, n, kind, nat_type, d_hash, bucket_count, d_bucket, stream);
+}
+
+extern "C" HALO_API int halo_flow_hash_compact_device(const halo_rx_record16_t* d_records, uint32_t n, uint32_t kind,
+                                                      uint32_t nat_type, uint64_t* d_hash, uint32_t bucket_count,
+                                                      uint32_t* d_bucket, halo_stream_t stream) {
+    return flow_hash(d_records, true, n, kind, nat_type, d_hash, bucket_count, d_bucket, stream);
 }

@@ -39,13 +39,17 @@ def GetHashCodeXXH3(data, offsets, lens, out=None, stream=None):  # noqa: N802 (
 
 def flow_hash(records, kind: int = FLOW_NAT_LAN, nat_type: int = NatTypeSymmetric, buckets: int = 0,
               stream=None):
-    """(hash, bucket) for a cuda uint8 [n, 32] record tensor (parse_frames_batch output)."""
+    """(hash, bucket) for a cuda uint8 [n, 32] record tensor (parse_frames_batch output), or a
+    [n, 16] tensor of compact records (halo_flow_hash_compact_device)."""
     import torch
 
+    width = int(records.shape[1]) if records.dim() == 2 else 32
+    assert width in (16, 32), "records: uint8 [n, 32] (full) or [n, 16] (compact)"
     n = int(records.shape[0]) if records.dim() == 2 else int(records.numel()) // 32
     h = torch.empty(n, dtype=torch.int64, device=records.device)
     b = torch.empty(n, dtype=torch.int32, device=records.device) if buckets else None
-    rc = _lib.lib.halo_flow_hash_device(_lib.ptr(records), n, kind, nat_type, _lib.ptr(h), buckets, _lib.ptr(b),
-                                        _stream(stream))
-    _lib.check("halo_flow_hash_device", rc)
+    fn = "halo_flow_hash_compact_device" if width == 16 else "halo_flow_hash_device"
+    rc = getattr(_lib.lib, fn)(_lib.ptr(records), n, kind, nat_type, _lib.ptr(h), buckets, _lib.ptr(b),
+                               _stream(stream))
+    _lib.check(fn, rc)
     return h, b

@@ -587,6 +587,13 @@ HALO_API int halo_flow_hash_device(const halo_rx_result_t* d_records, uint32_t n
                                    uint64_t* d_hash, uint32_t bucket_count, uint32_t* d_bucket,
                                    halo_stream_t stream);
 
+/* The same over compact records (HALO_RX_RECORD_COMPACT parse output): the five key fields are the
+ * whole 16-byte record, so nothing is fetched that the key does not use (a full record's key fields
+ * are 20 of its 32 bytes). Identical hashes and buckets for the same frames.                      */
+HALO_API int halo_flow_hash_compact_device(const halo_rx_record16_t* d_records, uint32_t n, uint32_t kind,
+                                           uint32_t nat_type, uint64_t* d_hash, uint32_t bucket_count,
+                                           uint32_t* d_bucket, halo_stream_t stream);
+
 /* The rx parse (halo_rx_parse_batch_device, same arguments and records) with the NAT flow key
  * of every record hashed in the same pass, exactly as halo_flow_hash_device would hash the
  * records it writes: the engine's receive -> forward -> NAT lookup chain without re-reading the

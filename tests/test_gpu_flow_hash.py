@@ -102,6 +102,35 @@ def test_flow_hash_golden_and_imix_records(dev, oracle_lib, golden, kind, nat_ty
                 assert np.array_equal(b.cpu().numpy().view(np.uint32), wb)
 
 
+@pytest.mark.parametrize("kind", [0, 1])
+def test_flow_hash_compact_records(dev, oracle_lib, kind):
+    """halo_flow_hash_compact_device over HALO_RX_RECORD_COMPACT parse output = the full records'
+    hashes and buckets (oracle)."""
+    import torch
+
+    from halo_amd import hashcode, protocol, synth
+    from halo_amd._lib import HALO_RX_RECORD_COMPACT, NetIf
+
+    lay = synth.layout(100_000, size_mode=1, proto_mode=3, mutate_shift=4, first_index=777)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    full = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                       max_len_hint=1500)
+    comp = torch.empty((lay["n"], 16), dtype=torch.uint8, device=dev)
+    rc = protocol._lib.lib.halo_rx_parse_batch_device(
+        fr["bytes"].data_ptr(), fr["offsets_dw"].data_ptr(), fr["lens"].data_ptr(), lay["n"],
+        1 | HALO_RX_RECORD_COMPACT, NetIf.make(), 1500, comp.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    for nat_type in (0, 1):
+        for buckets in (0, 1 << 20):
+            hf, bf = hashcode.flow_hash(full, kind, nat_type, buckets)
+            hc, bc = hashcode.flow_hash(comp, kind, nat_type, buckets)
+            wh, wb = oracle_lib.flow_hash_batch(protocol.records(full), kind, nat_type, buckets)
+            assert np.array_equal(hc.cpu().numpy().view(np.uint64), wh)
+            assert np.array_equal(hf.cpu().numpy().view(np.uint64), wh)
+            if buckets:
+                assert np.array_equal(bc.cpu().numpy().view(np.uint32), wb)
+
+
 def test_flow_hash_validation(dev):
     from halo_amd import _lib
 

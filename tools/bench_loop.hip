@@ -113,6 +113,16 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_flow_steps(
     return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
 }
 
+extern "C" __attribute__((visibility("default"))) int halo_bench_flow_compact_steps(
+    int nbatch, const halo_rx_record16_t* const* recs, uint32_t n, uint32_t kind, uint32_t nat_type, uint64_t* hash,
+    uint32_t buckets, uint32_t* bucket, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0) return HALO_E_INVAL;
+    auto launch = [&](int k) {
+        return halo_flow_hash_compact_device(recs[k % nbatch], n, kind, nat_type, hash, buckets, bucket, stream);
+    };
+    return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
+}
+
 extern "C" __attribute__((visibility("default"))) int halo_bench_xxh3_steps(
     int nbatch, const uint8_t* const* bytes, const uint64_t* const* offsets, const uint32_t* const* lens, uint32_t n,
     uint64_t* hash, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {

@@ -43,8 +43,11 @@ def alg_bytes():
         lay = synth.layout(n, **kw, ragged=not slen)
         frames = int(lay["lens"].astype("int64").sum())
         meta = 0 if slen else 6 * n
-        if name.startswith("flow_hash"):  # record bytes 0..19 in; hash + bucket out
-            out[name] = (20 * n, 12 * n)
+        if name.startswith("flow_hash"):  # record bytes 0..19 (compact: the 16 B record) in; hash + bucket out
+            out[name] = ((16 if name.endswith("_compact") else 20) * n, 12 * n)
+            continue
+        if name == "config2_batch_stream":  # `rot` batches per launch
+            out[name] = (_rot * (frames + meta), _rot * 32 * n)
             continue
         if name.startswith("lo_drain"):  # 50 B packets + offset/len in, 32 B record out
             out[name] = (56 * n, 32 * n)

@@ -24,10 +24,13 @@ WORKLOADS = [
     ("config5_jumbo_9000B_tcp_4M_ext", dict(length=9000, proto_mode=1, strided=True), 4 << 20, 1, 3, 9000, 3, 0),
     # PacketHandle's LoChan drain (§8a row a12): 1M x 50 B TxIpv4 loopback copies, HALO_RX_L3_START
     ("lo_drain_1M_50B", dict(length=64), 1 << 20, 1, 20, 0, 1 | 0x10, 64),
+    # config 2's batches handed over 8 per call (halo_rx_parse_batches_device: one launch per 8M frames)
+    ("config2_batch_stream", dict(length=64), 1 << 20, 8, 10, 0, 1, 64),
     # forward / transmit rewrite (§8f row f2): bench.TX_BENCH_STEPS on the config 2 frames
     ("tx_config2", dict(length=64), 1 << 20, 8, 20, 0, 1, 64),
     # flow-key hashing (§8f row f3): NatWanFlowHash + bucket on the parsed config 2 records
     ("flow_hash_config2", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
+    ("flow_hash_config2_compact", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
     # halo's packet ring (§8f row f1): the record walk over 1M 64 B records (68 MB span)
     ("ring_scan_1M_64B", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
     # transmit construction (§8f row f2, Build*): bench.tx_build_secondary's two workloads
@@ -89,9 +92,9 @@ def main():
             from halo_amd import protocol
 
             fb = bs[0]["bytes"][:n * 64].view(n, 64)  # uniform 64 B frames, packed
-            pk = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
-            pk[:, :50] = fb[:, 14:64]  # their IPv4 packets: what Ipv4RouteForward puts in a LoChan
-            offs = torch.arange(n, dtype=torch.int32, device=dev) * 16
+            pk = torch.zeros((n, 52), dtype=torch.uint8, device=dev)
+            pk[:, :50] = fb[:, 14:64]  # their IPv4 packets: what Ipv4RouteForward puts in a LoChan,
+            offs = torch.arange(n, dtype=torch.int32, device=dev) * 13  # packed at 4-byte aligned starts
             fl = torch.full((n,), 50, dtype=torch.int16, device=dev)
             torch.cuda.synchronize()
             for i in range(launches):
@@ -126,18 +129,34 @@ def main():
             del out, frames, pay, desc_d, b
             torch.cuda.empty_cache()
             continue
+        if name == "config2_batch_stream":
+            from halo_amd import protocol
+
+            outs = [torch.empty((n, 32), dtype=torch.uint8, device=dev) for _ in bs]
+            for i in range(launches):
+                protocol.parse_frames_batches([(b["bytes"], b["offsets_dw"], b["lens"], o) for b, o in zip(bs, outs)],
+                                              netif=netif, max_len_hint=64)
+            torch.cuda.synchronize()
+            print(f"{name}: {launches} launches of {len(bs)} x {n} frames", flush=True)
+            del bs, out, outs
+            torch.cuda.empty_cache()
+            continue
         if name.startswith("flow_hash"):
             from halo_amd import protocol
 
             fr = bs[0]
-            protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=netif, max_len_hint=64,
-                                        out=out)
+            compact = name.endswith("_compact")
+            if compact:
+                out = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+            _lib.check("parse", _lib.lib.halo_rx_parse_batch_device(
+                fr["bytes"].data_ptr(), fr["offsets_dw"].data_ptr(), fr["lens"].data_ptr(), n,
+                1 | (_lib.HALO_RX_RECORD_COMPACT if compact else 0), netif, 64, out.data_ptr(), None, stream))
             h = torch.empty(n, dtype=torch.int64, device=dev)
             bk = torch.empty(n, dtype=torch.int32, device=dev)
+            fn = _lib.lib.halo_flow_hash_compact_device if compact else _lib.lib.halo_flow_hash_device
             torch.cuda.synchronize()
             for i in range(launches):
-                _lib.check("flow", _lib.lib.halo_flow_hash_device(out.data_ptr(), n, 1, 0, h.data_ptr(), 1 << 20,
-                                                                  bk.data_ptr(), stream))
+                _lib.check("flow", fn(out.data_ptr(), n, 1, 0, h.data_ptr(), 1 << 20, bk.data_ptr(), stream))
             torch.cuda.synchronize()
             print(f"{name}: {launches} launches of {n} records", flush=True)
             del bs, out
