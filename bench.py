@@ -514,6 +514,10 @@ def tx_build_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
                      "kernel_ms": round(k, 5), "roofline": roofline(alg, k, load_traffic(name)),
                      "alg_bytes_per_launch": alg,
                      "what": "TxUdp -> BuildUdpPkt -> TxIpv4 (BuildIpv4Pkt, iphId) -> TxEthernet (BuildEthFrm)"}
+        # the same byte shape with no work: descriptors + payloads in, the frame slots + lengths +
+        # results out (coalesced 16-byte loads and stores)
+        with_probe(res[name]["roofline"], size_matched_probe(dev, n * (40 + plen), n * (stride + 3), d, nbuf=1,
+                                                             steps=20), k)
         if with_cpu:
             from oracle import oracle as O
 

@@ -280,3 +280,41 @@ def test_tx_build_desc_layout_and_validation(tmp_path):
     assert L.halo_tx_build_batch_device(*args(wsbytes=4)) == -1  # workspace too small
     if not torch.cuda.is_available():
         assert L.halo_tx_build_batch_device(*args()) == _lib.HALO_E_NODEV
+
+
+def test_round4_structs_and_validation(tmp_path):
+    """halo_rx_host_stats_t / halo_rx_batch_desc_t agree with the Python mirrors; the round-4 entry
+    points refuse bad arguments before touching a device."""
+    import ctypes
+
+    from halo_amd import _lib
+
+    src = tmp_path / "l4.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "halo_rx.h"\nint main(void){\n'
+        + "".join(f'printf("%zu\\n", offsetof(halo_rx_host_stats_t, {f}));\n' for f in _lib.HOST_STATS_DTYPE.names)
+        + 'printf("%zu\\n%zu\\n%zu\\n%zu\\n", sizeof(halo_rx_host_stats_t), sizeof(halo_rx_batch_desc_t), '
+          'offsetof(halo_rx_batch_desc_t, d_out), offsetof(halo_rx_batch_desc_t, n));\nreturn 0;}\n')
+    exe = tmp_path / "l4"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    names = _lib.HOST_STATS_DTYPE.names
+    assert vals[:len(names)] == [_lib.HOST_STATS_DTYPE.fields[f][1] for f in names]
+    assert vals[len(names)] == _lib.HOST_STATS_DTYPE.itemsize
+    assert vals[len(names) + 1:] == [ctypes.sizeof(_lib.BatchDesc), _lib.BatchDesc.d_out.offset, _lib.BatchDesc.n.offset]
+    L, n = _lib.lib, _lib.NetIf.make()
+    assert L.halo_rx_host_ctx_set_resident(None, 64, 0) == _lib.HALO_E_INVAL
+    assert L.halo_rx_host_ctx_set_service_timeout(None, 1) == _lib.HALO_E_INVAL
+    assert L.halo_rx_host_ctx_get_stats(None, None) == _lib.HALO_E_INVAL
+    assert L.halo_rx_ring_set_service_timeout(None, 1) == _lib.HALO_E_INVAL
+    descs = (_lib.BatchDesc * 33)()
+    assert L.halo_rx_parse_batches_device(None, 1, 1, n, 64, None, None) == _lib.HALO_E_INVAL
+    assert L.halo_rx_parse_batches_device(ctypes.cast(descs, ctypes.c_void_p), 0, 1, n, 64, None, None) == _lib.HALO_E_INVAL
+    assert L.halo_rx_parse_batches_device(ctypes.cast(descs, ctypes.c_void_p), 33, 1, n, 64, None, None) == _lib.HALO_E_INVAL
+    # all batches empty: nothing to do
+    assert L.halo_rx_parse_batches_device(ctypes.cast(descs, ctypes.c_void_p), 32, 1, n, 64, None, None) == 0
+    buf = np.zeros(64, np.uint8)
+    descs[0] = _lib.BatchDesc(buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, buf.ctypes.data + 4, 1, 0)
+    assert L.halo_rx_parse_batches_device(ctypes.cast(descs, ctypes.c_void_p), 1, 1, n, 64, None,
+                                          None) == _lib.HALO_E_INVAL  # misaligned records
+    assert L.halo_flow_hash_compact_device(None, 0, 2, 0, None, 0, None, None) == _lib.HALO_E_INVAL

@@ -85,6 +85,7 @@ for s in "$@"; do
     dropin) step dropin 600 python tools/bench_dropin.py ;;
     tmulti) step pytest_multi 600 python -u -m pytest tests/test_gpu_multi_batch.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     tnew)  step pytest_new 900 python -u -m pytest tests/test_gpu_host_resident.py tests/test_gpu_multi_batch.py tests/test_gpu_ring.py tests/test_gpu_single_frame.py tests/test_gpu_engine_cadence.py tests/test_gpu_route.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    ttxb)  step pytest_txb 600 python -u -m pytest tests/test_gpu_tx_build.py tests/test_gpu_loopback.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     txx)   step pytest_xxh3 600 python -u -m pytest tests/test_gpu_flow_hash.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
   esac
