@@ -57,6 +57,13 @@ enum SynthSlot : uint32_t {
 
 int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 
+// Partial status histograms of an rx launch (flush_hist, rx_parse.hip): kHistSlots slots of
+// kHistStride u32, one per block modulo kHistSlots, zero between launches. One array per (device,
+// stream) the library has parsed on with a histogram, allocated at first use and kept: launches on
+// one stream run in order, so they can share it.
+constexpr uint32_t kHistSlots = 1024, kHistStride = 16;
+uint32_t* hist_slots(hipStream_t s);  // nullptr: allocation failed
+
 // The resident small-poll consumer of a ring attached with HALO_RING_PERSISTENT (ring_rx.hip
 // drives it, rx_parse.hip runs it): kSvcGroups workgroups that wait on this control block, in
 // pinned host memory, for a request, parse its n frames as the lane kernel would (frames at

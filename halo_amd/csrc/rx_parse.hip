@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <map>
+#include <mutex>
 
 #include "device_util.h"
 #include "flow_key.h"
@@ -484,6 +486,11 @@ __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, boo
     frame_finish<G, FUSE, U, R0, kL3<LAYOUT>>(p, i, present, gl, grp_base, st, hist);
 }
 
+// The block's counts go to one of kHistSlots partial histograms (p.hist is the launch's slot array,
+// hist_slots): device-scope atomics on one address serialise at the memory side, ~10 ns each, and
+// 16384 one-wave blocks adding to the caller's 14 counters cost 170 us on a 21 us launch (bench
+// r4b: config2_status_histogram). Spread over 1024 slots they run in parallel; hist_finalize folds
+// the slots into the caller's counters after the launch.
 __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     if (!p.hist) return;
     uint32_t ok = hist.ok;
@@ -491,7 +498,29 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     for (int m = 1; m < 64; m <<= 1) ok += __shfl_xor(ok, m, 64);
     if ((threadIdx.x & 63u) == 0 && ok) atomicAdd(&hist.s[HALO_RX_OK], ok);
     __syncthreads();
-    if (threadIdx.x < HALO_RX_STATUS_COUNT && hist.s[threadIdx.x]) atomicAdd(&p.hist[threadIdx.x], hist.s[threadIdx.x]);
+    uint32_t* slot = p.hist + (blockIdx.x & (kHistSlots - 1u)) * kHistStride;
+    if (threadIdx.x < HALO_RX_STATUS_COUNT && hist.s[threadIdx.x]) atomicAdd(&slot[threadIdx.x], hist.s[threadIdx.x]);
+}
+
+// Sums the slots of hist_slots into the caller's counters and zeroes them for the next launch on the
+// stream: one block, thread t owns slot t.
+__global__ void __launch_bounds__(kHistSlots) hist_finalize(uint32_t* slots, uint32_t* out) {
+    __shared__ uint32_t s_tot[HALO_RX_STATUS_COUNT];
+    const uint32_t t = threadIdx.x;
+    if (t < HALO_RX_STATUS_COUNT) s_tot[t] = 0;
+    __syncthreads();
+    uint32_t* slot = slots + t * kHistStride;
+#pragma unroll
+    for (uint32_t k = 0; k < HALO_RX_STATUS_COUNT; ++k) {
+        uint32_t v = slot[k];
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
+        if ((t & 63u) == 0 && v) atomicAdd(&s_tot[k], v);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kHistStride; ++k) slot[k] = 0;
+    __syncthreads();
+    if (t < HALO_RX_STATUS_COUNT && s_tot[t]) atomicAdd(&out[t], s_tot[t]);
 }
 
 // Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
@@ -1376,10 +1405,12 @@ int pick_variant(uint32_t max_len, bool uniform, bool dense, uint32_t flags) {
     return 16;
 }
 
-int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, hipStream_t s) {
+int launch_parse(const RxParams& p_in, int layout, uint32_t max_len, bool uniform, hipStream_t s) {
     // ragged batches are taken as packed back to back (the stream kernel checks each window and
     // sums a sparse one frame by frame); strided frames of one length are dense when the stride
     // wastes < 1/4; strided frames with their own lengths may be anything below the stride
+    RxParams p = p_in;
+    if (p.hist && !(p.hist = hist_slots(s))) return HALO_E_NOMEM;  // the kernel counts into the slots
     const bool dense = layout == 0 || layout == 3 || (layout == 2 && p.stride <= max_len + max_len / 4 + 64);
     const int v = pick_variant(max_len, uniform, dense, p.flags);
     hipError_t e;
@@ -1391,6 +1422,10 @@ int launch_parse(const RxParams& p, int layout, uint32_t max_len, bool uniform, 
         case 1: e = launch_variant<1>(p, v, s); break;
         case 3: e = launch_variant<3>(p, v, s); break;  // LoChan packets: plain parse only
         default: e = launch_variant<2>(p, v, s); break;
+    }
+    if (e == hipSuccess && p.hist) {
+        hipLaunchKernelGGL(hist_finalize, dim3(1), dim3(kHistSlots), 0, s, p.hist, p_in.hist);
+        e = hipGetLastError();
     }
     return e == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
@@ -1415,6 +1450,24 @@ int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* 
 }
 
 }  // namespace
+
+uint32_t* hist_slots(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, uint32_t*> slots;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    auto& p = slots[{dev, s}];
+    if (!p) {
+        const size_t bytes = sizeof(uint32_t) * kHistSlots * kHistStride;
+        if (hipMalloc((void**)&p, bytes) != hipSuccess || hipMemsetAsync(p, 0, bytes, s) != hipSuccess) {
+            (void)hipGetLastError();
+            if (p) (void)hipFree(p);
+            p = nullptr;
+        }
+    }
+    return p;
+}
 }  // namespace halo
 
 extern "C" HALO_API int halo_rx_parse_batch_device(const uint8_t* d_bytes, const uint32_t* d_offsets_dw,
@@ -1551,13 +1604,15 @@ extern "C" HALO_API int halo_rx_parse_batches_device(const halo_rx_batch_desc_t*
     }
     mp.k = k;
     mp.p.n = 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (d_status_hist && !(mp.p.hist = halo::hist_slots(s))) return HALO_E_NOMEM;
     constexpr uint32_t wpb = HALO_RX_LANE_BLOCK / 64;
     const dim3 grid(halo::grid_for(windows * 64u, 64, HALO_RX_LANE_MAX_BLOCKS * 4 / wpb, wpb));
-    hipStream_t s = static_cast<hipStream_t>(stream);
     if (flags & HALO_RX_L3_START)
         hipLaunchKernelGGL(halo::rx_lane_multi_kernel<3>, grid, dim3(HALO_RX_LANE_BLOCK), HALO_RX_LANE_LDS_PAD, s, mp);
     else
         hipLaunchKernelGGL(halo::rx_lane_multi_kernel<0>, grid, dim3(HALO_RX_LANE_BLOCK), HALO_RX_LANE_LDS_PAD, s, mp);
+    if (d_status_hist) hipLaunchKernelGGL(halo::hist_finalize, dim3(1), dim3(halo::kHistSlots), 0, s, mp.p.hist, d_status_hist);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 

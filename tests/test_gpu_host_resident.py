@@ -282,11 +282,11 @@ def test_drains_while_a_persistent_ring_is_polled(dev, oracle_lib):
     finally:
         stop.set()
         th.join(timeout=30)
+        st = cons.stats()
         cons.close()
     assert not th.is_alive()
     assert not errors, errors[0]
     assert polls[0] > 10
     worst = {k: max(v) for k, v in durations.items()}
     assert all(v < 1.0 for v in worst.values()), worst
-    st = cons.stats()
     assert st["service_requests"] > 0, st
