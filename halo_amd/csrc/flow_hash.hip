@@ -564,8 +564,15 @@ struct RunLds {
     uint32_t pref[kRunWin];  // exclusive prefix of the strings' iteration counts
 };
 
+// Stripes per iteration of a long string (16-byte loads per lane in flight): 8 halves the
+// dependent memory round trips a wave makes (a window of 256 KCP-sized strings is ~56 of them at 4)
+#ifndef HALO_XXH3_RUN_B
+#define HALO_XXH3_RUN_B 8
+#endif
+constexpr uint32_t kRunB = HALO_XXH3_RUN_B;
+static_assert(kRunB == 4 || kRunB == 8, "a batch must not straddle a 16-stripe block");
 [[maybe_unused]] __device__ __forceinline__ uint32_t run_cost(uint32_t len) {
-    return len > 240 ? ((len - 1) / 64 + 4) / 4 : 1u;  // ceil((T + 1) / 4), T = loop stripes
+    return len > 240 ? ((len - 1) / 64 + kRunB) / kRunB : 1u;  // ceil((T + 1) / B), T = loop stripes
 }
 
 [[maybe_unused]] __device__ __forceinline__ uint64_t quad_sum(uint64_t v) {
@@ -637,15 +644,16 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
         const bool large = len > 128;
         const uint32_t lv = len > 96 ? 4u : len > 64 ? 3u : len > 32 ? 2u : 1u;  // hashMedium's pairs
         const uint32_t nmid = large ? ((len & ~15u) - 128) / 16 : 0u;           // hashLarge's middle terms
-        uint64_t lo[4], hi[4];
+        uint64_t lo[kRunB], hi[kRunB];
 #pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
+        for (uint32_t u = 0; u < kRunB; ++u) {
             const uint8_t* a = d;
             bool v = false;
             if (lng) {
                 const uint32_t x = st + u;
                 v = x <= T;
                 a = x < T ? d + 64 * x + 16 * j : d + len - 64 + 16 * j;
+            } else if (u >= 4) {  // the short hashes need four loads at most
             } else if (mid && !large) {
                 v = u < 2 && j < lv;
                 a = u == 0 ? d + 16 * j : d + len - 16 - 16 * j;
@@ -661,12 +669,12 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
         bool have = false;
         if (lng) {
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
+            for (uint32_t u = 0; u < kRunB; ++u) {
                 const uint32_t x = st + u;
                 if (x < T) stripe_acc2(a0, a1, lo[u], hi[u], sec.w8[(x & 15u) + 2 * j], sec.w8[(x & 15u) + 2 * j + 1]);
                 else if (x == T) stripe_acc2(a0, a1, lo[u], hi[u], sec.last[2 * j], sec.last[2 * j + 1]);
             }
-            st += 4;
+            st += kRunB;
             if ((st & 15u) == 0 && (st >> 4) <= nb) {  // a full block ended: scramble (xxh3.go:212-218)
                 a0 ^= a0 >> 47;
                 a1 ^= a1 >> 47;

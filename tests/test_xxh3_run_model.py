@@ -1,6 +1,6 @@
 """CPU: the schedule of flow_hash.hip's run kernel (xxh3_run_kernel), restated in Python and checked
 against the independent XXH3 restatement (oracle/ref_xxh3_py.py, pinned to the published sanity
-vectors). The kernel reorders hashLong (hashcode/xxh3.go:132-209) into batches of four stripes with
+vectors). The kernel reorders hashLong (hashcode/xxh3.go:132-209) into batches of B stripes with
 the last stripe as one more term of the final block, scrambles when a batch closes a full block, and
 splits hashMedium / hashLarge (:94-129) into per-lane term pairs; a window's strings are split into
 16 contiguous runs balanced by iteration count. This model follows those rules step by step (the
@@ -16,8 +16,11 @@ def _term(lo, hi, s0, s1):
     return _mulfold(lo ^ s0, hi ^ s1)
 
 
+B = 8  # HALO_XXH3_RUN_B
+
+
 def run_cost(n: int) -> int:
-    return ((n - 1) // 64 + 4) // 4 if n > 240 else 1
+    return ((n - 1) // 64 + B) // B if n > 240 else 1
 
 
 def model_long(d: bytes) -> int:
@@ -28,7 +31,7 @@ def model_long(d: bytes) -> int:
     iters = 0
     while True:
         iters += 1
-        for u in range(4):
+        for u in range(B):
             x = st + u
             if x > T:
                 continue
@@ -38,7 +41,7 @@ def model_long(d: bytes) -> int:
                 k = v ^ _r64(SECRET, soff + 8 * j)
                 acc[j ^ 1] = (acc[j ^ 1] + v) & M64
                 acc[j] = (acc[j] + (k & 0xFFFFFFFF) * (k >> 32)) & M64
-        st += 4
+        st += B
         if st % 16 == 0 and st // 16 <= nb:
             for j in range(8):
                 a = acc[j] ^ (acc[j] >> 47)
