@@ -392,7 +392,7 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
 // chunk (the masked path), finishes the checksum from the LDS slot, and the wave stores the 64
 // frames' head chunks four lanes per frame from LDS.
 #ifndef HALO_TXB_FLAT
-#define HALO_TXB_FLAT 1
+#define HALO_TXB_FLAT 0  // measured slower than build_big: see DESIGN.md §13.6
 #endif
 #ifndef HALO_TXB_FLAT_U
 #define HALO_TXB_FLAT_U 4

@@ -87,6 +87,11 @@ for s in "$@"; do
     tnew)  step pytest_new 900 python -u -m pytest tests/test_gpu_host_resident.py tests/test_gpu_multi_batch.py tests/test_gpu_ring.py tests/test_gpu_single_frame.py tests/test_gpu_engine_cadence.py tests/test_gpu_route.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     ttxb)  step pytest_txb 600 python -u -m pytest tests/test_gpu_tx_build.py tests/test_gpu_loopback.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     txx)   step pytest_xxh3 600 python -u -m pytest tests/test_gpu_flow_hash.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    prof4) PK_ARGS="config2 config2_batch_stream lo_drain_1M_50B flow_hash_config2 flow_hash_config2_compact tx_build_udp_256k_1514B"
+           step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step krd 600 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krd" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step kwrq 600 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/kwrq" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step ksq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ksq" -o run -- python3 tools/prof_kernels.py $PK_ARGS ;;
     *) echo "unknown step $s" ;;
   esac
 done
