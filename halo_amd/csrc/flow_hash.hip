@@ -384,6 +384,7 @@ struct XxhParams {
     const uint32_t* lens;
     uint32_t n;
     uint64_t* out;
+    uint32_t win;  // strings per wave of the run kernel (<= kRunWin)
 };
 
 // strings <= 240 B (the long ones are left to xxh3_long_kernel). A wave scans kShortScan strings
@@ -581,14 +582,24 @@ static_assert(kRunB == 4 || kRunB == 8, "a batch must not straddle a 16-stripe b
     return v;
 }
 
+// Branch-free iteration (HALO_XXH3_BF): every lane issues all kRunB loads, an idle slot (past a
+// string's last stripe, a short string, a finished group) reading this zero line instead of
+// branching around the load; the long path selects secrets and drops terms past the last stripe.
+#ifndef HALO_XXH3_BF
+#define HALO_XXH3_BF 1
+#endif
+#if HALO_XXH3_BF
+__device__ const uint8_t g_xxh3_pad[64] = {};
+#endif
+
 #if HALO_XXH3_RUNS
 __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
     __shared__ LongSecrets sec;
     __shared__ RunLds s;
     load_secrets(sec);
     const uint32_t lane = threadIdx.x;
-    const uint32_t base = blockIdx.x * kRunWin;
-    const uint32_t cnt = p.n - base < kRunWin ? p.n - base : kRunWin;
+    const uint32_t base = blockIdx.x * p.win;
+    const uint32_t cnt = p.n - base < p.win ? p.n - base : p.win;
     uint32_t total = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kRunPer; ++k) {  // stage the window's metadata; weights' exclusive prefix
@@ -662,8 +673,12 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
                 v = u < 2 || t <= nmid;
                 a = u < 2 ? d + 16 * t : t < nmid ? d + 128 + 16 * t : d + len - 16;
             }
+#if HALO_XXH3_BF
+            ld128u(v ? a : g_xxh3_pad, lo[u], hi[u]);  // no branch: idle slots read 16 zero bytes
+#else
             lo[u] = hi[u] = 0;
             if (v) ld128u(a, lo[u], hi[u]);
+#endif
         }
         uint64_t h = 0;
         bool have = false;
@@ -671,8 +686,19 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
 #pragma unroll
             for (uint32_t u = 0; u < kRunB; ++u) {
                 const uint32_t x = st + u;
+#if HALO_XXH3_BF
+                // select the secret and drop the term past the last stripe instead of branching
+                const uint64_t s0 = x < T ? sec.w8[(x & 15u) + 2 * j] : sec.last[2 * j];
+                const uint64_t s1 = x < T ? sec.w8[(x & 15u) + 2 * j + 1] : sec.last[2 * j + 1];
+                const uint64_t k0 = lo[u] ^ s0, k1 = hi[u] ^ s1;
+                const uint64_t t0 = hi[u] + (uint64_t)(uint32_t)k0 * (k0 >> 32);
+                const uint64_t t1 = lo[u] + (uint64_t)(uint32_t)k1 * (k1 >> 32);
+                a0 += x <= T ? t0 : 0ull;
+                a1 += x <= T ? t1 : 0ull;
+#else
                 if (x < T) stripe_acc2(a0, a1, lo[u], hi[u], sec.w8[(x & 15u) + 2 * j], sec.w8[(x & 15u) + 2 * j + 1]);
                 else if (x == T) stripe_acc2(a0, a1, lo[u], hi[u], sec.last[2 * j], sec.last[2 * j + 1]);
+#endif
             }
             st += kRunB;
             if ((st & 15u) == 0 && (st >> 4) <= nb) {  // a full block ended: scramble (xxh3.go:212-218)
@@ -789,7 +815,21 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
                        dim3(256), 0, s, p);
 #endif
 #if HALO_XXH3_RUNS
-    hipLaunchKernelGGL(halo::xxh3_run_kernel, dim3((n + halo::kRunWin - 1) / halo::kRunWin), dim3(64), 0, s, p);
+    // Window per wave: as many waves as fit the chip at once (HALO_XXH3_WAVES_TARGET: 5 per SIMD at
+    // the kernel's 95 VGPRs x 1024 SIMDs), at most kRunWin strings each: 1M strings -> 208-string
+    // windows, 5042 waves, every one resident from the start (256-string windows: 4096 waves, 4 per
+    // SIMD; 128: 8192, a second round)
+#ifndef HALO_XXH3_WAVES_TARGET
+#define HALO_XXH3_WAVES_TARGET 5120
+#endif
+    uint32_t win = halo::kRunWin;
+    if (HALO_XXH3_WAVES_TARGET) {
+        win = (uint32_t)(((uint64_t)n + HALO_XXH3_WAVES_TARGET - 1) / HALO_XXH3_WAVES_TARGET);
+        win = (win + 15u) & ~15u;
+        win = win < 64u ? 64u : win > halo::kRunWin ? halo::kRunWin : win;
+    }
+    p.win = win;
+    hipLaunchKernelGGL(halo::xxh3_run_kernel, dim3((n + win - 1) / win), dim3(64), 0, s, p);
 #else
     constexpr uint32_t wpb = HALO_XXH3_LONG_BLOCK / 64;
     const uint32_t long_blocks = (uint32_t)(((uint64_t)halo::blocks_for(n) * 4 + wpb - 1) / wpb);

@@ -24,7 +24,8 @@ struct RxParams {
     uint32_t mac_hi;  // own MAC bytes 4..5
     uint32_t own_ip;  // IpAddrToU(NetIf.IpAddr)
     halo_rx_result_t* out;
-    uint32_t* hist;
+    uint32_t* hist;      // the launch's partial histograms (hist_slots), or null
+    uint32_t* hist_out;  // the caller's counters the last block of the launch adds into
     // fused NAT flow-key hash of every record (halo_rx_parse_flow_batch_device), or null
     uint64_t* flow_hash;
     uint32_t* flow_bucket;
@@ -57,11 +58,13 @@ enum SynthSlot : uint32_t {
 
 int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 
-// Partial status histograms of an rx launch (flush_hist, rx_parse.hip): kHistSlots slots of
-// kHistStride u32, one per block modulo kHistSlots, zero between launches. One array per (device,
-// stream) the library has parsed on with a histogram, allocated at first use and kept: launches on
-// one stream run in order, so they can share it.
-constexpr uint32_t kHistSlots = 1024, kHistStride = 16;
+// Partial status histograms of an rx launch (flush_hist, rx_parse.hip): kHistSlots level-1 slots
+// (one per block modulo kHistSlots) then kHistSlots / kHistFan level-2 slots, kHistStride u32 each
+// (the statuses, then an arrival counter in the last word), zero between launches. One array per
+// (device, stream) the library has parsed on with a histogram, allocated at first use and kept:
+// launches on one stream run in order, so they can share it.
+constexpr uint32_t kHistSlots = 1024, kHistFan = 32, kHistStride = 16;
+constexpr uint32_t kHistWords = (kHistSlots + kHistSlots / kHistFan) * kHistStride;
 uint32_t* hist_slots(hipStream_t s);  // nullptr: allocation failed
 
 // The resident small-poll consumer of a ring attached with HALO_RING_PERSISTENT (ring_rx.hip

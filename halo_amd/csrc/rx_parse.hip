@@ -486,11 +486,38 @@ __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, boo
     frame_finish<G, FUSE, U, R0, kL3<LAYOUT>>(p, i, present, gl, grp_base, st, hist);
 }
 
-// The block's counts go to one of kHistSlots partial histograms (p.hist is the launch's slot array,
-// hist_slots): device-scope atomics on one address serialise at the memory side, ~10 ns each, and
-// 16384 one-wave blocks adding to the caller's 14 counters cost 170 us on a 21 us launch (bench
-// r4b: config2_status_histogram). Spread over 1024 slots they run in parallel; hist_finalize folds
-// the slots into the caller's counters after the launch.
+// The block's counts reach the caller's counters through a two-level tree of partial histograms
+// (p.hist, hist_slots) instead of device-scope atomics on the caller's 14 counters: those serialise
+// at the memory side, ~10 ns each, and 16384 one-wave blocks cost 170 us on a 21 us launch (bench
+// r4b). Level 1: block b adds into slot b % 1024 (16 blocks per slot for 1M frames). The last block
+// to arrive at a level-1 slot (an arrival counter in the slot's last word, threadfence-reduction
+// order: adds, fence, barrier, count) moves the slot into level-2 slot (b % 1024) / 32; the last to
+// arrive there moves it into the caller's counters: at most 32 x 14 atomics on them per launch, no
+// finalize launch (a separate 1-block launch cost ~10 us per step, r4e). Every slot is left zero
+// and every counter reset for the next launch on the stream. Every block of a kernel that counts
+// calls this exactly once, with the whole block.
+__device__ __forceinline__ bool hist_arrive(uint32_t* slot, uint32_t arrivals) {
+    __shared__ uint32_t s_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t old = atomicAdd(&slot[kHistStride - 1], 1u);
+        if (old == arrivals - 1u) __hip_atomic_store(&slot[kHistStride - 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == arrivals - 1u;
+    }
+    __syncthreads();
+    const bool last = s_last != 0;
+    if (last) __threadfence();
+    return last;
+}
+
+__device__ __forceinline__ void hist_move(uint32_t* from, uint32_t* to) {
+    if (threadIdx.x < HALO_RX_STATUS_COUNT) {
+        const uint32_t x = atomicExch(&from[threadIdx.x], 0u);
+        if (x) atomicAdd(&to[threadIdx.x], x);
+    }
+}
+
 __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     if (!p.hist) return;
     uint32_t ok = hist.ok;
@@ -498,29 +525,15 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     for (int m = 1; m < 64; m <<= 1) ok += __shfl_xor(ok, m, 64);
     if ((threadIdx.x & 63u) == 0 && ok) atomicAdd(&hist.s[HALO_RX_OK], ok);
     __syncthreads();
-    uint32_t* slot = p.hist + (blockIdx.x & (kHistSlots - 1u)) * kHistStride;
-    if (threadIdx.x < HALO_RX_STATUS_COUNT && hist.s[threadIdx.x]) atomicAdd(&slot[threadIdx.x], hist.s[threadIdx.x]);
-}
-
-// Sums the slots of hist_slots into the caller's counters and zeroes them for the next launch on the
-// stream: one block, thread t owns slot t.
-__global__ void __launch_bounds__(kHistSlots) hist_finalize(uint32_t* slots, uint32_t* out) {
-    __shared__ uint32_t s_tot[HALO_RX_STATUS_COUNT];
-    const uint32_t t = threadIdx.x;
-    if (t < HALO_RX_STATUS_COUNT) s_tot[t] = 0;
-    __syncthreads();
-    uint32_t* slot = slots + t * kHistStride;
-#pragma unroll
-    for (uint32_t k = 0; k < HALO_RX_STATUS_COUNT; ++k) {
-        uint32_t v = slot[k];
-#pragma unroll
-        for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
-        if ((t & 63u) == 0 && v) atomicAdd(&s_tot[k], v);
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kHistStride; ++k) slot[k] = 0;
-    __syncthreads();
-    if (t < HALO_RX_STATUS_COUNT && s_tot[t]) atomicAdd(&out[t], s_tot[t]);
+    const uint32_t s = blockIdx.x & (kHistSlots - 1u), g = gridDim.x;
+    uint32_t* l1 = p.hist + s * kHistStride;
+    if (threadIdx.x < HALO_RX_STATUS_COUNT && hist.s[threadIdx.x]) atomicAdd(&l1[threadIdx.x], hist.s[threadIdx.x]);
+    if (!hist_arrive(l1, g / kHistSlots + (g % kHistSlots > s))) return;
+    uint32_t* l2 = p.hist + (kHistSlots + s / kHistFan) * kHistStride;
+    hist_move(l1, l2);
+    const uint32_t used = g < kHistSlots ? g : kHistSlots, first = s & ~(kHistFan - 1u);
+    if (!hist_arrive(l2, used - first < kHistFan ? used - first : kHistFan)) return;
+    hist_move(l2, p.hist_out);
 }
 
 // Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
@@ -1410,6 +1423,7 @@ int launch_parse(const RxParams& p_in, int layout, uint32_t max_len, bool unifor
     // sums a sparse one frame by frame); strided frames of one length are dense when the stride
     // wastes < 1/4; strided frames with their own lengths may be anything below the stride
     RxParams p = p_in;
+    p.hist_out = p.hist;
     if (p.hist && !(p.hist = hist_slots(s))) return HALO_E_NOMEM;  // the kernel counts into the slots
     const bool dense = layout == 0 || layout == 3 || (layout == 2 && p.stride <= max_len + max_len / 4 + 64);
     const int v = pick_variant(max_len, uniform, dense, p.flags);
@@ -1422,10 +1436,6 @@ int launch_parse(const RxParams& p_in, int layout, uint32_t max_len, bool unifor
         case 1: e = launch_variant<1>(p, v, s); break;
         case 3: e = launch_variant<3>(p, v, s); break;  // LoChan packets: plain parse only
         default: e = launch_variant<2>(p, v, s); break;
-    }
-    if (e == hipSuccess && p.hist) {
-        hipLaunchKernelGGL(hist_finalize, dim3(1), dim3(kHistSlots), 0, s, p.hist, p_in.hist);
-        e = hipGetLastError();
     }
     return e == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
@@ -1459,7 +1469,7 @@ uint32_t* hist_slots(hipStream_t s) {
     std::lock_guard<std::mutex> g(mu);
     auto& p = slots[{dev, s}];
     if (!p) {
-        const size_t bytes = sizeof(uint32_t) * kHistSlots * kHistStride;
+        const size_t bytes = sizeof(uint32_t) * kHistWords;
         if (hipMalloc((void**)&p, bytes) != hipSuccess || hipMemsetAsync(p, 0, bytes, s) != hipSuccess) {
             (void)hipGetLastError();
             if (p) (void)hipFree(p);
@@ -1605,6 +1615,7 @@ extern "C" HALO_API int halo_rx_parse_batches_device(const halo_rx_batch_desc_t*
     mp.k = k;
     mp.p.n = 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    mp.p.hist_out = d_status_hist;
     if (d_status_hist && !(mp.p.hist = halo::hist_slots(s))) return HALO_E_NOMEM;
     constexpr uint32_t wpb = HALO_RX_LANE_BLOCK / 64;
     const dim3 grid(halo::grid_for(windows * 64u, 64, HALO_RX_LANE_MAX_BLOCKS * 4 / wpb, wpb));
@@ -1612,7 +1623,6 @@ extern "C" HALO_API int halo_rx_parse_batches_device(const halo_rx_batch_desc_t*
         hipLaunchKernelGGL(halo::rx_lane_multi_kernel<3>, grid, dim3(HALO_RX_LANE_BLOCK), HALO_RX_LANE_LDS_PAD, s, mp);
     else
         hipLaunchKernelGGL(halo::rx_lane_multi_kernel<0>, grid, dim3(HALO_RX_LANE_BLOCK), HALO_RX_LANE_LDS_PAD, s, mp);
-    if (d_status_hist) hipLaunchKernelGGL(halo::hist_finalize, dim3(1), dim3(halo::kHistSlots), 0, s, mp.p.hist, d_status_hist);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 

@@ -379,7 +379,155 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
     }
 }
 
-// The tile-flat build of long frames (HALO_TXB_FLAT, the default for the 16- and 32-lane launches):
+// build_big split in two for software pipelining across the steps of a tile (HALO_TXB_PIPE, the
+// default): a wave of 16- or 32-lane groups builds 64 / G frames per step, and every step was one
+// dependent round trip (load the frames' bytes, wait, merge, store), so a wave had at most one
+// step's bytes in flight — 3 KB for 1514 B frames — and 4 waves per SIMD kept ~12 MB in flight on
+// the chip, short of what 8 TB/s needs at loaded HBM latency (r4e: 0.74 of the size-matched
+// probe, 65 % of wave cycles waiting). big_load issues step k + 1's loads (the first round of
+// body chunks and the lane's head / tail chunk) before big_finish waits for step k's.
+#ifndef HALO_TXB_UNALIGNED
+#define HALO_TXB_UNALIGNED 1
+#endif
+template <int U>
+struct BigLoad {
+    uint32_t raw[U][HALO_TXB_UNALIGNED ? 4 : 5];
+    uint32_t head[5];
+};
+
+template <int G, int U>
+__device__ __forceinline__ void big_load(const Frame& f, uint32_t j, BigLoad<U>& b) {
+    const uint32_t pay_end = f.hdr_end + f.plen, ndw = (f.flen + 3u) >> 2;
+    const uint64_t P = f.pay - f.hdr_end;
+    const uint32_t sh = (uint32_t)(P & 3u), cb_end = pay_end >> 4;
+    typedef const __attribute__((address_space(1), unused)) uint32_t gu32_t;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4), unused));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t c = 4 + j + u * G;
+        if (c < cb_end) {
+#if HALO_TXB_UNALIGNED
+            // the chunk's 16 source bytes in one unaligned load (gfx9 global loads take any byte
+            // address; all 16 are payload bytes): no fifth dword, no v_alignbyte
+            typedef uint32_t u32x4b __attribute__((ext_vector_type(4), aligned(1)));
+            const u32x4b v = *(const __attribute__((address_space(1))) u32x4b*)(P + 16ull * c);
+            b.raw[u][0] = v.x; b.raw[u][1] = v.y; b.raw[u][2] = v.z; b.raw[u][3] = v.w;
+            (void)sh;
+#else
+            gu32_t* q = (gu32_t*)((P + 16ull * c) & ~3ull);
+            const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)q;
+            b.raw[u][0] = v.x; b.raw[u][1] = v.y; b.raw[u][2] = v.z; b.raw[u][3] = v.w;
+            b.raw[u][4] = sh ? q[4] : 0u;
+#endif
+        }
+    }
+    const uint32_t c = j < 4 ? j : cb_end;
+    const bool mine = j < 4 ? 4 * j < ndw : (j == 4 && cb_end >= 4 && 4 * cb_end < ndw);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) b.head[i] = 0u;
+    if (mine && chunk_has_payload(f, c, ndw)) payload_raw(f, c, b.head);
+}
+
+template <int G, int U>
+__device__ __forceinline__ void big_finish(const BuildParams& p, const Frame& f, const uint32_t* hdr, uint32_t j,
+                                           uint8_t* out, const BigLoad<U>& b) {
+    const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
+    const uint32_t l4s = f.base + 20u, pay_end = f.hdr_end + f.plen;
+    const uint32_t ndw = (f.flen + 3u) >> 2;
+    const uint64_t P = f.pay - f.hdr_end;
+    const uint32_t sh = (uint32_t)(P & 3u);
+    const uint32_t cb_end = pay_end >> 4;
+    typedef const __attribute__((address_space(1), unused)) uint32_t gu32_t;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4), unused));
+    uint32_t sum = 0;
+    auto body = [&](uint32_t c, const uint32_t (&r)[HALO_TXB_UNALIGNED ? 4 : 5]) {
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            w[i] = HALO_TXB_UNALIGNED ? r[i] : __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+            sum = hsum_acc(w[i], sum);
+        }
+        *reinterpret_cast<uint4*>(out + 16ull * c) = make_uint4(w[0], w[1], w[2], w[3]);
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t c = 4 + j + u * G;
+        if (c < cb_end) body(c, b.raw[u]);
+    }
+    for (uint32_t c0 = 4 + j + U * G; c0 < cb_end; c0 += U * G) {  // frames longer than one round
+        uint32_t raw[U][HALO_TXB_UNALIGNED ? 4 : 5];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            if (c < cb_end) {
+#if HALO_TXB_UNALIGNED
+                typedef uint32_t u32x4b __attribute__((ext_vector_type(4), aligned(1)));
+                const u32x4b v = *(const __attribute__((address_space(1))) u32x4b*)(P + 16ull * c);
+                raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
+#else
+                gu32_t* q = (gu32_t*)((P + 16ull * c) & ~3ull);
+                const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)q;
+                raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
+                raw[u][4] = sh ? q[4] : 0u;
+#endif
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (c0 + u * G < cb_end) body(c0 + u * G, raw[u]);
+    }
+    const uint32_t c = j < 4 ? j : cb_end;
+    const bool mine = j < 4 ? 4 * j < ndw : (j == 4 && cb_end >= 4 && 4 * cb_end < ndw);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (mine) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t k = 4 * c + i;
+            w[i] = __builtin_amdgcn_alignbyte(b.head[i + 1], b.head[i], sh) & byte_mask(k, f.hdr_end, pay_end);
+            if (k < 16) w[i] |= hdr[k] & byte_mask(k, 0, f.hdr_end);
+            sum = hsum_acc(w[i] & byte_mask(k, l4s, pay_end), sum);
+        }
+        if (j == 4) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(out) + 4 * c;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (4 * c + i < ndw) o[i] = w[i];
+        }
+    }
+    uint32_t part = group_sum<G>(fold16(sum));
+    uint32_t ck_le = 0;
+    uint32_t ck_at;
+    if (f.proto == kIpUdp || f.proto == kIpTcp) {
+        const uint32_t s = bswap32(f.src), t = bswap32(f.dst);
+        part += hsum(s) + hsum(t) + (f.proto << 8) + bswap16(f.l4hdr + f.plen);
+        ck_at = f.base + 20u + (f.proto == kIpUdp ? 6u : 16u);
+    } else {
+        ck_at = f.base + 22u;
+    }
+    if (csum || f.proto == kIpIcmp) ck_le = (~fold16(part)) & 0xFFFFu;  // ICMP always (icmp.go:84-87)
+    if (mine && j < 4) {
+        const uint32_t ck_dw = ck_at >> 2, ck_sh = (ck_at & 2u) * 8u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (4 * c + i == ck_dw) w[i] |= ck_le << ck_sh;
+        uint32_t* o = reinterpret_cast<uint32_t*>(out) + 4 * c;
+        if (4 * c + 4 <= ndw) {
+            *reinterpret_cast<uint4*>(o) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (4 * c + i < ndw) o[i] = w[i];
+        }
+    }
+}
+#ifndef HALO_TXB_PIPE
+#define HALO_TXB_PIPE 0  // measured slower (profiles/r04/r4g/ab_tx_pipe.log)
+#endif
+#ifndef HALO_TXB_PIPE_WAVES  // occupancy floor of the pipelined build (two load buffers)
+#define HALO_TXB_PIPE_WAVES 3
+#endif
+
+// The tile-flat build of long frames (HALO_TXB_FLAT=1, an alternative for the 16- and 32-lane launches):
 // build_big still walks a tile's 64 frames G lanes at a time, 64 / G frames per step, and every
 // step pays a descriptor decode, the zone bounds, a G-lane reduction and the masked head for two
 // frames. Here every per-frame piece is done once, by the lane that owns the frame, and the payload
@@ -626,23 +774,35 @@ __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t s
 #ifndef HALO_TXB_G1_WAVES
 #define HALO_TXB_G1_WAVES 4
 #endif
+// Waves per tile of the 16- and 32-lane builds (HALO_TXB_SPLIT): a 1514 B tile is 97 KB of
+// payload that one wave builds in G dependent steps, and 256k frames make only 4096 tiles — four
+// waves per SIMD. With S waves per tile, wave `part` of tile t builds the steps congruent to part
+// mod S (every wave still decides all 64 descriptors: the ranks need the whole tile's ballot), so
+// the grid has S x as many waves, each with 1 / S of the LDS staging.
+#ifndef HALO_TXB_SPLIT
+#define HALO_TXB_SPLIT 2
+#endif
+template <int G>
+constexpr uint32_t kSplit = (G >= 16 && !HALO_TXB_FLAT && !HALO_TXB_PIPE) ? HALO_TXB_SPLIT : 1;
+
 template <int G, int U>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G == 1 ? HALO_TXB_G1_WAVES : 4)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G == 1 ? HALO_TXB_G1_WAVES : (G >= 16 && HALO_TXB_PIPE) ? HALO_TXB_PIPE_WAVES : 4 * kSplit<G>)))
 tx_build_kernel(const BuildParams p) {
 #ifndef HALO_TXB_G1_LDS_TRIM
 #define HALO_TXB_G1_LDS_TRIM 1
 #endif
     // the descriptor staging is only for G > 1 (a lane per frame keeps its own): 11 KB less LDS
     // per block, so the lane-per-frame build fits eight blocks per CU
-    constexpr uint32_t kDescDw = (G > 1 || !HALO_TXB_G1_LDS_TRIM) ? kTile * 10 + 1 : 1;
-    constexpr uint32_t kMetaDw = (G > 1 || !HALO_TXB_G1_LDS_TRIM) ? kTile : 1;
+    constexpr uint32_t S = kSplit<G>, kOwn = kTile / S;  // waves per tile; frames each stages
+    constexpr uint32_t kDescDw = (G > 1 || !HALO_TXB_G1_LDS_TRIM) ? kOwn * 10 + 1 : 1;
+    constexpr uint32_t kMetaDw = (G > 1 || !HALO_TXB_G1_LDS_TRIM) ? kOwn : 1;
     __shared__ uint32_t s_desc[kBlock / 64][kDescDw];  // per wave: its tile's descriptors
     __shared__ uint32_t s_meta[kBlock / 64][kMetaDw];
     // per wave: frame-layout header dwords 0..15 (G > 1); G = 1: a lane's header for a long frame,
     // or its whole <= 64-byte frame staged for the wave's cooperative store (17-dword rows: the
     // row-wise writes and the chunk-wise reads both spread over the banks)
     constexpr uint32_t kRow = G == 1 ? 17 : 16;
-    __shared__ uint32_t s_hdr[kBlock / 64][kTile * kRow + 1];
+    __shared__ uint32_t s_hdr[kBlock / 64][kOwn * kRow + 1];
     __shared__ uint32_t s_ndw[kBlock / 64][G == 1 ? kTile : 1];  // G = 1: staged frame's dwords (0: none)
     constexpr bool kFlat = G >= 16 && HALO_TXB_FLAT;
     __shared__ FlatLds s_flat[kFlat ? kBlock / 64 : 1];
@@ -670,7 +830,8 @@ tx_build_kernel(const BuildParams p) {
     constexpr bool kPf = G == 1 && HALO_TXB_DESC_PREFETCH;
     uint32_t dn[10];
     if constexpr (kPf) load_desc(((blockIdx.x * kBlock + threadIdx.x) >> 6) * kTile + lane, dn);
-    for (uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 6; t < p.n_tiles; t += nw) {
+    for (uint32_t tw = (blockIdx.x * kBlock + threadIdx.x) >> 6; tw < p.n_tiles * S; tw += nw) {
+        const uint32_t t = tw / S, part = tw % S;
         const uint32_t first = t * kTile, i = first + lane;
         uint32_t d[10];
         if constexpr (kPf) {
@@ -684,7 +845,7 @@ tx_build_kernel(const BuildParams p) {
         const uint32_t code = i < p.n ? verdict(d[2], d[9], p.stride, flen) : HALO_TX_B_PROTO;
         const bool rej = i < p.n && code != HALO_TX_B_OK;
         const uint64_t bal = __ballot(rej);
-        if (lane == 0) p.ws[1 + t] = (uint32_t)__popcll(bal);  // rejections in this tile
+        if (lane == 0 && part == 0) p.ws[1 + t] = (uint32_t)__popcll(bal);  // rejections in this tile
         const uint32_t before =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
         // iphId++ then use (ipv4.go:103-104); rejections in earlier tiles settled by launches 2/3
@@ -748,33 +909,74 @@ tx_build_kernel(const BuildParams p) {
             flat_tile<HALO_TXB_FLAT_U>(p, decode(d, p.payload), (mine >> 31) != 0, hv, first, lane, s_hdr[wv],
                                        s_flat[wv]);
         } else {
+            // this wave's frames (steps congruent to `part` mod S) at compact LDS slots
+            constexpr uint32_t F = 64u / G;  // frames per step
+            const uint32_t my_step = lane / F;
+            const uint32_t slot = (my_step / S) * F + lane % F;
+            if (my_step % S == part) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) s_hdr[wv][kRow * lane + k] = hv[k];
-            // the wave's descriptors through its own LDS region (no block barrier), so that they
-            // are not live in registers across the build steps
+                for (int k = 0; k < 16; ++k) s_hdr[wv][kRow * slot + k] = hv[k];
+                // the wave's descriptors through its own LDS region (no block barrier), so that they
+                // are not live in registers across the build steps
 #pragma unroll
-            for (int k = 0; k < 10; ++k) s_desc[wv][10 * lane + k] = d[k];
-            s_meta[wv][lane] = mine;
+                for (int k = 0; k < 10; ++k) s_desc[wv][10 * slot + k] = d[k];
+                s_meta[wv][slot] = mine;
+            }
             __builtin_amdgcn_wave_barrier();
-#pragma unroll 1
-            for (uint32_t step = 0; step < (uint32_t)G; ++step) {
-                const uint32_t fl = step * (64u / G) + g;  // this group's frame, as a lane of the tile
-                const uint32_t meta = s_meta[wv][fl];
-                if (meta >> 31) {  // uniform over the group
+            if constexpr (G >= 16 && HALO_TXB_BIG_PATH && HALO_TXB_PIPE && S == 1) {
+                // step k + 1's loads go out before step k's build waits for its own
+                auto frame_at = [&](uint32_t fl) {
                     uint32_t dd[10];
 #pragma unroll
                     for (int k = 0; k < 10; ++k) dd[k] = s_desc[wv][10 * fl + k];
+                    return decode(dd, p.payload);
+                };
+                // two buffers used alternately (the loop is unrolled by two): copying the next
+                // step's buffer into the current one would wait for its loads
+                BigLoad<U> ba, bb;
+                constexpr uint32_t F = 64u / G;
+                auto finish = [&](uint32_t fl, const BigLoad<U>& b) {
+                    big_finish<G, U>(p, frame_at(fl), &s_hdr[wv][kRow * fl], j,
+                                     p.frames + (uint64_t)(first + fl) * p.stride, b);
+                };
+                uint32_t m0 = s_meta[wv][g];
+                if (m0 >> 31) big_load<G, U>(frame_at(g), j, ba);
+#pragma unroll 1
+                for (uint32_t step = 0; step < (uint32_t)G; step += 2) {
+                    const uint32_t f0 = step * F + g, f1 = f0 + F, f2 = f1 + F;
+                    const uint32_t m1 = s_meta[wv][f1];
+                    // (the empty asm keeps the compiler from holding a decoded frame in registers
+                    // across the other frame's build: it re-reads the descriptor from LDS)
+                    if (m1 >> 31) big_load<G, U>(frame_at(f1), j, bb);
+                    asm volatile("" ::: "memory");
+                    if (m0 >> 31) finish(f0, ba);
+                    const uint32_t m2 = step + 2 < (uint32_t)G ? s_meta[wv][f2] : 0u;
+                    if (m2 >> 31) big_load<G, U>(frame_at(f2), j, ba);
+                    asm volatile("" ::: "memory");
+                    if (m1 >> 31) finish(f1, bb);
+                    m0 = m2;
+                }
+            } else
+#pragma unroll 1
+            for (uint32_t step = 0; step < (uint32_t)G / S; ++step) {
+                const uint32_t sl = step * F + g;                // this group's frame's LDS slot
+                const uint32_t fl = (step * S + part) * F + g;  // ... and its lane in the tile
+                const uint32_t meta = s_meta[wv][sl];
+                if (meta >> 31) {  // uniform over the group
+                    uint32_t dd[10];
+#pragma unroll
+                    for (int k = 0; k < 10; ++k) dd[k] = s_desc[wv][10 * sl + k];
                     if constexpr (G >= 16 && HALO_TXB_BIG_PATH)
-                        build_big<G, U>(p, decode(dd, p.payload), &s_hdr[wv][kRow * fl], j,
+                        build_big<G, U>(p, decode(dd, p.payload), &s_hdr[wv][kRow * sl], j,
                                         p.frames + (uint64_t)(first + fl) * p.stride);
                     else
-                        build_frame<G, U>(p, decode(dd, p.payload), &s_hdr[wv][kRow * fl], j,
+                        build_frame<G, U>(p, decode(dd, p.payload), &s_hdr[wv][kRow * sl], j,
                                           p.frames + (uint64_t)(first + fl) * p.stride);
                 }
             }
             __builtin_amdgcn_wave_barrier();  // the region is rewritten for the next tile
         }
-        if (i < p.n) {  // after the build: these stores do not hold up the payload loads
+        if (part == 0 && i < p.n) {  // after the build: these stores do not hold up the payload loads
             p.lens[i] = code == HALO_TX_B_OK ? (uint16_t)flen : (uint16_t)0;
             if (p.result) p.result[i] = (uint8_t)code;
         }
@@ -895,12 +1097,13 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
 #ifndef HALO_TXB_MAX_BLOCKS
 #define HALO_TXB_MAX_BLOCKS (HALO_TXB_G1_WAVES * 256u)  // waves x 1024 SIMDs / 4 per block: one resident round
 #endif
-    const uint32_t waves = p.n_tiles, blocks = (waves + 3) / 4;
-    const dim3 grid(blocks < HALO_TXB_MAX_BLOCKS ? blocks : HALO_TXB_MAX_BLOCKS), blk(halo::kBlock);
     // lanes per frame and chunks per lane from the largest frame expected (a frame needs
     // ceil(flen / 16) chunks; longer ones than G * U chunks take extra rounds)
     const uint32_t h = max_payload_hint ? max_payload_hint : 1472u;
     const uint32_t chunks = (h + 42u + 15u) / 16u;  // UDP / ICMP headers; TCP frames 12 B longer
+    const uint32_t split = chunks > 32 ? halo::kSplit<16> : 1u;  // waves per tile (G >= 16)
+    const uint32_t waves = p.n_tiles * split, blocks = (waves + 3) / 4, cap = HALO_TXB_MAX_BLOCKS * split;
+    const dim3 grid(blocks < cap ? blocks : cap), blk(halo::kBlock);
     if (chunks <= 4) hipLaunchKernelGGL((halo::tx_build_kernel<1, 4>), grid, blk, 0, s, p);
     else if (chunks <= 16) hipLaunchKernelGGL((halo::tx_build_kernel<4, 4>), grid, blk, 0, s, p);
     else if (chunks <= 32) hipLaunchKernelGGL((halo::tx_build_kernel<8, 4>), grid, blk, 0, s, p);

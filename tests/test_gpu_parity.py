@@ -339,6 +339,34 @@ def test_config4_shard_16M_64B_whole_batch(dev, oracle_lib):
     assert_records_equal(recs, want, None, "config4 shard 7 of 8 (16M x 64 B)")
 
 
+@pytest.mark.parametrize("variant", [1, 4, 16, -1, -2])
+def test_histogram_tree_across_grid_sizes_and_launches(dev, variant):
+    """The status histogram's two-level tree (flush_hist: 1024 level-1 slots, 32 level-2 slots, the
+    last block to arrive moves a slot up): grids below, at and above 1024 and 32 x 1024 blocks,
+    three launches in a row into one histogram on one stream (the slots and arrival counters must
+    be left zero by every launch), and a histogram-less launch in between. Histogram == 3 x the
+    records' statuses."""
+    import torch
+
+    from halo_amd import protocol, synth
+    from halo_amd._lib import NetIf
+
+    for n, length in [(7, 64), (64 * 1024 + 1, 64), (40000, 200), (1 << 21, 64)]:
+        lay = synth.layout(n, length=length, mutate_shift=3)
+        fr = synth.frames_device(lay, NetIf.make(), device=dev)
+        hist = torch.zeros(14, dtype=torch.int32, device=dev)
+        for rep in range(3):
+            out = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                              max_len_hint=length, hist=hist, variant=variant)
+            if rep == 1:
+                protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                            max_len_hint=length, variant=variant)
+        torch.cuda.synchronize()
+        want = 3 * np.bincount(protocol.records(out)["status"], minlength=14)
+        assert np.array_equal(hist.cpu().numpy().astype(np.int64), want), (n, length, variant)
+        assert want[1:].sum() > 0 or n < 64
+
+
 def test_config5_full_size_4M_9000B(dev, oracle_lib):
     """BASELINE config 5 at full size: 4M x 9000 B TCP, strided, 37.7 GB in one call (frame
     addresses past 2^32 and 2^35). Reference verdict (caps kept): ETH_LEN for every frame. Jumbo

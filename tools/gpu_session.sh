@@ -86,6 +86,9 @@ for s in "$@"; do
     tmulti) step pytest_multi 600 python -u -m pytest tests/test_gpu_multi_batch.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     tnew)  step pytest_new 900 python -u -m pytest tests/test_gpu_host_resident.py tests/test_gpu_multi_batch.py tests/test_gpu_ring.py tests/test_gpu_single_frame.py tests/test_gpu_engine_cadence.py tests/test_gpu_route.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     ttxb)  step pytest_txb 600 python -u -m pytest tests/test_gpu_tx_build.py tests/test_gpu_loopback.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    thist) step pytest_hist 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_multi_batch.py -k "histogram or hist or multi" -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    abxb)  step ab_xxh3_bf 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_xxh3.py" ${AB_XB:-xxbf0 new} ;;
+    abtp)  step ab_tx_pipe 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_tx_build.py" ${AB_TP:-txpipe0 new} ;;
     txx)   step pytest_xxh3 600 python -u -m pytest tests/test_gpu_flow_hash.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     prof4) PK_ARGS="config2 config2_batch_stream lo_drain_1M_50B flow_hash_config2 flow_hash_config2_compact tx_build_udp_256k_1514B"
            step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 tools/prof_kernels.py $PK_ARGS
