@@ -588,6 +588,25 @@ static_assert(kRunB == 4 || kRunB == 8, "a batch must not straddle a 16-stripe b
 #ifndef HALO_XXH3_BF
 #define HALO_XXH3_BF 1
 #endif
+#ifndef HALO_XXH3_MERGED  // one finishing sequence for long merges and 17..240 B strings
+#define HALO_XXH3_MERGED 0   // measured slower: 0.189 / 0.189 ms against 0.188 / 0.186 (profiles/r04/r4i)
+#endif
+// Dword-aligned loads (HALO_XXH3_ALIGNED): the 16 bytes at any address as an aligned 16-byte load
+// plus one dword, merged with v_alignbyte, instead of one byte-unaligned 16-byte load
+#ifndef HALO_XXH3_ALIGNED
+#define HALO_XXH3_ALIGNED 0  // measured slower: 0.214 / 0.214 ms against 0.185 / 0.185 (profiles/r04/r4j)
+#endif
+__device__ __forceinline__ void ld128a(const uint8_t* p, uint64_t& lo, uint64_t& hi) {
+    typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = (uint32_t)(a & 3u);
+    const uintptr_t q = a & ~(uintptr_t)3;
+    const u32x4a v = *(const __attribute__((address_space(1))) u32x4a*)q;
+    // the fifth dword holds bytes 16 - sh .. 15 of the span when sh != 0; else any dword inside it
+    const uint32_t w4 = *(const __attribute__((address_space(1))) uint32_t*)(q + (sh ? 16 : 12));
+    lo = join64(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh));
+    hi = join64(__builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(w4, v.w, sh));
+}
 #if HALO_XXH3_BF
 __device__ const uint8_t g_xxh3_pad[64] = {};
 #endif
@@ -673,8 +692,10 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
                 v = u < 2 || t <= nmid;
                 a = u < 2 ? d + 16 * t : t < nmid ? d + 128 + 16 * t : d + len - 16;
             }
-#if HALO_XXH3_BF
-            ld128u(v ? a : g_xxh3_pad, lo[u], hi[u]);  // no branch: idle slots read 16 zero bytes
+#if HALO_XXH3_BF && HALO_XXH3_ALIGNED
+            ld128a(v ? a : g_xxh3_pad, lo[u], hi[u]);  // no branch: idle slots read 16 zero bytes
+#elif HALO_XXH3_BF
+            ld128u(v ? a : g_xxh3_pad, lo[u], hi[u]);
 #else
             lo[u] = hi[u] = 0;
             if (v) ld128u(a, lo[u], hi[u]);
@@ -682,6 +703,57 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
         }
         uint64_t h = 0;
         bool have = false;
+#if HALO_XXH3_MERGED
+        bool fin = false;
+        if (lng) {
+#pragma unroll
+            for (uint32_t u = 0; u < kRunB; ++u) {
+                const uint32_t x = st + u;
+                const uint64_t s0 = x < T ? sec.w8[(x & 15u) + 2 * j] : sec.last[2 * j];
+                const uint64_t s1 = x < T ? sec.w8[(x & 15u) + 2 * j + 1] : sec.last[2 * j + 1];
+                const uint64_t k0 = lo[u] ^ s0, k1 = hi[u] ^ s1;
+                const uint64_t t0 = hi[u] + (uint64_t)(uint32_t)k0 * (k0 >> 32);
+                const uint64_t t1 = lo[u] + (uint64_t)(uint32_t)k1 * (k1 >> 32);
+                a0 += x <= T ? t0 : 0ull;
+                a1 += x <= T ? t1 : 0ull;
+            }
+            st += kRunB;
+            if ((st & 15u) == 0 && (st >> 4) <= nb) {  // a full block ended: scramble (xxh3.go:212-218)
+                a0 ^= a0 >> 47;
+                a1 ^= a1 >> 47;
+                a0 ^= sec.w8[16 + 2 * j];
+                a1 ^= sec.w8[17 + 2 * j];
+                a0 *= P32_1;
+                a1 *= P32_1;
+            }
+            fin = st > T;
+        }
+        // One finishing sequence for a long string's merge (xxh3.go:139-145: pair (2j, 2j+1) with
+        // secret 11 + 16j) and a 17..240 B string's first terms (hashMedium's pair j, hashLarge's
+        // terms 2j and 2j+1: the same secret words 32j .. 32j+24), run by the whole wave once
+        // instead of once per branch; then hashLarge's middle terms and one final avalanche.
+        const bool lend = lng && fin;
+        if (__builtin_amdgcn_ballot_w64(lend || mid)) {
+            const uint64_t A = lend ? a0 ^ sec.merge[2 * j] : lo[0] ^ sec.w8[4 * j];
+            const uint64_t Bq = lend ? a1 ^ sec.merge[2 * j + 1] : hi[0] ^ sec.w8[4 * j + 1];
+            uint64_t t = mul_fold64(A, Bq);
+            if (mid) t += mul_fold64(lo[1] ^ sec.w8[4 * j + 2], hi[1] ^ sec.w8[4 * j + 3]);
+            if (mid && !large && j >= lv) t = 0;
+            uint64_t x = (uint64_t)len * P64_1 + quad_sum(t);
+            if (mid && large) {  // hashLarge: avalanche, then terms 2j, 2j+1 of the middle + last
+                uint64_t t23 = 0;
+#pragma unroll
+                for (uint32_t u = 2; u < 4; ++u) {
+                    const uint32_t q = 2 * j + (u & 1u);
+                    if (q < nmid) t23 += mul_fold64(lo[u] ^ sec.mid3[2 * q], hi[u] ^ sec.mid3[2 * q + 1]);
+                    else if (q == nmid) t23 += mul_fold64(lo[u] ^ sec.mlast[0], hi[u] ^ sec.mlast[1]);
+                }
+                x = avalanche(x) + quad_sum(t23);
+            }
+            h = avalanche(x);
+            have = lend || mid;
+        }
+#else
         if (lng) {
 #pragma unroll
             for (uint32_t u = 0; u < kRunB; ++u) {
@@ -736,6 +808,7 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
             }
             have = true;
         }
+#endif
         if (sml) {  // hashSmall: every lane of the group computes it
             h = hash_upto16(d, len);
             have = true;
@@ -815,12 +888,12 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
                        dim3(256), 0, s, p);
 #endif
 #if HALO_XXH3_RUNS
-    // Window per wave: as many waves as fit the chip at once (HALO_XXH3_WAVES_TARGET: 5 per SIMD at
-    // the kernel's 95 VGPRs x 1024 SIMDs), at most kRunWin strings each: 1M strings -> 208-string
-    // windows, 5042 waves, every one resident from the start (256-string windows: 4096 waves, 4 per
-    // SIMD; 128: 8192, a second round)
+    // Window per wave: kRunWin strings, or (HALO_XXH3_WAVES_TARGET, a knob) as many waves as fit the
+    // chip at once, e.g. 5120 = 5 per SIMD at the kernel's 95 VGPRs: 1M strings -> 208-string
+    // windows, 5042 waves all resident. Measured slower: 0.199 / 0.200 ms against 0.186 / 0.186 for
+    // 256-string windows (4096 waves; profiles/r04/r4h/ab_xxh3_bf.log)
 #ifndef HALO_XXH3_WAVES_TARGET
-#define HALO_XXH3_WAVES_TARGET 5120
+#define HALO_XXH3_WAVES_TARGET 0
 #endif
     uint32_t win = halo::kRunWin;
     if (HALO_XXH3_WAVES_TARGET) {

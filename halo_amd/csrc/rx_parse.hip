@@ -489,35 +489,15 @@ __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, boo
 // The block's counts reach the caller's counters through a two-level tree of partial histograms
 // (p.hist, hist_slots) instead of device-scope atomics on the caller's 14 counters: those serialise
 // at the memory side, ~10 ns each, and 16384 one-wave blocks cost 170 us on a 21 us launch (bench
-// r4b). Level 1: block b adds into slot b % 1024 (16 blocks per slot for 1M frames). The last block
-// to arrive at a level-1 slot (an arrival counter in the slot's last word, threadfence-reduction
-// order: adds, fence, barrier, count) moves the slot into level-2 slot (b % 1024) / 32; the last to
-// arrive there moves it into the caller's counters: at most 32 x 14 atomics on them per launch, no
-// finalize launch (a separate 1-block launch cost ~10 us per step, r4e). Every slot is left zero
-// and every counter reset for the next launch on the stream. Every block of a kernel that counts
-// calls this exactly once, with the whole block.
-__device__ __forceinline__ bool hist_arrive(uint32_t* slot, uint32_t arrivals) {
-    __shared__ uint32_t s_last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t old = atomicAdd(&slot[kHistStride - 1], 1u);
-        if (old == arrivals - 1u) __hip_atomic_store(&slot[kHistStride - 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == arrivals - 1u;
-    }
-    __syncthreads();
-    const bool last = s_last != 0;
-    if (last) __threadfence();
-    return last;
-}
-
-__device__ __forceinline__ void hist_move(uint32_t* from, uint32_t* to) {
-    if (threadIdx.x < HALO_RX_STATUS_COUNT) {
-        const uint32_t x = atomicExch(&from[threadIdx.x], 0u);
-        if (x) atomicAdd(&to[threadIdx.x], x);
-    }
-}
-
+// r4b). Every word of the tree is a 64-bit (arrivals << 40 | count) pair, one per status: block b
+// adds (1 << 40 | its count) to status k of level-1 slot b % 1024 (16 blocks per slot for 1M
+// frames), and the add that brings the arrivals to the slot's block count returns the slot's final
+// count, so that thread alone moves it on — to level-2 slot (b % 1024) / 32, whose last arrival
+// adds it to the caller's counter (at most 32 x 14 atomics on them per launch) — and zeroes the word
+// for the next launch on the stream. Each word carries its own completion, so no fence is needed: a
+// __threadfence per block (agent-scope release / acquire, L2 writeback and invalidate across the
+// XCDs on gfx950) cost 0.55 ms per 1M-frame launch (bench r4i), and a separate finalize launch
+// ~10 us (r4e). Every block of a kernel that counts calls this once, with the whole block.
 __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     if (!p.hist) return;
     uint32_t ok = hist.ok;
@@ -525,15 +505,21 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     for (int m = 1; m < 64; m <<= 1) ok += __shfl_xor(ok, m, 64);
     if ((threadIdx.x & 63u) == 0 && ok) atomicAdd(&hist.s[HALO_RX_OK], ok);
     __syncthreads();
+    const uint32_t t = threadIdx.x;
+    if (t >= HALO_RX_STATUS_COUNT) return;
+    constexpr unsigned long long kOne = 1ull << 40, kCount = kOne - 1;
     const uint32_t s = blockIdx.x & (kHistSlots - 1u), g = gridDim.x;
-    uint32_t* l1 = p.hist + s * kHistStride;
-    if (threadIdx.x < HALO_RX_STATUS_COUNT && hist.s[threadIdx.x]) atomicAdd(&l1[threadIdx.x], hist.s[threadIdx.x]);
-    if (!hist_arrive(l1, g / kHistSlots + (g % kHistSlots > s))) return;
-    uint32_t* l2 = p.hist + (kHistSlots + s / kHistFan) * kHistStride;
-    hist_move(l1, l2);
+    unsigned long long* tree = reinterpret_cast<unsigned long long*>(p.hist);
+    unsigned long long* l1 = tree + s * kHistStride + t;
+    unsigned long long now = atomicAdd(l1, kOne | hist.s[t]) + (kOne | hist.s[t]);
+    if ((now >> 40) != g / kHistSlots + (g % kHistSlots > s)) return;
+    atomicExch(l1, 0ull);
     const uint32_t used = g < kHistSlots ? g : kHistSlots, first = s & ~(kHistFan - 1u);
-    if (!hist_arrive(l2, used - first < kHistFan ? used - first : kHistFan)) return;
-    hist_move(l2, p.hist_out);
+    unsigned long long* l2 = tree + (kHistSlots + s / kHistFan) * kHistStride + t;
+    now = atomicAdd(l2, kOne | (now & kCount)) + (kOne | (now & kCount));
+    if ((now >> 40) != (used - first < kHistFan ? used - first : kHistFan)) return;
+    atomicExch(l2, 0ull);
+    if (now & kCount) atomicAdd(&p.hist_out[t], (uint32_t)(now & kCount));
 }
 
 // Uniform batches: G lanes per frame for every frame (G in {1,4,8,16}); 64/G frames per wave.
@@ -1469,7 +1455,7 @@ uint32_t* hist_slots(hipStream_t s) {
     std::lock_guard<std::mutex> g(mu);
     auto& p = slots[{dev, s}];
     if (!p) {
-        const size_t bytes = sizeof(uint32_t) * kHistWords;
+        const size_t bytes = sizeof(uint64_t) * kHistWords;
         if (hipMalloc((void**)&p, bytes) != hipSuccess || hipMemsetAsync(p, 0, bytes, s) != hipSuccess) {
             (void)hipGetLastError();
             if (p) (void)hipFree(p);

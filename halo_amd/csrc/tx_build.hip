@@ -780,7 +780,7 @@ __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t s
 // mod S (every wave still decides all 64 descriptors: the ranks need the whole tile's ballot), so
 // the grid has S x as many waves, each with 1 / S of the LDS staging.
 #ifndef HALO_TXB_SPLIT
-#define HALO_TXB_SPLIT 2
+#define HALO_TXB_SPLIT 1  // 2 measured neutral: 0.2032 / 0.2021 ms against 0.2021 / 0.2044 (profiles/r04/r4h)
 #endif
 template <int G>
 constexpr uint32_t kSplit = (G >= 16 && !HALO_TXB_FLAT && !HALO_TXB_PIPE) ? HALO_TXB_SPLIT : 1;

@@ -310,6 +310,83 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_stream_rw(const
     return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
 }
 
+// The transmit build's own layout with no build work (the tx_build line's layout-matched probe):
+// waves own 64-frame tiles like tx_build_kernel (lane l loads descriptor l's 40 bytes), then 32
+// lanes per frame, two frames per step, three 16-byte chunks per lane: payload bytes [16c - 42,
+// +16) of the frame's payload (unaligned 16-byte loads from the same addresses the build reads),
+// the slot's dwords up to the frame's end stored at the same addresses, then length and result.
+// What the output format (1514 B frames in 1516 B slots, payloads 1472 B apart) costs before any
+// arithmetic; the size-matched probe streams the same byte counts aligned and contiguous.
+__global__ void __launch_bounds__(256) tx_layout_probe_kernel(const uint2* desc, const uint8_t* pay, uint32_t plen,
+                                                              uint8_t* frames, uint32_t stride, uint32_t flen,
+                                                              uint16_t* lens, uint8_t* res, uint32_t n,
+                                                              uint32_t* sink) {
+    typedef uint32_t u32x4b __attribute__((ext_vector_type(4), aligned(1)));
+    const uint32_t lane = threadIdx.x & 63u, j = lane & 31u, g = lane >> 5;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t chunks = (flen + 15u) / 16u, ndw = (flen + 3u) / 4u, tiles = (n + 63u) / 64u;
+    for (uint32_t t = wave; t < tiles; t += nw) {
+        uint32_t x = 0;
+        if (t * 64u + lane < n) {
+            const uint2* d = desc + 5ull * (t * 64u + lane);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) x ^= d[k].x + d[k].y;
+        }
+#pragma unroll 1
+        for (uint32_t step = 0; step < 32; ++step) {
+            const uint32_t f = t * 64u + 2 * step + g;
+            const uint32_t y = (uint32_t)__shfl((int)x, (int)(2 * step + g), 64);
+            if (f >= n) continue;
+            uint32_t w[3][4];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const uint32_t c = j + 32u * u;
+                w[u][0] = w[u][1] = w[u][2] = w[u][3] = y + c;
+                if (16 * c >= 42 && 16 * c + 16 <= 42 + plen) {
+                    const u32x4b v = *(const __attribute__((address_space(1))) u32x4b*)(pay + (uint64_t)plen * f + 16 * c - 42);
+                    w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const uint32_t c = j + 32u * u;
+                if (c >= chunks) continue;
+                uint32_t* o = reinterpret_cast<uint32_t*>(frames + (uint64_t)stride * f) + 4 * c;
+                if (4 * c + 4 <= ndw) {
+                    *reinterpret_cast<uint4*>(o) = make_uint4(w[u][0], w[u][1], w[u][2], w[u][3]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (4 * c + i < ndw) o[i] = w[u][i];
+                }
+            }
+            if (j == 0) {
+                lens[f] = (uint16_t)flen;
+                res[f] = (uint8_t)(y == 0x9E3779B9u);
+            }
+        }
+    }
+    if (lane == 64) sink[0] = 0;  // never: keeps the signature uniform with the other probes
+}
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_tx_layout_probe(
+    const void* desc, const void* pay, uint32_t plen, void* frames, uint32_t stride, uint32_t flen, void* lens,
+    void* res, uint32_t n, uint32_t* sink, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (!desc || !pay || !frames || !lens || !res || n == 0 || (stride & 3u) || flen > stride || flen > 1536u ||
+        (reinterpret_cast<uintptr_t>(frames) & 3u))
+        return HALO_E_INVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint32_t tiles = (n + 63u) / 64u, blocks = (tiles + 3u) / 4u;
+    const dim3 grid(blocks < 1024u ? blocks : 1024u);  // tx_build_kernel's grid for this batch
+    auto launch = [&](int) {
+        hipLaunchKernelGGL(tx_layout_probe_kernel, grid, dim3(256), 0, s, static_cast<const uint2*>(desc),
+                           static_cast<const uint8_t*>(pay), plen, static_cast<uint8_t*>(frames), stride, flen,
+                           static_cast<uint16_t*>(lens), static_cast<uint8_t*>(res), n, sink);
+        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+    };
+    return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
+}
+
 // Which physical device a rank ran on (bench.py's per-rank identity in the N-GPU line).
 extern "C" __attribute__((visibility("default"))) int halo_bench_pci_bus_id(int device, char* buf, int len) {
     if (!buf || len < 13) return HALO_E_INVAL;
