@@ -307,7 +307,7 @@ def bench_lib():
         L.halo_bench_host_calls.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, i32, i32, vp,
                                             ctypes.POINTER(ctypes.c_uint32)]
         L.halo_bench_tx_layout_probe.restype = ctypes.c_int
-        L.halo_bench_tx_layout_probe.argtypes = [vp, vp, u32, vp, u32, u32, vp, vp, u32, vp] + tail
+        L.halo_bench_tx_layout_probe.argtypes = [vp, vp, u32, u32, vp, u32, u32, vp, vp, u32, vp, u32] + tail
         _BENCH_LIB = L
     return _BENCH_LIB
 
@@ -524,9 +524,9 @@ def tx_build_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
             # the same bytes at the same addresses (1514 B frames in 1516 B slots, payloads packed
             # 1472 B apart, the build's grid and lanes) with no build work: what the layout costs
             sink = torch.zeros(16, dtype=torch.int32, device=dev)
-            _, kl = time_native(bench_lib().halo_bench_tx_layout_probe, desc_d.data_ptr(), pay_d.data_ptr(), plen,
+            _, kl = time_native(bench_lib().halo_bench_tx_layout_probe, desc_d.data_ptr(), pay_d.data_ptr(), plen, plen,
                                 frames.data_ptr(), stride, flen, lens.data_ptr(), rcode.data_ptr(), n,
-                                sink.data_ptr(), steps=20, warmup=3, d=d)
+                                sink.data_ptr(), 0, steps=20, warmup=3, d=d)
             res[name]["roofline"]["layout_matched_probe_ms"] = round(kl, 5)
             res[name]["roofline"]["frac_of_layout_matched"] = round(kl / k, 4)
         if with_cpu:

@@ -277,8 +277,15 @@ __device__ __forceinline__ void stripe_acc(uint64_t& acc, uint64_t in, uint64_t 
 // reads 16 strings' 64-byte stripes. The load is unaligned (gfx9 global loads accept any byte
 // address; the 16 bytes are all string bytes, so no other page is touched).
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+#ifndef HALO_XXH3_NT  // non-temporal string loads (the bytes are read once, bar run boundaries)
+#define HALO_XXH3_NT 0
+#endif
 __device__ __forceinline__ void ld128u(const uint8_t* p, uint64_t& lo, uint64_t& hi) {
+#if HALO_XXH3_NT
+    const u32x4u v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4u*)p);
+#else
     const u32x4u v = *(const __attribute__((address_space(1))) u32x4u*)p;
+#endif
     lo = join64(v.x, v.y);
     hi = join64(v.z, v.w);
 }
@@ -596,7 +603,7 @@ static_assert(kRunB == 4 || kRunB == 8, "a batch must not straddle a 16-stripe b
 #ifndef HALO_XXH3_ALIGNED
 #define HALO_XXH3_ALIGNED 0  // measured slower: 0.214 / 0.214 ms against 0.185 / 0.185 (profiles/r04/r4j)
 #endif
-__device__ __forceinline__ void ld128a(const uint8_t* p, uint64_t& lo, uint64_t& hi) {
+[[maybe_unused]] __device__ __forceinline__ void ld128a(const uint8_t* p, uint64_t& lo, uint64_t& hi) {
     typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t sh = (uint32_t)(a & 3u);

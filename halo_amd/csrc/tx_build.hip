@@ -293,6 +293,12 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
 #ifndef HALO_TXB_BIG_PATH
 #define HALO_TXB_BIG_PATH 1
 #endif
+#ifndef HALO_TXB_NT_LD  // body payload loads non-temporal (read once)
+#define HALO_TXB_NT_LD 0
+#endif
+#ifndef HALO_TXB_NT_ST  // body frame stores non-temporal (written once)
+#define HALO_TXB_NT_ST 0
+#endif
 template <int G, int U>
 __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, const uint32_t* hdr, uint32_t j,
                                           uint8_t* out) {
@@ -313,7 +319,11 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
             const uint32_t c = c0 + u * G;
             if (c < cb_end) {
                 gu32_t* q = (gu32_t*)((P + 16ull * c) & ~3ull);
+#if HALO_TXB_NT_LD
+                const u32x4 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)q);
+#else
                 const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)q;
+#endif
                 raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
                 raw[u][4] = sh ? q[4] : 0u;
             }
@@ -328,7 +338,12 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
                 w[i] = __builtin_amdgcn_alignbyte(raw[u][i + 1], raw[u][i], sh);
                 sum = hsum_acc(w[i], sum);
             }
+#if HALO_TXB_NT_ST
+            typedef uint32_t u32x4s __attribute__((ext_vector_type(4), aligned(4)));
+            __builtin_nontemporal_store(u32x4s{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4s*>(out + 16ull * c));
+#else
             *reinterpret_cast<uint4*>(out + 16ull * c) = make_uint4(w[0], w[1], w[2], w[3]);
+#endif
         }
     }
     const uint32_t c = j < 4 ? j : cb_end;
@@ -983,6 +998,70 @@ tx_build_kernel(const BuildParams p) {
     }
 }
 
+// Launch 1 for frames of more than 64 chunks (HALO_TXB_PAIR, the default): one wave per pair of
+// frames, 32 lanes each (build_big), no grid-stride loop — the dispatcher walks the batch in order
+// the way the size-matched probe's blocks do. A wave that owns a 64-frame tile for 32 dependent
+// steps keeps 4096 streams 97 KB apart open at once for 256k frames; the same bytes moved by a
+// no-work probe with that structure ran 0.184-0.202 ms against 0.145 for the streaming probe
+// (tools/exp/tx_layout_sweep.py, profiles/r04/r4l). Each wave still decides its tile's 64
+// descriptors (their dwords 2 and 9 only: 512 B, shared by the tile's 32 waves through the L2) for
+// the rank of its two frames among the tile's rejections; the wave holding the tile's first pair
+// writes the tile's rejection count for launches 2 and 3.
+#ifndef HALO_TXB_PAIR
+#define HALO_TXB_PAIR 1
+#endif
+template <int U>
+__global__ void __launch_bounds__(kBlock) tx_build_pair_kernel(const BuildParams p) {
+    __shared__ uint32_t s_hdr[kBlock / 64][2 * 16];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t pair = blockIdx.x * (kBlock / 64) + wv;
+    if (2ull * pair >= p.n) return;  // wave-uniform
+    const uint32_t g = lane >> 5, j = lane & 31u;
+    const uint32_t i = 2 * pair + g, t = (2 * pair) / kTile, il = t * kTile + lane;
+    uint32_t d2 = 0, d9 = 0, flen_l = 0;
+    if (il < p.n) {
+        const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.desc + il);
+        d2 = dw[2];
+        d9 = dw[9];
+    }
+    const uint32_t code_l = il < p.n ? verdict(d2, d9, p.stride, flen_l) : HALO_TX_B_PROTO;
+    const uint64_t bal = __ballot(il < p.n && code_l != HALO_TX_B_OK);
+    if (lane == 0 && (pair % (kTile / 2)) == 0) p.ws[1 + t] = (uint32_t)__popcll(bal);  // rejections in tile t
+    const uint32_t fl = i % kTile;
+    const uint32_t code = (uint32_t)__shfl((int)code_l, (int)fl, 64), flen = (uint32_t)__shfl((int)flen_l, (int)fl, 64);
+    const uint32_t before = (uint32_t)__popcll(bal & ((1ull << fl) - 1ull));
+    const bool build = i < p.n && code == HALO_TX_B_OK;
+    const uint32_t id = (*p.ip_id + 1u + i - before) & 0xFFFFu;  // iphId++ then use (ipv4.go:103-104)
+    uint32_t d[10];
+    if (i < p.n) {
+        const uint2* src = reinterpret_cast<const uint2*>(p.desc + i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint2 v = src[k];
+            d[2 * k] = v.x;
+            d[2 * k + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) d[k] = 0u;
+    }
+    const Frame f = decode(d, p.payload);
+    if (j == 0 && build) {  // the frame's header dwords 0..15 (Ethernet layout, or the loopback bytes)
+        uint32_t e[18];
+        eth_header(f, id, ipv4_cksum(f, id, (p.flags & HALO_RX_CSUM_ENABLE) != 0), p, e);
+        const bool l3 = f.mode == HALO_TX_BUILD_LOOPBACK;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            s_hdr[wv][16 * g + k] = k >= 14 ? 0u : l3 ? ((e[k + 3] >> 16) | (e[k + 4] << 16)) : e[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (build) build_big<32, U>(p, f, &s_hdr[wv][16 * g], j, p.frames + (uint64_t)i * p.stride);
+    if (j == 0 && i < p.n) {
+        p.lens[i] = build ? (uint16_t)flen : (uint16_t)0;
+        if (p.result) p.result[i] = (uint8_t)code;
+    }
+}
+
 // Launch 2 (one block): the rejections of the whole batch and before every tile; the new iphId.
 __global__ void __launch_bounds__(1024) tx_settle_kernel(const BuildParams p) {
     __shared__ uint32_t s_part[1024 / 64];
@@ -1114,6 +1193,9 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
 #define HALO_TXB_BIG_G 32
 #define HALO_TXB_BIG_U 3
 #endif
+    else if (HALO_TXB_PAIR)
+        hipLaunchKernelGGL((halo::tx_build_pair_kernel<HALO_TXB_BIG_U>), dim3((uint32_t)(((uint64_t)n + 7u) / 8u)), blk,
+                           0, s, p);
     else hipLaunchKernelGGL((halo::tx_build_kernel<HALO_TXB_BIG_G, HALO_TXB_BIG_U>), grid, blk, 0, s, p);
     hipLaunchKernelGGL(halo::tx_settle_kernel, dim3(1), dim3(1024), 0, s, p);
     hipLaunchKernelGGL(halo::tx_renumber_kernel, dim3(p.n_tiles < 256u ? p.n_tiles : 256u), dim3(halo::kBlock), 0,

@@ -313,14 +313,14 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_stream_rw(const
 // The transmit build's own layout with no build work (the tx_build line's layout-matched probe):
 // waves own 64-frame tiles like tx_build_kernel (lane l loads descriptor l's 40 bytes), then 32
 // lanes per frame, two frames per step, three 16-byte chunks per lane: payload bytes [16c - 42,
-// +16) of the frame's payload (unaligned 16-byte loads from the same addresses the build reads),
+// +16) of the frame's payload (unaligned 16-byte loads from the same addresses the build reads; payload i at pitch * i),
 // the slot's dwords up to the frame's end stored at the same addresses, then length and result.
 // What the output format (1514 B frames in 1516 B slots, payloads 1472 B apart) costs before any
 // arithmetic; the size-matched probe streams the same byte counts aligned and contiguous.
 __global__ void __launch_bounds__(256) tx_layout_probe_kernel(const uint2* desc, const uint8_t* pay, uint32_t plen,
-                                                              uint8_t* frames, uint32_t stride, uint32_t flen,
+                                                              uint32_t pitch, uint8_t* frames, uint32_t stride, uint32_t flen,
                                                               uint16_t* lens, uint8_t* res, uint32_t n,
-                                                              uint32_t* sink) {
+                                                              uint32_t* sink, uint32_t interleave) {
     typedef uint32_t u32x4b __attribute__((ext_vector_type(4), aligned(1)));
     const uint32_t lane = threadIdx.x & 63u, j = lane & 31u, g = lane >> 5;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
@@ -334,7 +334,10 @@ __global__ void __launch_bounds__(256) tx_layout_probe_kernel(const uint2* desc,
         }
 #pragma unroll 1
         for (uint32_t step = 0; step < 32; ++step) {
-            const uint32_t f = t * 64u + 2 * step + g;
+            // interleave (a diagnostic): step s of wave w takes frame pair s * nw + w instead, so the
+            // waves in flight at any time cover one contiguous window of frames
+            const uint32_t f = interleave ? 2 * ((t - wave) / nw * 32 * nw + step * nw + wave) + g
+                                          : t * 64u + 2 * step + g;
             const uint32_t y = (uint32_t)__shfl((int)x, (int)(2 * step + g), 64);
             if (f >= n) continue;
             uint32_t w[3][4];
@@ -343,7 +346,7 @@ __global__ void __launch_bounds__(256) tx_layout_probe_kernel(const uint2* desc,
                 const uint32_t c = j + 32u * u;
                 w[u][0] = w[u][1] = w[u][2] = w[u][3] = y + c;
                 if (16 * c >= 42 && 16 * c + 16 <= 42 + plen) {
-                    const u32x4b v = *(const __attribute__((address_space(1))) u32x4b*)(pay + (uint64_t)plen * f + 16 * c - 42);
+                    const u32x4b v = *(const __attribute__((address_space(1))) u32x4b*)(pay + (uint64_t)pitch * f + 16 * c - 42);
                     w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
                 }
             }
@@ -370,8 +373,9 @@ __global__ void __launch_bounds__(256) tx_layout_probe_kernel(const uint2* desc,
 }
 
 extern "C" __attribute__((visibility("default"))) int halo_bench_tx_layout_probe(
-    const void* desc, const void* pay, uint32_t plen, void* frames, uint32_t stride, uint32_t flen, void* lens,
-    void* res, uint32_t n, uint32_t* sink, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    const void* desc, const void* pay, uint32_t plen, uint32_t pitch, void* frames, uint32_t stride, uint32_t flen, void* lens,
+    void* res, uint32_t n, uint32_t* sink, uint32_t interleave, int warmup, int steps, void* stream, float* region_ms,
+    double* wall_s) {
     if (!desc || !pay || !frames || !lens || !res || n == 0 || (stride & 3u) || flen > stride || flen > 1536u ||
         (reinterpret_cast<uintptr_t>(frames) & 3u))
         return HALO_E_INVAL;
@@ -380,8 +384,8 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_tx_layout_probe
     const dim3 grid(blocks < 1024u ? blocks : 1024u);  // tx_build_kernel's grid for this batch
     auto launch = [&](int) {
         hipLaunchKernelGGL(tx_layout_probe_kernel, grid, dim3(256), 0, s, static_cast<const uint2*>(desc),
-                           static_cast<const uint8_t*>(pay), plen, static_cast<uint8_t*>(frames), stride, flen,
-                           static_cast<uint16_t*>(lens), static_cast<uint8_t*>(res), n, sink);
+                           static_cast<const uint8_t*>(pay), plen, pitch, static_cast<uint8_t*>(frames), stride, flen,
+                           static_cast<uint16_t*>(lens), static_cast<uint8_t*>(res), n, sink, interleave);
         return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
     };
     return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
