@@ -306,6 +306,8 @@ def bench_lib():
         L.halo_bench_host_calls.restype = ctypes.c_int
         L.halo_bench_host_calls.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, i32, i32, vp,
                                             ctypes.POINTER(ctypes.c_uint32)]
+        L.halo_bench_gather_probe.restype = ctypes.c_int
+        L.halo_bench_gather_probe.argtypes = [vp, vp, i32, u32, vp] + tail
         L.halo_bench_tx_layout_probe.restype = ctypes.c_int
         L.halo_bench_tx_layout_probe.argtypes = [vp, vp, u32, u32, vp, u32, u32, vp, vp, u32, vp, u32] + tail
         _BENCH_LIB = L
@@ -749,6 +751,15 @@ def route_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
            "note": "alg bytes = address in + route id out; each lookup also reads 1-2 random 4 B table "
                    "entries (tbl24 stays resident in the 256 MB Infinity Cache)"}
     t.close()
+    # the lookups' own access pattern with no lookup logic: tbl[ip >> 8] over a 64 MB table, one
+    # random 4-byte read per address (what DIR-24-8's first level costs), same addresses, same count
+    tbl = torch.randint(0, 1 << 30, (1 << 24,), dtype=torch.int32, device=dev)
+    _, kg = time_native(bench_lib().halo_bench_gather_probe, tbl.data_ptr(), arr, len(bs), n, out.data_ptr(),
+                        steps=steps, warmup=warmup, d=d)
+    res["roofline"]["gather_probe_ms"] = round(kg, 5)
+    res["roofline"]["frac_of_gather_probe"] = round(kg / k, 4)
+    res["gather_probe"] = "one random 4 B read of a 2^24-entry table per address (tbl[ip >> 8]) + 4 B out"
+    del tbl
     if with_cpu:
         from oracle import oracle as O
 

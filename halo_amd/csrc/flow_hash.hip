@@ -578,7 +578,7 @@ struct RunLds {
 #define HALO_XXH3_RUN_B 8
 #endif
 constexpr uint32_t kRunB = HALO_XXH3_RUN_B;
-static_assert(kRunB == 4 || kRunB == 8, "a batch must not straddle a 16-stripe block");
+static_assert(kRunB == 4 || kRunB == 8 || kRunB == 16, "a batch must not straddle a 16-stripe block");
 [[maybe_unused]] __device__ __forceinline__ uint32_t run_cost(uint32_t len) {
     return len > 240 ? ((len - 1) / 64 + kRunB) / kRunB : 1u;  // ceil((T + 1) / B), T = loop stripes
 }

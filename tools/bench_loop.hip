@@ -391,6 +391,30 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_tx_layout_probe
     return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
 }
 
+// The route lookup's access pattern with no lookup logic (the route line's gather probe): one
+// table entry per address at a random index (tbl[ip >> 8] over a 2^24-entry, 64 MB table, as
+// DIR-24-8's first level), one 4-byte result out, lane per address, rotating address arrays.
+__global__ void __launch_bounds__(256) gather_probe_kernel(const uint32_t* __restrict__ tbl,
+                                                           const uint32_t* __restrict__ ips, uint32_t n,
+                                                           uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) out[i] = tbl[ips[i] >> 8];
+}
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_gather_probe(
+    const void* tbl, const void* const* ips, int nb, uint32_t n, void* out, int warmup, int steps, void* stream,
+    float* region_ms, double* wall_s) {
+    if (!tbl || !ips || nb <= 0 || !out || n == 0) return HALO_E_INVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto launch = [&](int step) {
+        hipLaunchKernelGGL(gather_probe_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s,
+                           static_cast<const uint32_t*>(tbl), static_cast<const uint32_t*>(ips[step % nb]), n,
+                           static_cast<uint32_t*>(out));
+        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+    };
+    return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
+}
+
 // Which physical device a rank ran on (bench.py's per-rank identity in the N-GPU line).
 extern "C" __attribute__((visibility("default"))) int halo_bench_pci_bus_id(int device, char* buf, int len) {
     if (!buf || len < 13) return HALO_E_INVAL;
