@@ -786,6 +786,9 @@ __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t s
 #ifndef HALO_TXB_DESC_PREFETCH
 #define HALO_TXB_DESC_PREFETCH 0
 #endif
+#ifndef HALO_TXB_DESC_LDS  // G = 1: the tile's descriptors read coalesced, through LDS
+#define HALO_TXB_DESC_LDS 0  // measured slower: 64 B 30.2 / 30.5 us against 29.1 / 29.3 (profiles/r04/r4p)
+#endif
 #ifndef HALO_TXB_G1_WAVES
 #define HALO_TXB_G1_WAVES 4
 #endif
@@ -853,6 +856,24 @@ tx_build_kernel(const BuildParams p) {
 #pragma unroll
             for (int k = 0; k < 10; ++k) d[k] = dn[k];
             load_desc((t + nw) * kTile + lane, dn);
+        } else if constexpr (G == 1 && HALO_TXB_DESC_LDS) {
+            // the tile's 64 descriptors as 320 consecutive 8-byte words, lane l taking words l,
+            // l + 64, ... (each load instruction reads 512 contiguous bytes instead of 64 words 40 B
+            // apart), through the wave's header rows (free until the headers are written below)
+            const uint2* src = reinterpret_cast<const uint2*>(p.desc + first);
+            const uint32_t words = (p.n - first < kTile ? p.n - first : kTile) * 5u;
+            uint32_t* scratch = &s_hdr[wv][0];
+#pragma unroll
+            for (uint32_t k = 0; k < 5; ++k) {
+                const uint32_t w = 64u * k + lane;
+                const uint2 v = w < words ? src[w] : make_uint2(0u, 0u);
+                scratch[2 * w] = v.x;
+                scratch[2 * w + 1] = v.y;
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int k = 0; k < 10; ++k) d[k] = scratch[10 * lane + k];
+            __builtin_amdgcn_wave_barrier();  // read before the header rows are written
         } else {
             load_desc(i, d);
         }
@@ -1010,11 +1031,23 @@ tx_build_kernel(const BuildParams p) {
 #ifndef HALO_TXB_PAIR
 #define HALO_TXB_PAIR 1
 #endif
+#ifndef HALO_TXB_PAIR_XCD
+#define HALO_TXB_PAIR_XCD 1
+#endif
 template <int U>
 __global__ void __launch_bounds__(kBlock) tx_build_pair_kernel(const BuildParams p) {
     __shared__ uint32_t s_hdr[kBlock / 64][2 * 16];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t pair = blockIdx.x * (kBlock / 64) + wv;
+    // XCD-aware order (HALO_TXB_PAIR_XCD): blocks are dealt round-robin over the 8 XCDs, and the 8
+    // blocks of a tile all read the tile's descriptor block — in dispatch order once per XCD, 1.19x
+    // the algorithmic reads (r4p). Within each run of 64 blocks (8 tiles), block b takes tile
+    // b % 8 of the run, part (b / 8) % 8: a tile stays on one XCD, and the batch is still walked
+    // in order 8 tiles at a time. (Giving each XCD a contiguous eighth of the batch instead cut the
+    // reads to 1.0002x but ran 2-3 % slower: r4q.)
+    const uint32_t lb = HALO_TXB_PAIR_XCD == 2 ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                      : HALO_TXB_PAIR_XCD == 1 ? (blockIdx.x & ~63u) | ((blockIdx.x & 7u) << 3) | ((blockIdx.x >> 3) & 7u)
+                                               : blockIdx.x;
+    const uint32_t pair = lb * (kBlock / 64) + wv;
     if (2ull * pair >= p.n) return;  // wave-uniform
     const uint32_t g = lane >> 5, j = lane & 31u;
     const uint32_t i = 2 * pair + g, t = (2 * pair) / kTile, il = t * kTile + lane;
@@ -1194,8 +1227,8 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
 #define HALO_TXB_BIG_U 3
 #endif
     else if (HALO_TXB_PAIR)
-        hipLaunchKernelGGL((halo::tx_build_pair_kernel<HALO_TXB_BIG_U>), dim3((uint32_t)(((uint64_t)n + 7u) / 8u)), blk,
-                           0, s, p);
+        hipLaunchKernelGGL((halo::tx_build_pair_kernel<HALO_TXB_BIG_U>),
+                           dim3((uint32_t)(((uint64_t)n + 511u) / 512u * 64u)), blk, 0, s, p);  // runs of 8 tiles
     else hipLaunchKernelGGL((halo::tx_build_kernel<HALO_TXB_BIG_G, HALO_TXB_BIG_U>), grid, blk, 0, s, p);
     hipLaunchKernelGGL(halo::tx_settle_kernel, dim3(1), dim3(1024), 0, s, p);
     hipLaunchKernelGGL(halo::tx_renumber_kernel, dim3(p.n_tiles < 256u ? p.n_tiles : 256u), dim3(halo::kBlock), 0,

@@ -84,13 +84,13 @@ def main():
         if w.startswith("flow_hash"):
             return "flow_hash_kernel"
         if w.startswith("tx_build"):
-            return "tx_build_kernel"
+            return "tx_build_"
         return "tx_fixup" if w.startswith("tx_") else "rx_"
 
     def attribute(rows, key="Dispatch_Id"):
         """dispatch id -> workload: each kernel family's dispatches in launch order."""
         amap = {}
-        for fam in ("rx_", "tx_fixup", "flow_hash_kernel", "tx_build_kernel"):
+        for fam in ("rx_", "tx_fixup", "flow_hash_kernel", "tx_build_"):
             disp = sorted({int(r[key]) for r in rows if fam in r["Kernel_Name"]})
             ws = [w for w in order if family(w) == fam]
             # (the flow-hash workload's one preparatory parse comes after every rx workload's
