@@ -13,11 +13,11 @@
 // the k-th built frame of the batch carries base + k. A descriptor that Build* rejects is rare
 // (a caller error), so frame i is built with base + 1 + i - (rejected descriptors before it in
 // its own 64-descriptor tile) — everything its wave knows — and the rejections in earlier tiles
-// are settled afterwards: a one-block launch checks the per-tile rejection counts (writing the
-// new iphId) and, only when there were any, a third launch patches the identification and header
-// checksum of the frames behind them (RFC 1624). No atomics and no inter-block waiting anywhere:
-// a ticketed single pass with a decoupled look-back measured 175 us for 1M 64 B frames (its
-// ticket atomics serialise at ~25 ns each: 4096 tickets alone cost 100 us).
+// are settled afterwards by one more launch: it writes the new iphId and, only when a tile marked
+// a rejection, patches the identification and header checksum of the frames behind it (RFC 1624).
+// No atomics and no inter-block waiting anywhere: a ticketed single pass with a decoupled
+// look-back measured 175 us for 1M 64 B frames (its ticket atomics serialise at ~25 ns each: 4096
+// tickets alone cost 100 us).
 //
 // Build. Each wave owns 64-descriptor tiles (grid-stride): lane i loads descriptor i, decides it
 // (Build* length limits, slot size), ranks the rejections with a ballot and writes its frame's
@@ -35,6 +35,7 @@
 // DESIGN.md §10.5).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <type_traits>
 
 #include "device_util.h"
@@ -56,6 +57,7 @@ struct BuildParams {
     uint32_t* ws;                 // [0] rejections in the batch, [1 + t] rejections before / in tile t
     uint32_t n, n_tiles, flags, stride;
     uint32_t mac_lo, mac_hi;      // the NetIf's MAC (BuildEthFrm srcMac), little-endian packed
+    uint32_t seq;                 // this launch's sequence number (ws[0] = seq: a tile saw a rejection)
 };
 
 
@@ -881,7 +883,10 @@ tx_build_kernel(const BuildParams p) {
         const uint32_t code = i < p.n ? verdict(d[2], d[9], p.stride, flen) : HALO_TX_B_PROTO;
         const bool rej = i < p.n && code != HALO_TX_B_OK;
         const uint64_t bal = __ballot(rej);
-        if (lane == 0 && part == 0) p.ws[1 + t] = (uint32_t)__popcll(bal);  // rejections in this tile
+        if (lane == 0 && part == 0) {
+            p.ws[1 + t] = (uint32_t)__popcll(bal);  // rejections in this tile
+            if (bal) p.ws[0] = p.seq;
+        }
         const uint32_t before =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
         // iphId++ then use (ipv4.go:103-104); rejections in earlier tiles settled by launches 2/3
@@ -1059,7 +1064,10 @@ __global__ void __launch_bounds__(kBlock) tx_build_pair_kernel(const BuildParams
     }
     const uint32_t code_l = il < p.n ? verdict(d2, d9, p.stride, flen_l) : HALO_TX_B_PROTO;
     const uint64_t bal = __ballot(il < p.n && code_l != HALO_TX_B_OK);
-    if (lane == 0 && (pair % (kTile / 2)) == 0) p.ws[1 + t] = (uint32_t)__popcll(bal);  // rejections in tile t
+    if (lane == 0 && (pair % (kTile / 2)) == 0) {
+        p.ws[1 + t] = (uint32_t)__popcll(bal);  // rejections in tile t
+        if (bal) p.ws[0] = p.seq;
+    }
     const uint32_t fl = i % kTile;
     const uint32_t code = (uint32_t)__shfl((int)code_l, (int)fl, 64), flen = (uint32_t)__shfl((int)flen_l, (int)fl, 64);
     const uint32_t before = (uint32_t)__popcll(bal & ((1ull << fl) - 1ull));
@@ -1095,24 +1103,29 @@ __global__ void __launch_bounds__(kBlock) tx_build_pair_kernel(const BuildParams
     }
 }
 
-// Launch 2 (one block): the rejections of the whole batch and before every tile; the new iphId.
-__global__ void __launch_bounds__(1024) tx_settle_kernel(const BuildParams p) {
+// Launch 2: the new iphId, and only after a rejection the renumbering of the frames behind it. A
+// tile that saw a rejection stores this launch's sequence number (p.seq) in ws[0] beside its count
+// in ws[1 + t]. The common case — no tile did — is one load per block and one iphId update: round 3
+// ran a one-block settle launch and a renumber launch after every build, ~6 us of launch gaps per
+// step (a 64 B build is 23 us of kernel; r4t). A stale or uninitialised ws[0] equal to p.seq only by
+// chance takes the full path, which recomputes everything from the tile counts and is exact anyway.
+// Full path: every block scans the tile counts 1024 at a time (exclusive prefix in LDS) and patches
+// the frames of its own tiles (t = block mod grid) that were numbered too high by the rejections in
+// earlier tiles: identification and, with checksums on, the IPv4 header checksum (RFC 1624
+// incremental update of the value BuildIpv4Pkt computed); block 0 writes the new iphId.
+__global__ void __launch_bounds__(1024) tx_finish_kernel(const BuildParams p) {
     __shared__ uint32_t s_part[1024 / 64];
     __shared__ uint32_t s_carry;
+    __shared__ uint32_t s_pre[1024];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    // the common case first: no rejection anywhere (every load of the pass in flight at once)
-    uint32_t any = 0;
-    for (uint32_t t = tid; t < p.n_tiles; t += 1024) any |= p.ws[1 + t];
-    if (tid == 0) s_carry = 0;
-    const int none = __syncthreads_or(any != 0) == 0;
-    if (none) {
-        if (tid == 0) {
-            p.ws[0] = 0;
-            *p.ip_id = (uint16_t)(*p.ip_id + p.n);  // one iphId++ per built packet
-        }
-        return;  // the tile counts are all 0 = the rejections before every tile
+    if (p.ws[0] != p.seq) {  // no rejection in this launch
+        if (blockIdx.x == 0 && tid == 0) *p.ip_id = (uint16_t)(*p.ip_id + p.n);  // one iphId++ per built packet
+        return;
     }
-    for (uint32_t t0 = 0; t0 < p.n_tiles; t0 += 1024) {  // exclusive scan, 1024 tiles per pass
+    const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t t0 = 0; t0 < p.n_tiles; t0 += 1024) {
         const uint32_t t = t0 + tid;
         const uint32_t v = t < p.n_tiles ? p.ws[1 + t] : 0u;
         uint32_t x = v;
@@ -1125,45 +1138,35 @@ __global__ void __launch_bounds__(1024) tx_settle_kernel(const BuildParams p) {
         __syncthreads();
         uint32_t off = s_carry;
         for (uint32_t w = 0; w < wave; ++w) off += s_part[w];
-        if (t < p.n_tiles) p.ws[1 + t] = off + x - v;  // rejections before tile t
+        s_pre[tid] = off + x - v;  // rejections before tile t
         __syncthreads();
+        // this block's tiles of the pass, one wave per tile, lane = frame of the tile
+        const uint32_t r0 = (blockIdx.x + gridDim.x - t0 % gridDim.x) % gridDim.x;
+        for (uint32_t r = r0 + wave * gridDim.x; r < 1024 && t0 + r < p.n_tiles; r += 16 * gridDim.x) {
+            const uint32_t back = s_pre[r];
+            const uint32_t i = (t0 + r) * kTile + lane;
+            if (back == 0u || i >= p.n || p.lens[i] == 0) continue;
+            const uint32_t mode = (reinterpret_cast<const uint32_t*>(p.desc + i)[9] >> 16) & 0xFFu;
+            uint8_t* ip = p.frames + (uint64_t)i * p.stride + (mode == HALO_TX_BUILD_LOOPBACK ? 0u : 14u);
+            const uint32_t old_id = ((uint32_t)ip[4] << 8) | ip[5];
+            const uint32_t new_id = (old_id - back) & 0xFFFFu;
+            ip[4] = (uint8_t)(new_id >> 8);
+            ip[5] = (uint8_t)new_id;
+            if (csum) {  // HC' = ~(~HC + ~m + m')
+                const uint32_t hc = ((uint32_t)ip[10] << 8) | ip[11];
+                const uint32_t nc = (~fold16((~hc & 0xFFFFu) + (~old_id & 0xFFFFu) + new_id)) & 0xFFFFu;
+                ip[10] = (uint8_t)(nc >> 8);
+                ip[11] = (uint8_t)nc;
+            }
+        }
         if (tid == 0) {
             uint32_t tot = 0;
             for (uint32_t w = 0; w < 1024 / 64; ++w) tot += s_part[w];
             s_carry += tot;
         }
-        __syncthreads();
+        __syncthreads();  // s_pre and s_part are rewritten by the next pass
     }
-    if (tid == 0) {
-        p.ws[0] = s_carry;
-        *p.ip_id = (uint16_t)(*p.ip_id + p.n - s_carry);  // one iphId++ per built packet
-    }
-}
-
-// Launch 3 (only useful after a rejection): frames behind rejections in earlier tiles were
-// numbered too high by that many; patch their identification and, with checksums on, their
-// IPv4 header checksum (RFC 1624 incremental update of the value BuildIpv4Pkt computed).
-__global__ void __launch_bounds__(kBlock) tx_renumber_kernel(const BuildParams p) {
-    if (p.ws[0] == 0u) return;  // the common case: nothing was rejected
-    const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
-    for (uint32_t t = blockIdx.x; t < p.n_tiles; t += gridDim.x) {
-        const uint32_t back = p.ws[1 + t];
-        if (back == 0u || threadIdx.x >= kTile) continue;
-        const uint32_t i = t * kTile + threadIdx.x;
-        if (i >= p.n || p.lens[i] == 0) continue;
-        const uint32_t mode = (reinterpret_cast<const uint32_t*>(p.desc + i)[9] >> 16) & 0xFFu;
-        uint8_t* ip = p.frames + (uint64_t)i * p.stride + (mode == HALO_TX_BUILD_LOOPBACK ? 0u : 14u);
-        const uint32_t old_id = ((uint32_t)ip[4] << 8) | ip[5];
-        const uint32_t new_id = (old_id - back) & 0xFFFFu;
-        ip[4] = (uint8_t)(new_id >> 8);
-        ip[5] = (uint8_t)new_id;
-        if (csum) {  // HC' = ~(~HC + ~m + m')
-            const uint32_t hc = ((uint32_t)ip[10] << 8) | ip[11];
-            const uint32_t nc = (~fold16((~hc & 0xFFFFu) + (~old_id & 0xFFFFu) + new_id)) & 0xFFFFu;
-            ip[10] = (uint8_t)(nc >> 8);
-            ip[11] = (uint8_t)nc;
-        }
-    }
+    if (blockIdx.x == 0 && tid == 0) *p.ip_id = (uint16_t)(*p.ip_id + p.n - s_carry);
 }
 
 }  // namespace
@@ -1204,6 +1207,8 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
     p.mac_lo = (uint32_t)netif->mac[0] | ((uint32_t)netif->mac[1] << 8) | ((uint32_t)netif->mac[2] << 16) |
                ((uint32_t)netif->mac[3] << 24);
     p.mac_hi = (uint32_t)netif->mac[4] | ((uint32_t)netif->mac[5] << 8);
+    static std::atomic<uint32_t> launches{0};
+    do p.seq = launches.fetch_add(1, std::memory_order_relaxed) + 1u; while (p.seq == 0u);
     hipStream_t s = static_cast<hipStream_t>(stream);
     // a wave per tile of 64 descriptors, grid-stride: up to 8 resident 4-wave blocks per CU
 #ifndef HALO_TXB_MAX_BLOCKS
@@ -1230,8 +1235,6 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
         hipLaunchKernelGGL((halo::tx_build_pair_kernel<HALO_TXB_BIG_U>),
                            dim3((uint32_t)(((uint64_t)n + 511u) / 512u * 64u)), blk, 0, s, p);  // runs of 8 tiles
     else hipLaunchKernelGGL((halo::tx_build_kernel<HALO_TXB_BIG_G, HALO_TXB_BIG_U>), grid, blk, 0, s, p);
-    hipLaunchKernelGGL(halo::tx_settle_kernel, dim3(1), dim3(1024), 0, s, p);
-    hipLaunchKernelGGL(halo::tx_renumber_kernel, dim3(p.n_tiles < 256u ? p.n_tiles : 256u), dim3(halo::kBlock), 0,
-                       s, p);
+    hipLaunchKernelGGL(halo::tx_finish_kernel, dim3(p.n_tiles < 64u ? p.n_tiles : 64u), dim3(1024), 0, s, p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }

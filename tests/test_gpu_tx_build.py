@@ -127,6 +127,44 @@ def test_build_slots_ids_and_two_launches(dev, oracle_lib):
     assert b.iph_id == 7 + 2 * built
 
 
+@pytest.mark.parametrize("hint", [22, 1472])
+def test_build_rejections_then_clean_launch(dev, oracle_lib, hint):
+    """The finish launch's two paths on one workspace: a batch with rejections spread over many
+    tiles (every 97th descriptor an unknown protocol), then a clean batch (the workspace still holds
+    the first launch's marks), then the first batch again — frames, lengths, results and the iphId
+    sequence equal the oracle's after each launch."""
+    import torch
+
+    from halo_amd._lib import BUILD_DESC_DTYPE
+    from halo_amd.protocol import TxBuilder
+
+    n = 70_000
+    plen = hint
+    desc = np.zeros(n, BUILD_DESC_DTYPE)
+    desc["proto"] = 17
+    desc["payload_len"] = plen
+    desc["payload_off"] = np.arange(n, dtype=np.uint64) * plen
+    desc["src_ip"], desc["dst_ip"] = 0x0A000001, 0x0A000002
+    bad = desc.copy()
+    bad["proto"][::97] = 99
+    payload = (np.arange(n * plen + 64, dtype=np.uint64) * 7).astype(np.uint8)
+    mac = bytes.fromhex("020000000001")
+    b = TxBuilder(n, device=dev, ip_id=0xFFF0)
+    pl = torch.from_numpy(payload).to(dev)
+    want_id = 0xFFF0
+    for batch in (bad, desc, bad):
+        d = torch.from_numpy(batch.view(np.uint8)).to(dev)
+        frames = torch.zeros((n, 1516), dtype=torch.uint8, device=dev)
+        frames, lens, res = b.build(d, pl, netif=_netif(mac.hex()), out_stride=1516, frames=frames,
+                                    max_payload_hint=hint)
+        torch.cuda.synchronize()
+        wf, wl, wr, we = oracle_lib.tx_build_batch(batch, payload, mac, 1, 1516, want_id)
+        assert np.array_equal(res.cpu().numpy(), wr) and np.array_equal(lens.cpu().numpy().view(np.uint16), wl)
+        assert np.array_equal(frames.cpu().numpy(), wf)
+        assert b.iph_id == we
+        want_id = we
+
+
 def test_build_then_parse_round_trip(dev):
     """1M 64-byte UDP frames built on the GPU into 64 B slots parse clean on the GPU receive path
     (halo_rx_parse_strided_device) with the descriptors' addresses, ports and payload lengths."""

@@ -92,7 +92,7 @@ for s in "$@"; do
     vxx)   step vxx 600 bash tools/exp/variant_tests.sh "tests/test_gpu_flow_hash.py -m gpu" ${VX:-xxg8} ;;
     txlay) step tx_layout 600 python tools/exp/tx_layout_sweep.py ;;
     txx)   step pytest_xxh3 600 python -u -m pytest tests/test_gpu_flow_hash.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
-    prof4) PK_ARGS="config2 config2_batch_stream lo_drain_1M_50B flow_hash_config2 flow_hash_config2_compact tx_build_udp_256k_1514B"
+    prof4) PK_ARGS="${PK4:-config2 config2_batch_stream lo_drain_1M_50B flow_hash_config2 flow_hash_config2_compact tx_build_udp_256k_1514B}"
            step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 tools/prof_kernels.py $PK_ARGS
            step krd 600 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krd" -o run -- python3 tools/prof_kernels.py $PK_ARGS
            step kwrq 600 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/kwrq" -o run -- python3 tools/prof_kernels.py $PK_ARGS
