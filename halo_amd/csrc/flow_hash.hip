@@ -595,6 +595,9 @@ static_assert(kRunB == 4 || kRunB == 8 || kRunB == 16, "a batch must not straddl
 #ifndef HALO_XXH3_BF
 #define HALO_XXH3_BF 1
 #endif
+#ifndef HALO_XXH3_PROBE  // tools only: the run kernel's loads without the hashing (wrong hashes)
+#define HALO_XXH3_PROBE 0
+#endif
 #ifndef HALO_XXH3_MERGED  // one finishing sequence for long merges and 17..240 B strings
 #define HALO_XXH3_MERGED 0   // measured slower: 0.189 / 0.189 ms against 0.188 / 0.186 (profiles/r04/r4i)
 #endif
@@ -710,7 +713,25 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
         }
         uint64_t h = 0;
         bool have = false;
-#if HALO_XXH3_MERGED
+#if HALO_XXH3_PROBE
+        // measurement probe (tools only, wrong hashes): the same loads and control flow, no hashing
+        if (lng) {
+#pragma unroll
+            for (uint32_t u = 0; u < kRunB; ++u) {
+                a0 ^= lo[u];
+                a1 ^= hi[u];
+            }
+            st += kRunB;
+            if (st > T) {
+                h = a0 ^ a1;
+                have = true;
+            }
+        }
+        if (mid) {
+            h = lo[0] ^ hi[0] ^ lo[1] ^ hi[1] ^ lo[2] ^ hi[2] ^ lo[3] ^ hi[3];
+            have = true;
+        }
+#elif HALO_XXH3_MERGED
         bool fin = false;
         if (lng) {
 #pragma unroll
@@ -834,6 +855,199 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
     }
 }
 #endif  // HALO_XXH3_RUNS
+
+// ---- the run kernel, software-pipelined (HALO_XXH3_PIPE) -----------------------------------
+// The branch-free run kernel with step k + 1's loads issued before step k's arithmetic: the next
+// step of a group is known before its data arrives (the same long string B stripes on, or the next
+// string of the run), so a wave keeps two steps' loads in flight. With 4096 waves for 1M strings
+// the grid is 4 waves per SIMD whatever the kernel's VGPRs, so the second buffer costs no occupancy
+// up to 128 VGPRs.
+#ifndef HALO_XXH3_PIPE
+#define HALO_XXH3_PIPE 0
+#endif
+#if HALO_XXH3_PIPE && HALO_XXH3_RUNS
+struct RunState {
+    const uint8_t* d;
+    uint32_t idx, len, T, nb, st;
+};
+#ifndef HALO_XXH3_PIPE_WAVES
+#define HALO_XXH3_PIPE_WAVES 4
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HALO_XXH3_PIPE_WAVES)))
+xxh3_runp_kernel(const XxhParams p) {
+    __shared__ LongSecrets sec;
+    __shared__ RunLds s;
+    load_secrets(sec);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t base = blockIdx.x * p.win;
+    const uint32_t cnt = p.n - base < p.win ? p.n - base : p.win;
+    uint32_t total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kRunPer; ++k) {
+        const uint32_t r = 64 * k + lane;
+        const bool in = r < cnt;
+        const uint32_t len = in ? p.lens[base + r] : 0u;
+        s.len[r] = len;
+        s.off[r] = in ? p.offsets[base + r] : 0ull;
+        const uint32_t w = in ? run_cost(len) : 0u;
+        uint32_t incl = w;
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t o = __shfl_up(incl, dd, 64);
+            if (lane >= (uint32_t)dd) incl += o;
+        }
+        s.pref[r] = total + incl - w;
+        total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    __syncthreads();
+    const uint32_t g = lane >> 2, j = lane & 3u;
+    auto first_at = [&](uint32_t t) {
+        uint32_t lo = 0, hi = cnt;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (s.pref[m] < t) lo = m + 1;
+            else hi = m;
+        }
+        return lo;
+    };
+    const uint32_t idx0 = first_at((uint32_t)(((uint64_t)g * total + 15) / 16));
+    const uint32_t end = g == 15 ? cnt : first_at((uint32_t)(((uint64_t)(g + 1) * total + 15) / 16));
+    constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+    const uint64_t init0 = j == 0 ? kInit[0] : j == 1 ? kInit[2] : j == 2 ? kInit[4] : kInit[6];
+    const uint64_t init1 = j == 0 ? kInit[1] : j == 1 ? kInit[3] : j == 2 ? kInit[5] : kInit[7];
+    auto state_at = [&](uint32_t i) {
+        RunState r;
+        r.idx = i;
+        r.st = 0;
+        r.len = i < end ? s.len[i] : 0u;
+        r.d = p.bytes + (i < end ? s.off[i] : 0ull);
+        r.T = r.len > 240 ? (r.len - 1) / 64 : 0u;
+        r.nb = r.len > 240 ? (r.len - 1) / 1024 : 0u;
+        return r;
+    };
+    auto advance = [&](const RunState& c) {  // the step after c
+        if (c.idx < end && c.len > 240 && c.st + kRunB <= c.T) {
+            RunState r = c;
+            r.st += kRunB;
+            return r;
+        }
+        return state_at(c.idx < end ? c.idx + 1 : end);
+    };
+    auto issue = [&](const RunState& c, uint64_t (&lo)[kRunB], uint64_t (&hi)[kRunB]) {
+        const bool act = c.idx < end;
+        const bool lng = act && c.len > 240, mid = act && c.len > 16 && c.len <= 240;
+        const bool large = c.len > 128;
+        const uint32_t lv = c.len > 96 ? 4u : c.len > 64 ? 3u : c.len > 32 ? 2u : 1u;
+        const uint32_t nmid = large ? ((c.len & ~15u) - 128) / 16 : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kRunB; ++u) {
+            const uint8_t* a = c.d;
+            bool v = false;
+            if (lng) {
+                const uint32_t x = c.st + u;
+                v = x <= c.T;
+                a = x < c.T ? c.d + 64 * x + 16 * j : c.d + c.len - 64 + 16 * j;
+            } else if (u >= 4) {
+            } else if (mid && !large) {
+                v = u < 2 && j < lv;
+                a = u == 0 ? c.d + 16 * j : c.d + c.len - 16 - 16 * j;
+            } else if (mid) {
+                const uint32_t t = 2 * j + (u & 1u);
+                v = u < 2 || t <= nmid;
+                a = u < 2 ? c.d + 16 * t : t < nmid ? c.d + 128 + 16 * t : c.d + c.len - 16;
+            }
+            ld128u(v ? a : g_xxh3_pad, lo[u], hi[u]);
+        }
+    };
+    uint64_t a0 = init0, a1 = init1;
+    auto process = [&](const RunState& c, const uint64_t (&lo)[kRunB], const uint64_t (&hi)[kRunB]) {
+        const bool act = c.idx < end;
+        const bool lng = act && c.len > 240, mid = act && c.len > 16 && c.len <= 240, sml = act && c.len <= 16;
+        const bool large = c.len > 128;
+        const uint32_t lv = c.len > 96 ? 4u : c.len > 64 ? 3u : c.len > 32 ? 2u : 1u;
+        const uint32_t nmid = large ? ((c.len & ~15u) - 128) / 16 : 0u;
+        uint64_t h = 0;
+        bool have = false;
+        if (lng) {
+#pragma unroll
+            for (uint32_t u = 0; u < kRunB; ++u) {
+                const uint32_t x = c.st + u;
+                const uint64_t s0 = x < c.T ? sec.w8[(x & 15u) + 2 * j] : sec.last[2 * j];
+                const uint64_t s1 = x < c.T ? sec.w8[(x & 15u) + 2 * j + 1] : sec.last[2 * j + 1];
+                const uint64_t k0 = lo[u] ^ s0, k1 = hi[u] ^ s1;
+                const uint64_t t0 = hi[u] + (uint64_t)(uint32_t)k0 * (k0 >> 32);
+                const uint64_t t1 = lo[u] + (uint64_t)(uint32_t)k1 * (k1 >> 32);
+                a0 += x <= c.T ? t0 : 0ull;
+                a1 += x <= c.T ? t1 : 0ull;
+            }
+            const uint32_t st = c.st + kRunB;
+            if ((st & 15u) == 0 && (st >> 4) <= c.nb) {  // a full block ended: scramble (xxh3.go:212-218)
+                a0 ^= a0 >> 47;
+                a1 ^= a1 >> 47;
+                a0 ^= sec.w8[16 + 2 * j];
+                a1 ^= sec.w8[17 + 2 * j];
+                a0 *= P32_1;
+                a1 *= P32_1;
+            }
+            if (st > c.T) {  // merge (xxh3.go:139-145)
+                const uint64_t m = quad_sum(mul_fold64(a0 ^ sec.merge[2 * j], a1 ^ sec.merge[2 * j + 1]));
+                h = avalanche((uint64_t)c.len * P64_1 + m);
+                have = true;
+            }
+        }
+        if (mid) {
+            uint64_t t01 = 0, t23 = 0;
+            if (!large) {
+                if (j < lv)
+                    t01 = mul_fold64(lo[0] ^ sec.w8[4 * j], hi[0] ^ sec.w8[4 * j + 1]) +
+                          mul_fold64(lo[1] ^ sec.w8[4 * j + 2], hi[1] ^ sec.w8[4 * j + 3]);
+                h = avalanche((uint64_t)c.len * P64_1 + quad_sum(t01));
+            } else {
+                t01 = mul_fold64(lo[0] ^ sec.w8[4 * j], hi[0] ^ sec.w8[4 * j + 1]) +
+                      mul_fold64(lo[1] ^ sec.w8[4 * j + 2], hi[1] ^ sec.w8[4 * j + 3]);
+                const uint64_t acc = avalanche((uint64_t)c.len * P64_1 + quad_sum(t01));
+#pragma unroll
+                for (uint32_t u = 2; u < 4; ++u) {
+                    const uint32_t t = 2 * j + (u & 1u);
+                    if (t < nmid) t23 += mul_fold64(lo[u] ^ sec.mid3[2 * t], hi[u] ^ sec.mid3[2 * t + 1]);
+                    else if (t == nmid) t23 += mul_fold64(lo[u] ^ sec.mlast[0], hi[u] ^ sec.mlast[1]);
+                }
+                h = avalanche(acc + quad_sum(t23));
+            }
+            have = true;
+        }
+        if (sml) {
+            h = hash_upto16(c.d, c.len);
+            have = true;
+        }
+        if (have) {
+            if (j == 0) s.hash[c.idx] = h;
+            a0 = init0;
+            a1 = init1;
+        }
+    };
+    uint64_t la[kRunB], ha[kRunB], lb[kRunB], hb[kRunB];
+    RunState c = state_at(idx0);
+    issue(c, la, ha);
+    for (;;) {  // unrolled by two: the buffers trade places without copies
+        if (!__builtin_amdgcn_ballot_w64(c.idx < end)) break;
+        const RunState n1 = advance(c);
+        issue(n1, lb, hb);
+        process(c, la, ha);
+        if (!__builtin_amdgcn_ballot_w64(n1.idx < end)) break;
+        const RunState n2 = advance(n1);
+        issue(n2, la, ha);
+        process(n1, lb, hb);
+        c = n2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kRunPer; ++k) {
+        const uint32_t r = 64 * k + lane;
+        if (r < cnt) p.out[base + r] = s.hash[r];
+    }
+}
+#endif  // HALO_XXH3_PIPE
 
 // ---- the run kernel on 8-lane groups (HALO_XXH3_G8) -------------------------------------------
 // The same window / run / iteration scheme with 8 groups of 8 lanes: lanes j and j + 4 of a group
@@ -1079,6 +1293,8 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
     p.win = win;
 #if HALO_XXH3_G8
     hipLaunchKernelGGL(halo::xxh3_run8_kernel, dim3((n + win - 1) / win), dim3(64), 0, s, p);
+#elif HALO_XXH3_PIPE
+    hipLaunchKernelGGL(halo::xxh3_runp_kernel, dim3((n + win - 1) / win), dim3(64), 0, s, p);
 #else
     hipLaunchKernelGGL(halo::xxh3_run_kernel, dim3((n + win - 1) / win), dim3(64), 0, s, p);
 #endif
