@@ -283,6 +283,8 @@ def bench_lib():
         L.halo_bench_route_steps.argtypes = [i32, vp, vp, u32, vp] + tail
         L.halo_bench_xxh3_steps.restype = ctypes.c_int
         L.halo_bench_xxh3_steps.argtypes = [i32, vp, vp, vp, u32, vp] + tail
+        L.halo_bench_xxh3_probe_steps.restype = ctypes.c_int
+        L.halo_bench_xxh3_probe_steps.argtypes = [i32, vp, vp, vp, u32, vp] + tail
         u64 = ctypes.c_uint64
         L.halo_bench_read_peak.restype = ctypes.c_int
         L.halo_bench_read_peak.argtypes = [vp, u64, vp] + tail
@@ -698,6 +700,13 @@ def xxh3_secondary(dev, steps, warmup, d: Dist, with_cpu: bool = False):
     res = {"strings": n, "mstrings_per_s": round(n * steps / w / 1e6, 1),
            "gbytes_per_s": round(bs[0][3] * steps / w / 1e9, 1), "kernel_ms": round(k, 4),
            "roofline": roofline(alg, k, load_traffic("xxh3_kcp_1M")), "alg_bytes_per_launch": alg}
+    # the same kernel's loads, windows, runs and control flow with the hashing replaced by XORs
+    # (flow_hash.hip built as HALO_XXH3_PROBE into tools/libhalo_bench.so): its access-pattern floor
+    _, kp = time_native(bench_lib().halo_bench_xxh3_probe_steps, len(bs), arr([b[0].data_ptr() for b in bs]),
+                        arr([b[1].data_ptr() for b in bs]), arr([b[2].data_ptr() for b in bs]), n, h.data_ptr(),
+                        steps=steps, warmup=warmup, d=d)
+    res["roofline"]["load_pattern_probe_ms"] = round(kp, 5)
+    res["roofline"]["frac_of_load_pattern_probe"] = round(kp / k, 4)
     if with_cpu:
         from oracle import oracle as O
 

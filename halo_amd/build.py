@@ -68,7 +68,10 @@ def build_bench(force: bool = False, verbose: bool = False) -> str:
             os.path.getmtime(BENCH_SRC), os.path.getmtime(lib)):
         return BENCH_OUT
     cmd = [_hipcc(), "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
-           "-I" + os.path.join(ROOT, "include"), BENCH_SRC, "-L" + os.path.dirname(OUT), "-lhalo_rx",
+           "-I" + os.path.join(ROOT, "include"), BENCH_SRC,
+           # the XXH3 line's load-pattern probe: flow_hash.hip's run kernel without the hashing
+           os.path.join(CSRC, "flow_hash.hip"), "-DHALO_XXH3_PROBE=1", "-DHALO_XXH3_PROBE_ENTRY=1",
+           "-I" + CSRC, "-L" + os.path.dirname(OUT), "-lhalo_rx",
            "-Wl,-rpath,$ORIGIN/../halo_amd/lib", "-o", BENCH_OUT + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)

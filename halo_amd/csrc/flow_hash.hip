@@ -1261,6 +1261,23 @@ uint32_t blocks_for(uint64_t threads) {
 }  // namespace
 }  // namespace halo
 
+#if HALO_XXH3_PROBE_ENTRY
+// The XXH3 line's load-pattern probe (measurement tooling): tools/libhalo_bench.so compiles this
+// file a second time with HALO_XXH3_PROBE=1 HALO_XXH3_PROBE_ENTRY=1, and this entry — nothing of the
+// product's — launches the run kernel with its hashing replaced by XORs (the same windows, runs,
+// loads and control flow; the hashes it writes are not XXH3).
+extern "C" __attribute__((visibility("default"))) int halo_bench_xxh3_probe_launch(
+    const uint8_t* d_bytes, const uint64_t* d_offsets, const uint32_t* d_lens, uint32_t n, uint64_t* d_hash,
+    void* stream) {
+    static_assert(HALO_XXH3_PROBE && HALO_XXH3_RUNS, "the probe entry is the run kernel built as a probe");
+    if (n == 0 || !d_bytes || !d_offsets || !d_lens || !d_hash) return HALO_E_INVAL;
+    halo::XxhParams p{d_bytes, d_offsets, d_lens, n, d_hash};
+    p.win = halo::kRunWin;
+    hipLaunchKernelGGL(halo::xxh3_run_kernel, dim3((n + p.win - 1) / p.win), dim3(64), 0,
+                       static_cast<hipStream_t>(stream), p);
+    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+}
+#else
 extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const uint64_t* d_offsets,
                                                   const uint32_t* d_lens, uint32_t n, uint64_t* d_hash,
                                                   halo_stream_t stream) {
@@ -1339,3 +1356,4 @@ extern "C" HALO_API int halo_flow_hash_compact_device(const halo_rx_record16_t* 
                                                       uint32_t* d_bucket, halo_stream_t stream) {
     return flow_hash(d_records, true, n, kind, nat_type, d_hash, bucket_count, d_bucket, stream);
 }
+#endif  // HALO_XXH3_PROBE_ENTRY

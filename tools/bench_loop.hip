@@ -134,6 +134,20 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_xxh3_steps(
     return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
 }
 
+// flow_hash.hip built again as the XXH3 load-pattern probe (halo_amd/build.py build_bench)
+extern "C" int halo_bench_xxh3_probe_launch(const uint8_t* d_bytes, const uint64_t* d_offsets, const uint32_t* d_lens,
+                                            uint32_t n, uint64_t* d_hash, void* stream);
+extern "C" __attribute__((visibility("default"))) int halo_bench_xxh3_probe_steps(
+    int nbatch, const uint8_t* const* bytes, const uint64_t* const* offsets, const uint32_t* const* lens, uint32_t n,
+    uint64_t* hash, int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0) return HALO_E_INVAL;
+    auto launch = [&](int k) {
+        const int b = k % nbatch;
+        return halo_bench_xxh3_probe_launch(bytes[b], offsets[b], lens[b], n, hash, stream);
+    };
+    return timed_loop(launch, warmup, steps, static_cast<hipStream_t>(stream), region_ms, wall_s);
+}
+
 extern "C" __attribute__((visibility("default"))) int halo_bench_route_steps(
     int nbatch, const halo_route_table_t* t, const uint32_t* const* ips, uint32_t n, uint32_t* out, int warmup,
     int steps, void* stream, float* region_ms, double* wall_s) {
