@@ -295,6 +295,9 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
 #ifndef HALO_TXB_BIG_PATH
 #define HALO_TXB_BIG_PATH 1
 #endif
+#ifndef HALO_TXB_BIG_UNALIGNED  // body chunks as byte-unaligned 16-byte loads instead of aligned + v_alignbyte
+#define HALO_TXB_BIG_UNALIGNED 0
+#endif
 #ifndef HALO_TXB_NT_LD  // body payload loads non-temporal (read once)
 #define HALO_TXB_NT_LD 0
 #endif
@@ -311,8 +314,8 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
     const uint64_t P = f.pay - f.hdr_end;  // the source address of frame byte 0's position
     const uint32_t sh = (uint32_t)(P & 3u);
     const uint32_t cb_end = pay_end >> 4;  // chunks [4, cb_end): payload bytes only
-    typedef const __attribute__((address_space(1))) uint32_t gu32_t;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+    typedef const __attribute__((address_space(1), unused)) uint32_t gu32_t;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4), unused));
     uint32_t sum = 0;
     for (uint32_t c0 = 4 + j; c0 < cb_end; c0 += U * G) {
         uint32_t raw[U][5];
@@ -320,6 +323,13 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
         for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + u * G;
             if (c < cb_end) {
+#if HALO_TXB_BIG_UNALIGNED
+                // the chunk's 16 source bytes in one byte-unaligned load: no fifth dword, no merge
+                typedef uint32_t u32x4b __attribute__((ext_vector_type(4), aligned(1)));
+                const u32x4b v = *(const __attribute__((address_space(1))) u32x4b*)(P + 16ull * c);
+                raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
+                raw[u][4] = 0u;
+#else
                 gu32_t* q = (gu32_t*)((P + 16ull * c) & ~3ull);
 #if HALO_TXB_NT_LD
                 const u32x4 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)q);
@@ -328,6 +338,7 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
 #endif
                 raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
                 raw[u][4] = sh ? q[4] : 0u;
+#endif
             }
         }
 #pragma unroll
@@ -337,7 +348,7 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
             uint32_t w[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                w[i] = __builtin_amdgcn_alignbyte(raw[u][i + 1], raw[u][i], sh);
+                w[i] = HALO_TXB_BIG_UNALIGNED ? raw[u][i] : __builtin_amdgcn_alignbyte(raw[u][i + 1], raw[u][i], sh);
                 sum = hsum_acc(w[i], sum);
             }
 #if HALO_TXB_NT_ST

@@ -89,6 +89,7 @@ for s in "$@"; do
     thist) step pytest_hist 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_multi_batch.py -k "histogram or hist or multi" -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     abxb)  step ab_xxh3_bf 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_xxh3.py" ${AB_XB:-xxbf0 new} ;;
     abtp)  step ab_tx_pipe 900 bash tools/exp/ab_variants.sh "python tools/exp/bench_tx_build.py" ${AB_TP:-txpipe0 new} ;;
+    vtx)   step vtx 600 bash tools/exp/variant_tests.sh "tests/test_gpu_tx_build.py tests/test_gpu_loopback.py -m gpu" ${VT:-txbu} ;;
     vxx)   step vxx 600 bash tools/exp/variant_tests.sh "tests/test_gpu_flow_hash.py -m gpu" ${VX:-xxg8} ;;
     txlay) step tx_layout 600 python tools/exp/tx_layout_sweep.py ;;
     txx)   step pytest_xxh3 600 python -u -m pytest tests/test_gpu_flow_hash.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
