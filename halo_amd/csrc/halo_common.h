@@ -61,8 +61,9 @@ int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 // Partial status histograms of an rx launch (flush_hist, rx_parse.hip): kHistSlots level-1 slots
 // (one per block modulo kHistSlots) then kHistSlots / kHistFan level-2 slots, kHistStride 64-bit
 // words each (arrivals << 40 | count, one per status), zero between launches. One array per
-// (device, stream) the library has parsed on with a histogram, allocated at first use and kept:
-// launches on one stream run in order, so they can share it.
+// (device, stream) the library has parsed on with a histogram, allocated at first use and kept
+// for the life of the process (135 KB each; a caller cycling through many short-lived streams with
+// histograms on grows this set): launches on one stream run in order, so they can share it.
 constexpr uint32_t kHistSlots = 1024, kHistFan = 32, kHistStride = 16;
 constexpr uint32_t kHistWords = (kHistSlots + kHistSlots / kHistFan) * kHistStride;  // 64-bit words
 uint32_t* hist_slots(hipStream_t s);  // nullptr: allocation failed
