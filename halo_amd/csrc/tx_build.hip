@@ -295,6 +295,9 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
 #ifndef HALO_TXB_BIG_PATH
 #define HALO_TXB_BIG_PATH 1
 #endif
+#ifndef HALO_TXB_BIG_NB  // a chunk's fifth source dword from the neighbour lane (ds_bpermute)
+#define HALO_TXB_BIG_NB 1
+#endif
 #ifndef HALO_TXB_BIG_UNALIGNED  // body chunks as byte-unaligned 16-byte loads instead of aligned + v_alignbyte
 #define HALO_TXB_BIG_UNALIGNED 0
 #endif
@@ -318,7 +321,7 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4), unused));
     uint32_t sum = 0;
     for (uint32_t c0 = 4 + j; c0 < cb_end; c0 += U * G) {
-        uint32_t raw[U][5];
+        uint32_t raw[U][5] = {};  // (a row past cb_end is offered to the neighbour lane, never used)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + u * G;
@@ -337,10 +340,32 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
                 const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)q;
 #endif
                 raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
+#if HALO_TXB_BIG_NB
+                // only a chunk whose successor no lane of this round loaded fetches its fifth dword
+                raw[u][4] = (sh && (c + 1 == cb_end || (j == G - 1 && u == U - 1))) ? q[4] : 0u;
+#else
                 raw[u][4] = sh ? q[4] : 0u;
+#endif
 #endif
             }
         }
+#if HALO_TXB_BIG_NB && !HALO_TXB_BIG_UNALIGNED
+        // The fifth dword of chunk c is the first dword of chunk c + 1, which lane j + 1 loaded in
+        // the same row (lane G - 1: lane 0's next row): one ds_bpermute per row instead of a
+        // second global load per chunk. Lane 0 offers its next row's first dword (only lane G - 1
+        // asks lane 0), every other lane its own row's.
+        {
+            const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+            const int src = 4 * (int)(j < G - 1 ? lane + 1 : lane & ~(uint32_t)(G - 1));
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t offer = (j == 0 && u + 1 < U) ? raw[u + 1 < U ? u + 1 : u][0] : raw[u][0];
+                const uint32_t nb = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)offer);
+                const uint32_t c = c0 + u * G;
+                if (!(c + 1 == cb_end || (j == G - 1 && u == U - 1))) raw[u][4] = nb;
+            }
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + u * G;
