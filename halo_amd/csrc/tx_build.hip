@@ -295,6 +295,9 @@ __device__ __forceinline__ void build_frame(const BuildParams& p, const Frame& f
 #ifndef HALO_TXB_BIG_PATH
 #define HALO_TXB_BIG_PATH 1
 #endif
+#ifndef HALO_TXB_HEAD_EARLY  // build_big: the head / tail chunk loads issued with the body's
+#define HALO_TXB_HEAD_EARLY 0  // neutral: 0.194 / 0.195 against 0.190 / 0.195 ms (profiles/r04/r4z)
+#endif
 #ifndef HALO_TXB_BIG_NB  // a chunk's fifth source dword from the neighbour lane (ds_bpermute)
 #define HALO_TXB_BIG_NB 1
 #endif
@@ -320,6 +323,12 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
     typedef const __attribute__((address_space(1), unused)) uint32_t gu32_t;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4), unused));
     uint32_t sum = 0;
+    // the head / tail chunk of lanes 0..4 (masked path below): its loads go out with the body's,
+    // one memory round trip per frame instead of two (HALO_TXB_HEAD_EARLY)
+    const uint32_t c = j < 4 ? j : cb_end;
+    const bool mine = j < 4 ? 4 * j < ndw : (j == 4 && cb_end >= 4 && 4 * cb_end < ndw);
+    uint32_t hraw[5] = {0u, 0u, 0u, 0u, 0u};
+    if (HALO_TXB_HEAD_EARLY && mine && chunk_has_payload(f, c, ndw)) payload_raw(f, c, hraw);
     for (uint32_t c0 = 4 + j; c0 < cb_end; c0 += U * G) {
         uint32_t raw[U][5] = {};  // (a row past cb_end is offered to the neighbour lane, never used)
 #pragma unroll
@@ -384,12 +393,10 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
 #endif
         }
     }
-    const uint32_t c = j < 4 ? j : cb_end;
-    const bool mine = j < 4 ? 4 * j < ndw : (j == 4 && cb_end >= 4 && 4 * cb_end < ndw);
     uint32_t w[4] = {0u, 0u, 0u, 0u};
     if (mine) {
-        uint32_t raw[5] = {0u, 0u, 0u, 0u, 0u};
-        if (chunk_has_payload(f, c, ndw)) payload_raw(f, c, raw);
+        uint32_t* raw = hraw;
+        if (!HALO_TXB_HEAD_EARLY && chunk_has_payload(f, c, ndw)) payload_raw(f, c, hraw);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t k = 4 * c + i;
@@ -1092,6 +1099,21 @@ __global__ void __launch_bounds__(kBlock) tx_build_pair_kernel(const BuildParams
     if (2ull * pair >= p.n) return;  // wave-uniform
     const uint32_t g = lane >> 5, j = lane & 31u;
     const uint32_t i = 2 * pair + g, t = (2 * pair) / kTile, il = t * kTile + lane;
+    const uint32_t base_id = *p.ip_id;
+    // this group's descriptor first: its loads go out with the tile's verdict loads below
+    uint32_t d[10];
+    if (i < p.n) {
+        const uint2* src = reinterpret_cast<const uint2*>(p.desc + i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint2 v = src[k];
+            d[2 * k] = v.x;
+            d[2 * k + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) d[k] = 0u;
+    }
     uint32_t d2 = 0, d9 = 0, flen_l = 0;
     if (il < p.n) {
         const uint32_t* dw = reinterpret_cast<const uint32_t*>(p.desc + il);
@@ -1108,20 +1130,7 @@ __global__ void __launch_bounds__(kBlock) tx_build_pair_kernel(const BuildParams
     const uint32_t code = (uint32_t)__shfl((int)code_l, (int)fl, 64), flen = (uint32_t)__shfl((int)flen_l, (int)fl, 64);
     const uint32_t before = (uint32_t)__popcll(bal & ((1ull << fl) - 1ull));
     const bool build = i < p.n && code == HALO_TX_B_OK;
-    const uint32_t id = (*p.ip_id + 1u + i - before) & 0xFFFFu;  // iphId++ then use (ipv4.go:103-104)
-    uint32_t d[10];
-    if (i < p.n) {
-        const uint2* src = reinterpret_cast<const uint2*>(p.desc + i);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const uint2 v = src[k];
-            d[2 * k] = v.x;
-            d[2 * k + 1] = v.y;
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 10; ++k) d[k] = 0u;
-    }
+    const uint32_t id = (base_id + 1u + i - before) & 0xFFFFu;  // iphId++ then use (ipv4.go:103-104)
     const Frame f = decode(d, p.payload);
     if (j == 0 && build) {  // the frame's header dwords 0..15 (Ethernet layout, or the loopback bytes)
         uint32_t e[18];
