@@ -639,6 +639,11 @@ def flow_hash_secondary(batches, out_records, netif, steps, warmup, d: Dist, wit
                               "alg_bytes_per_launch": algc,
                               "what": "the same keys from HALO_RX_RECORD_COMPACT records (16 B: the key fields only)"}
     del crecs
+    # size-matched probes: the bytes the memory system must move (whole 32 B / 16 B records in,
+    # hash + bucket out), streamed with no work, over as many rotating buffers
+    with_probe(res["roofline"], size_matched_probe(dev_of(out_records), n * 32, n * 12, d, nbuf=len(batches)), k)
+    with_probe(res["compact_records"]["roofline"],
+               size_matched_probe(dev_of(out_records), n * 16, n * 12, d, nbuf=len(batches)), kc)
     if with_cpu:
         from oracle import oracle as O
 
@@ -1094,6 +1099,10 @@ def size_matched_probe(dev, read_bytes: int, write_bytes: int, d: Dist, nbuf: in
     del srcs, dsts, sink
     torch.cuda.empty_cache()
     return k
+
+
+def dev_of(t):
+    return t.device
 
 
 def with_probe(r: dict, probe_ms: float, kernel_ms: float) -> dict:
