@@ -856,366 +856,10 @@ __global__ void __launch_bounds__(64) xxh3_run_kernel(const XxhParams p) {
 }
 #endif  // HALO_XXH3_RUNS
 
-// ---- the run kernel, software-pipelined (HALO_XXH3_PIPE) -----------------------------------
-// The branch-free run kernel with step k + 1's loads issued before step k's arithmetic: the next
-// step of a group is known before its data arrives (the same long string B stripes on, or the next
-// string of the run), so a wave keeps two steps' loads in flight. With 4096 waves for 1M strings
-// the grid is 4 waves per SIMD whatever the kernel's VGPRs, so the second buffer costs no occupancy
-// up to 128 VGPRs.
-#ifndef HALO_XXH3_PIPE
-#define HALO_XXH3_PIPE 0
-#endif
-#if HALO_XXH3_PIPE && HALO_XXH3_RUNS
-struct RunState {
-    const uint8_t* d;
-    uint32_t idx, len, T, nb, st;
-};
-#ifndef HALO_XXH3_PIPE_WAVES
-#define HALO_XXH3_PIPE_WAVES 4
-#endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HALO_XXH3_PIPE_WAVES)))
-xxh3_runp_kernel(const XxhParams p) {
-    __shared__ LongSecrets sec;
-    __shared__ RunLds s;
-    load_secrets(sec);
-    const uint32_t lane = threadIdx.x;
-    const uint32_t base = blockIdx.x * p.win;
-    const uint32_t cnt = p.n - base < p.win ? p.n - base : p.win;
-    uint32_t total = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kRunPer; ++k) {
-        const uint32_t r = 64 * k + lane;
-        const bool in = r < cnt;
-        const uint32_t len = in ? p.lens[base + r] : 0u;
-        s.len[r] = len;
-        s.off[r] = in ? p.offsets[base + r] : 0ull;
-        const uint32_t w = in ? run_cost(len) : 0u;
-        uint32_t incl = w;
-#pragma unroll
-        for (int dd = 1; dd < 64; dd <<= 1) {
-            const uint32_t o = __shfl_up(incl, dd, 64);
-            if (lane >= (uint32_t)dd) incl += o;
-        }
-        s.pref[r] = total + incl - w;
-        total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    }
-    __syncthreads();
-    const uint32_t g = lane >> 2, j = lane & 3u;
-    auto first_at = [&](uint32_t t) {
-        uint32_t lo = 0, hi = cnt;
-        while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            if (s.pref[m] < t) lo = m + 1;
-            else hi = m;
-        }
-        return lo;
-    };
-    const uint32_t idx0 = first_at((uint32_t)(((uint64_t)g * total + 15) / 16));
-    const uint32_t end = g == 15 ? cnt : first_at((uint32_t)(((uint64_t)(g + 1) * total + 15) / 16));
-    constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
-    const uint64_t init0 = j == 0 ? kInit[0] : j == 1 ? kInit[2] : j == 2 ? kInit[4] : kInit[6];
-    const uint64_t init1 = j == 0 ? kInit[1] : j == 1 ? kInit[3] : j == 2 ? kInit[5] : kInit[7];
-    auto state_at = [&](uint32_t i) {
-        RunState r;
-        r.idx = i;
-        r.st = 0;
-        r.len = i < end ? s.len[i] : 0u;
-        r.d = p.bytes + (i < end ? s.off[i] : 0ull);
-        r.T = r.len > 240 ? (r.len - 1) / 64 : 0u;
-        r.nb = r.len > 240 ? (r.len - 1) / 1024 : 0u;
-        return r;
-    };
-    auto advance = [&](const RunState& c) {  // the step after c
-        if (c.idx < end && c.len > 240 && c.st + kRunB <= c.T) {
-            RunState r = c;
-            r.st += kRunB;
-            return r;
-        }
-        return state_at(c.idx < end ? c.idx + 1 : end);
-    };
-    auto issue = [&](const RunState& c, uint64_t (&lo)[kRunB], uint64_t (&hi)[kRunB]) {
-        const bool act = c.idx < end;
-        const bool lng = act && c.len > 240, mid = act && c.len > 16 && c.len <= 240;
-        const bool large = c.len > 128;
-        const uint32_t lv = c.len > 96 ? 4u : c.len > 64 ? 3u : c.len > 32 ? 2u : 1u;
-        const uint32_t nmid = large ? ((c.len & ~15u) - 128) / 16 : 0u;
-#pragma unroll
-        for (uint32_t u = 0; u < kRunB; ++u) {
-            const uint8_t* a = c.d;
-            bool v = false;
-            if (lng) {
-                const uint32_t x = c.st + u;
-                v = x <= c.T;
-                a = x < c.T ? c.d + 64 * x + 16 * j : c.d + c.len - 64 + 16 * j;
-            } else if (u >= 4) {
-            } else if (mid && !large) {
-                v = u < 2 && j < lv;
-                a = u == 0 ? c.d + 16 * j : c.d + c.len - 16 - 16 * j;
-            } else if (mid) {
-                const uint32_t t = 2 * j + (u & 1u);
-                v = u < 2 || t <= nmid;
-                a = u < 2 ? c.d + 16 * t : t < nmid ? c.d + 128 + 16 * t : c.d + c.len - 16;
-            }
-            ld128u(v ? a : g_xxh3_pad, lo[u], hi[u]);
-        }
-    };
-    uint64_t a0 = init0, a1 = init1;
-    auto process = [&](const RunState& c, const uint64_t (&lo)[kRunB], const uint64_t (&hi)[kRunB]) {
-        const bool act = c.idx < end;
-        const bool lng = act && c.len > 240, mid = act && c.len > 16 && c.len <= 240, sml = act && c.len <= 16;
-        const bool large = c.len > 128;
-        const uint32_t lv = c.len > 96 ? 4u : c.len > 64 ? 3u : c.len > 32 ? 2u : 1u;
-        const uint32_t nmid = large ? ((c.len & ~15u) - 128) / 16 : 0u;
-        uint64_t h = 0;
-        bool have = false;
-        if (lng) {
-#pragma unroll
-            for (uint32_t u = 0; u < kRunB; ++u) {
-                const uint32_t x = c.st + u;
-                const uint64_t s0 = x < c.T ? sec.w8[(x & 15u) + 2 * j] : sec.last[2 * j];
-                const uint64_t s1 = x < c.T ? sec.w8[(x & 15u) + 2 * j + 1] : sec.last[2 * j + 1];
-                const uint64_t k0 = lo[u] ^ s0, k1 = hi[u] ^ s1;
-                const uint64_t t0 = hi[u] + (uint64_t)(uint32_t)k0 * (k0 >> 32);
-                const uint64_t t1 = lo[u] + (uint64_t)(uint32_t)k1 * (k1 >> 32);
-                a0 += x <= c.T ? t0 : 0ull;
-                a1 += x <= c.T ? t1 : 0ull;
-            }
-            const uint32_t st = c.st + kRunB;
-            if ((st & 15u) == 0 && (st >> 4) <= c.nb) {  // a full block ended: scramble (xxh3.go:212-218)
-                a0 ^= a0 >> 47;
-                a1 ^= a1 >> 47;
-                a0 ^= sec.w8[16 + 2 * j];
-                a1 ^= sec.w8[17 + 2 * j];
-                a0 *= P32_1;
-                a1 *= P32_1;
-            }
-            if (st > c.T) {  // merge (xxh3.go:139-145)
-                const uint64_t m = quad_sum(mul_fold64(a0 ^ sec.merge[2 * j], a1 ^ sec.merge[2 * j + 1]));
-                h = avalanche((uint64_t)c.len * P64_1 + m);
-                have = true;
-            }
-        }
-        if (mid) {
-            uint64_t t01 = 0, t23 = 0;
-            if (!large) {
-                if (j < lv)
-                    t01 = mul_fold64(lo[0] ^ sec.w8[4 * j], hi[0] ^ sec.w8[4 * j + 1]) +
-                          mul_fold64(lo[1] ^ sec.w8[4 * j + 2], hi[1] ^ sec.w8[4 * j + 3]);
-                h = avalanche((uint64_t)c.len * P64_1 + quad_sum(t01));
-            } else {
-                t01 = mul_fold64(lo[0] ^ sec.w8[4 * j], hi[0] ^ sec.w8[4 * j + 1]) +
-                      mul_fold64(lo[1] ^ sec.w8[4 * j + 2], hi[1] ^ sec.w8[4 * j + 3]);
-                const uint64_t acc = avalanche((uint64_t)c.len * P64_1 + quad_sum(t01));
-#pragma unroll
-                for (uint32_t u = 2; u < 4; ++u) {
-                    const uint32_t t = 2 * j + (u & 1u);
-                    if (t < nmid) t23 += mul_fold64(lo[u] ^ sec.mid3[2 * t], hi[u] ^ sec.mid3[2 * t + 1]);
-                    else if (t == nmid) t23 += mul_fold64(lo[u] ^ sec.mlast[0], hi[u] ^ sec.mlast[1]);
-                }
-                h = avalanche(acc + quad_sum(t23));
-            }
-            have = true;
-        }
-        if (sml) {
-            h = hash_upto16(c.d, c.len);
-            have = true;
-        }
-        if (have) {
-            if (j == 0) s.hash[c.idx] = h;
-            a0 = init0;
-            a1 = init1;
-        }
-    };
-    uint64_t la[kRunB], ha[kRunB], lb[kRunB], hb[kRunB];
-    RunState c = state_at(idx0);
-    issue(c, la, ha);
-    for (;;) {  // unrolled by two: the buffers trade places without copies
-        if (!__builtin_amdgcn_ballot_w64(c.idx < end)) break;
-        const RunState n1 = advance(c);
-        issue(n1, lb, hb);
-        process(c, la, ha);
-        if (!__builtin_amdgcn_ballot_w64(n1.idx < end)) break;
-        const RunState n2 = advance(n1);
-        issue(n2, la, ha);
-        process(n1, lb, hb);
-        c = n2;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < kRunPer; ++k) {
-        const uint32_t r = 64 * k + lane;
-        if (r < cnt) p.out[base + r] = s.hash[r];
-    }
-}
-#endif  // HALO_XXH3_PIPE
+// Tried and removed (round 4; in git history up to commit 68eed30): the run kernel
+// on 8 groups of 8 lanes (128 contiguous bytes per string per load instruction) and a software-
+// pipelined run kernel (step k + 1's loads before step k's arithmetic). Both bit-exact, both slower.
 
-// ---- the run kernel on 8-lane groups (HALO_XXH3_G8) -------------------------------------------
-// The same window / run / iteration scheme with 8 groups of 8 lanes: lanes j and j + 4 of a group
-// take the two stripes of a 128-byte pair (j & 3 = the accumulator pair, as in the 4-lane form), so
-// a load instruction reads 128 contiguous bytes per string instead of 64 — a byte-unaligned 128-byte
-// span meets three 64-byte sectors where two 64-byte spans meet four. Each half keeps partial
-// accumulators (the low half starts from the initial values, the high half from 0; the sums commute
-// within a block), and the halves are added (a 4-lane xor shuffle) before each scramble and the
-// merge. An iteration is one 16-stripe block: eight 16-byte loads per lane; hashMedium's pair terms
-// and hashLarge's first-eight / middle terms take one lane each (hash_mid8's split).
-#ifndef HALO_XXH3_G8
-#define HALO_XXH3_G8 0
-#endif
-#if HALO_XXH3_G8
-__device__ __forceinline__ uint32_t run_cost8(uint32_t len) {
-    return len > 240 ? (len - 1) / 1024 + 1 : 1u;  // one iteration per 16-stripe block (the last partial)
-}
-__device__ __forceinline__ uint64_t xor4(uint64_t v) {  // the value of lane ^ 4
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, 4, 64);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), 4, 64);
-    return join64(lo, hi);
-}
-__global__ void __launch_bounds__(64) xxh3_run8_kernel(const XxhParams p) {
-    __shared__ LongSecrets sec;
-    __shared__ RunLds s;
-    load_secrets(sec);
-    const uint32_t lane = threadIdx.x;
-    const uint32_t base = blockIdx.x * p.win;
-    const uint32_t cnt = p.n - base < p.win ? p.n - base : p.win;
-    uint32_t total = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kRunPer; ++k) {
-        const uint32_t r = 64 * k + lane;
-        const bool in = r < cnt;
-        const uint32_t len = in ? p.lens[base + r] : 0u;
-        s.len[r] = len;
-        s.off[r] = in ? p.offsets[base + r] : 0ull;
-        const uint32_t w = in ? run_cost8(len) : 0u;
-        uint32_t incl = w;
-#pragma unroll
-        for (int dd = 1; dd < 64; dd <<= 1) {
-            const uint32_t o = __shfl_up(incl, dd, 64);
-            if (lane >= (uint32_t)dd) incl += o;
-        }
-        s.pref[r] = total + incl - w;
-        total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    }
-    __syncthreads();
-    const uint32_t g = lane >> 3, j = lane & 7u, q = j & 3u, hf = j >> 2;
-    auto first_at = [&](uint32_t t) {
-        uint32_t lo = 0, hi = cnt;
-        while (lo < hi) {
-            const uint32_t m = (lo + hi) >> 1;
-            if (s.pref[m] < t) lo = m + 1;
-            else hi = m;
-        }
-        return lo;
-    };
-    uint32_t idx = first_at((uint32_t)(((uint64_t)g * total + 7) / 8));
-    const uint32_t end = g == 7 ? cnt : first_at((uint32_t)(((uint64_t)(g + 1) * total + 7) / 8));
-    constexpr uint64_t kInit[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
-    const uint64_t init0 = hf ? 0ull : q == 0 ? kInit[0] : q == 1 ? kInit[2] : q == 2 ? kInit[4] : kInit[6];
-    const uint64_t init1 = hf ? 0ull : q == 0 ? kInit[1] : q == 1 ? kInit[3] : q == 2 ? kInit[5] : kInit[7];
-    uint32_t len = 0, T = 0, nb = 0, st = 0;
-    const uint8_t* d = p.bytes;
-    uint64_t a0 = init0, a1 = init1;
-    auto begin = [&]() {
-        len = s.len[idx];
-        d = p.bytes + s.off[idx];
-        T = len > 240 ? (len - 1) / 64 : 0u;
-        nb = len > 240 ? (len - 1) / 1024 : 0u;
-        st = 0;
-        a0 = init0;
-        a1 = init1;
-    };
-    if (idx < end) begin();
-    for (;;) {
-        const bool act = idx < end;
-        if (!__builtin_amdgcn_ballot_w64(act)) break;
-        const bool lng = act && len > 240, mid = act && len > 16 && len <= 240, sml = act && len <= 16;
-        const bool large = len > 128;
-        const uint32_t lv = len > 96 ? 4u : len > 64 ? 3u : len > 32 ? 2u : 1u;  // hashMedium's pairs
-        const uint32_t nmid = large ? ((len & ~15u) - 128) / 16 : 0u;           // hashLarge's middle terms
-        const uint32_t mk = j >> 1, side = j & 1u;                              // hashMedium: pair, end
-        uint64_t lo[8], hi[8];
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u) {
-            const uint8_t* a = d;
-            bool v = false;
-            if (lng) {
-                const uint32_t x = st + 2 * u + hf;
-                v = x <= T;
-                a = x < T ? d + 64 * x + 16 * q : d + len - 64 + 16 * q;
-            } else if (u >= 2) {
-            } else if (mid && !large) {
-                v = u == 0 && mk < lv;
-                a = side ? d + len - 16 - 16 * mk : d + 16 * mk;
-            } else if (mid) {
-                v = u == 0 || j <= nmid;
-                a = u == 0 ? d + 16 * j : j < nmid ? d + 128 + 16 * j : d + len - 16;
-            }
-            ld128u(v ? a : g_xxh3_pad, lo[u], hi[u]);
-        }
-        uint64_t h = 0;
-        bool have = false;
-        if (lng) {
-#pragma unroll
-            for (uint32_t u = 0; u < 8; ++u) {
-                const uint32_t x = st + 2 * u + hf;
-                const uint64_t s0 = x < T ? sec.w8[(x & 15u) + 2 * q] : sec.last[2 * q];
-                const uint64_t s1 = x < T ? sec.w8[(x & 15u) + 2 * q + 1] : sec.last[2 * q + 1];
-                const uint64_t k0 = lo[u] ^ s0, k1 = hi[u] ^ s1;
-                const uint64_t t0 = hi[u] + (uint64_t)(uint32_t)k0 * (k0 >> 32);
-                const uint64_t t1 = lo[u] + (uint64_t)(uint32_t)k1 * (k1 >> 32);
-                a0 += x <= T ? t0 : 0ull;
-                a1 += x <= T ? t1 : 0ull;
-            }
-            st += 16;
-            if ((st >> 4) <= nb) {  // a full block ended: both halves' sums, scramble (xxh3.go:212-218)
-                a0 += xor4(a0);
-                a1 += xor4(a1);
-                a0 ^= a0 >> 47;
-                a1 ^= a1 >> 47;
-                a0 ^= sec.w8[16 + 2 * q];
-                a1 ^= sec.w8[17 + 2 * q];
-                a0 *= P32_1;
-                a1 *= P32_1;
-                if (hf) a0 = a1 = 0ull;
-            } else {  // the last block: merge (xxh3.go:139-145) over the quad of each half
-                a0 += xor4(a0);
-                a1 += xor4(a1);
-                const uint64_t m = quad_sum(mul_fold64(a0 ^ sec.merge[2 * q], a1 ^ sec.merge[2 * q + 1]));
-                h = avalanche((uint64_t)len * P64_1 + m);
-                have = true;
-            }
-        }
-        if (mid) {
-            if (!large) {  // hashMedium: lane j = end `side` of pair mk, secret 32 mk + 16 side
-                const uint64_t t = mk < lv ? mul_fold64(lo[0] ^ sec.w8[4 * mk + 2 * side],
-                                                        hi[0] ^ sec.w8[4 * mk + 2 * side + 1]) : 0ull;
-                h = avalanche((uint64_t)len * P64_1 + sum8(t));
-            } else {       // hashLarge: term j of the first eight, then middle term j or the last
-                const uint64_t acc = avalanche((uint64_t)len * P64_1 +
-                                               sum8(mul_fold64(lo[0] ^ sec.w8[2 * j], hi[0] ^ sec.w8[2 * j + 1])));
-                const uint64_t t = j < nmid ? mul_fold64(lo[1] ^ sec.mid3[2 * j], hi[1] ^ sec.mid3[2 * j + 1])
-                                 : j == nmid ? mul_fold64(lo[1] ^ sec.mlast[0], hi[1] ^ sec.mlast[1]) : 0ull;
-                h = avalanche(acc + sum8(t));
-            }
-            have = true;
-        }
-        if (sml) {
-            h = hash_upto16(d, len);
-            have = true;
-        }
-        if (have) {
-            if (j == 0) s.hash[idx] = h;
-            ++idx;
-            if (idx < end) begin();
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < kRunPer; ++k) {
-        const uint32_t r = 64 * k + lane;
-        if (r < cnt) p.out[base + r] = s.hash[r];
-    }
-}
-#endif  // HALO_XXH3_G8
 
 // ---- NAT flow keys from parsed records ------------------------------------------------------
 struct FlowParams {
@@ -1308,13 +952,7 @@ extern "C" HALO_API int halo_xxh3_64_batch_device(const uint8_t* d_bytes, const 
         win = win < 64u ? 64u : win > halo::kRunWin ? halo::kRunWin : win;
     }
     p.win = win;
-#if HALO_XXH3_G8
-    hipLaunchKernelGGL(halo::xxh3_run8_kernel, dim3((n + win - 1) / win), dim3(64), 0, s, p);
-#elif HALO_XXH3_PIPE
-    hipLaunchKernelGGL(halo::xxh3_runp_kernel, dim3((n + win - 1) / win), dim3(64), 0, s, p);
-#else
     hipLaunchKernelGGL(halo::xxh3_run_kernel, dim3((n + win - 1) / win), dim3(64), 0, s, p);
-#endif
 #else
     constexpr uint32_t wpb = HALO_XXH3_LONG_BLOCK / 64;
     const uint32_t long_blocks = (uint32_t)(((uint64_t)halo::blocks_for(n) * 4 + wpb - 1) / wpb);

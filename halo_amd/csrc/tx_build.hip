@@ -439,311 +439,9 @@ __device__ __forceinline__ void build_big(const BuildParams& p, const Frame& f, 
     }
 }
 
-// build_big split in two for software pipelining across the steps of a tile (HALO_TXB_PIPE, the
-// default): a wave of 16- or 32-lane groups builds 64 / G frames per step, and every step was one
-// dependent round trip (load the frames' bytes, wait, merge, store), so a wave had at most one
-// step's bytes in flight — 3 KB for 1514 B frames — and 4 waves per SIMD kept ~12 MB in flight on
-// the chip, short of what 8 TB/s needs at loaded HBM latency (r4e: 0.74 of the size-matched
-// probe, 65 % of wave cycles waiting). big_load issues step k + 1's loads (the first round of
-// body chunks and the lane's head / tail chunk) before big_finish waits for step k's.
-#ifndef HALO_TXB_UNALIGNED
-#define HALO_TXB_UNALIGNED 1
-#endif
-template <int U>
-struct BigLoad {
-    uint32_t raw[U][HALO_TXB_UNALIGNED ? 4 : 5];
-    uint32_t head[5];
-};
-
-template <int G, int U>
-__device__ __forceinline__ void big_load(const Frame& f, uint32_t j, BigLoad<U>& b) {
-    const uint32_t pay_end = f.hdr_end + f.plen, ndw = (f.flen + 3u) >> 2;
-    const uint64_t P = f.pay - f.hdr_end;
-    const uint32_t sh = (uint32_t)(P & 3u), cb_end = pay_end >> 4;
-    typedef const __attribute__((address_space(1), unused)) uint32_t gu32_t;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4), unused));
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t c = 4 + j + u * G;
-        if (c < cb_end) {
-#if HALO_TXB_UNALIGNED
-            // the chunk's 16 source bytes in one unaligned load (gfx9 global loads take any byte
-            // address; all 16 are payload bytes): no fifth dword, no v_alignbyte
-            typedef uint32_t u32x4b __attribute__((ext_vector_type(4), aligned(1)));
-            const u32x4b v = *(const __attribute__((address_space(1))) u32x4b*)(P + 16ull * c);
-            b.raw[u][0] = v.x; b.raw[u][1] = v.y; b.raw[u][2] = v.z; b.raw[u][3] = v.w;
-            (void)sh;
-#else
-            gu32_t* q = (gu32_t*)((P + 16ull * c) & ~3ull);
-            const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)q;
-            b.raw[u][0] = v.x; b.raw[u][1] = v.y; b.raw[u][2] = v.z; b.raw[u][3] = v.w;
-            b.raw[u][4] = sh ? q[4] : 0u;
-#endif
-        }
-    }
-    const uint32_t c = j < 4 ? j : cb_end;
-    const bool mine = j < 4 ? 4 * j < ndw : (j == 4 && cb_end >= 4 && 4 * cb_end < ndw);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) b.head[i] = 0u;
-    if (mine && chunk_has_payload(f, c, ndw)) payload_raw(f, c, b.head);
-}
-
-template <int G, int U>
-__device__ __forceinline__ void big_finish(const BuildParams& p, const Frame& f, const uint32_t* hdr, uint32_t j,
-                                           uint8_t* out, const BigLoad<U>& b) {
-    const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
-    const uint32_t l4s = f.base + 20u, pay_end = f.hdr_end + f.plen;
-    const uint32_t ndw = (f.flen + 3u) >> 2;
-    const uint64_t P = f.pay - f.hdr_end;
-    const uint32_t sh = (uint32_t)(P & 3u);
-    const uint32_t cb_end = pay_end >> 4;
-    typedef const __attribute__((address_space(1), unused)) uint32_t gu32_t;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4), unused));
-    uint32_t sum = 0;
-    auto body = [&](uint32_t c, const uint32_t (&r)[HALO_TXB_UNALIGNED ? 4 : 5]) {
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            w[i] = HALO_TXB_UNALIGNED ? r[i] : __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
-            sum = hsum_acc(w[i], sum);
-        }
-        *reinterpret_cast<uint4*>(out + 16ull * c) = make_uint4(w[0], w[1], w[2], w[3]);
-    };
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t c = 4 + j + u * G;
-        if (c < cb_end) body(c, b.raw[u]);
-    }
-    for (uint32_t c0 = 4 + j + U * G; c0 < cb_end; c0 += U * G) {  // frames longer than one round
-        uint32_t raw[U][HALO_TXB_UNALIGNED ? 4 : 5];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = c0 + u * G;
-            if (c < cb_end) {
-#if HALO_TXB_UNALIGNED
-                typedef uint32_t u32x4b __attribute__((ext_vector_type(4), aligned(1)));
-                const u32x4b v = *(const __attribute__((address_space(1))) u32x4b*)(P + 16ull * c);
-                raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
-#else
-                gu32_t* q = (gu32_t*)((P + 16ull * c) & ~3ull);
-                const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)q;
-                raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
-                raw[u][4] = sh ? q[4] : 0u;
-#endif
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (c0 + u * G < cb_end) body(c0 + u * G, raw[u]);
-    }
-    const uint32_t c = j < 4 ? j : cb_end;
-    const bool mine = j < 4 ? 4 * j < ndw : (j == 4 && cb_end >= 4 && 4 * cb_end < ndw);
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if (mine) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t k = 4 * c + i;
-            w[i] = __builtin_amdgcn_alignbyte(b.head[i + 1], b.head[i], sh) & byte_mask(k, f.hdr_end, pay_end);
-            if (k < 16) w[i] |= hdr[k] & byte_mask(k, 0, f.hdr_end);
-            sum = hsum_acc(w[i] & byte_mask(k, l4s, pay_end), sum);
-        }
-        if (j == 4) {
-            uint32_t* o = reinterpret_cast<uint32_t*>(out) + 4 * c;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (4 * c + i < ndw) o[i] = w[i];
-        }
-    }
-    uint32_t part = group_sum<G>(fold16(sum));
-    uint32_t ck_le = 0;
-    uint32_t ck_at;
-    if (f.proto == kIpUdp || f.proto == kIpTcp) {
-        const uint32_t s = bswap32(f.src), t = bswap32(f.dst);
-        part += hsum(s) + hsum(t) + (f.proto << 8) + bswap16(f.l4hdr + f.plen);
-        ck_at = f.base + 20u + (f.proto == kIpUdp ? 6u : 16u);
-    } else {
-        ck_at = f.base + 22u;
-    }
-    if (csum || f.proto == kIpIcmp) ck_le = (~fold16(part)) & 0xFFFFu;  // ICMP always (icmp.go:84-87)
-    if (mine && j < 4) {
-        const uint32_t ck_dw = ck_at >> 2, ck_sh = (ck_at & 2u) * 8u;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (4 * c + i == ck_dw) w[i] |= ck_le << ck_sh;
-        uint32_t* o = reinterpret_cast<uint32_t*>(out) + 4 * c;
-        if (4 * c + 4 <= ndw) {
-            *reinterpret_cast<uint4*>(o) = make_uint4(w[0], w[1], w[2], w[3]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (4 * c + i < ndw) o[i] = w[i];
-        }
-    }
-}
-#ifndef HALO_TXB_PIPE
-#define HALO_TXB_PIPE 0  // measured slower (profiles/r04/r4g/ab_tx_pipe.log)
-#endif
-#ifndef HALO_TXB_PIPE_WAVES  // occupancy floor of the pipelined build (two load buffers)
-#define HALO_TXB_PIPE_WAVES 3
-#endif
-
-// The tile-flat build of long frames (HALO_TXB_FLAT=1, an alternative for the 16- and 32-lane launches):
-// build_big still walks a tile's 64 frames G lanes at a time, 64 / G frames per step, and every
-// step pays a descriptor decode, the zone bounds, a G-lane reduction and the masked head for two
-// frames. Here every per-frame piece is done once, by the lane that owns the frame, and the payload
-// chunks of all 64 frames form one flat list: chunk k of the tile is body chunk k - start[f] of the
-// frame f with start[f] <= k < start[f + 1] (an exclusive scan of the frames' body-chunk counts).
-// Lane l takes chunks l, l + 64, ..., so consecutive lanes load and store consecutive 16-byte chunks
-// of a frame whatever its length, U chunks in flight per lane. A lane's chunks belong to ascending
-// frames: it keeps its frame index and its running L4 sum and adds the sum into the frame's LDS
-// slot when it moves on. Then each lane builds its own frame's head chunks 0..3 and last partial
-// chunk (the masked path), finishes the checksum from the LDS slot, and the wave stores the 64
-// frames' head chunks four lanes per frame from LDS.
-#ifndef HALO_TXB_FLAT
-#define HALO_TXB_FLAT 0  // measured slower than build_big: see DESIGN.md §13.6
-#endif
-#ifndef HALO_TXB_FLAT_U
-#define HALO_TXB_FLAT_U 4
-#endif
-struct FlatLds {
-    uint64_t src[kTile];        // payload address of frame byte 0's position (pay - hdr_end)
-    uint32_t start[kTile + 1];  // exclusive scan of the frames' body chunks (chunks 4 .. pay_end/16 - 1)
-    uint32_t sum[kTile];        // the frames' body L4 sums (one's-complement halves, LE domain)
-    uint32_t ndw[kTile];        // the frames' dwords (0: not built)
-};
-
-template <int U>
-__device__ __forceinline__ void flat_tile(const BuildParams& p, const Frame& f, bool live, const uint32_t (&hv)[16],
-                                          uint32_t first, uint32_t lane, uint32_t* s_row, FlatLds& fl) {
-    typedef const __attribute__((address_space(1))) uint32_t gu32_t;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
-    const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
-    const uint32_t l4s = f.base + 20u, pay_end = f.hdr_end + f.plen;
-    const uint32_t ndw = live ? (f.flen + 3u) >> 2 : 0u;
-    const uint32_t cb_end = pay_end >> 4;
-    const uint32_t nbody = live && cb_end > 4 ? cb_end - 4 : 0u;
-    uint32_t incl = nbody;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
-        if (lane >= (uint32_t)o) incl += y;
-    }
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    fl.start[lane] = incl - nbody;
-    if (lane == 63) fl.start[kTile] = total;
-    fl.src[lane] = f.pay - f.hdr_end;
-    fl.sum[lane] = 0;
-    fl.ndw[lane] = ndw;
-    __builtin_amdgcn_wave_barrier();
-    // body: every payload-only chunk of the tile, 64 lanes side by side
-    uint32_t cur = 0, acc_f = 0xFFFFFFFFu, acc = 0;
-    for (uint32_t k0 = lane; k0 < total; k0 += 64u * U) {
-        uint32_t raw[U][5], fr[U], cc[U], shv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t k = k0 + 64u * u;
-            fr[u] = 0xFFFFFFFFu;
-            if (k < total) {
-                while (k >= fl.start[cur + 1]) ++cur;
-                fr[u] = cur;
-                cc[u] = 4u + k - fl.start[cur];
-                const uint64_t P = fl.src[cur];
-                shv[u] = (uint32_t)(P & 3u);
-                gu32_t* q = (gu32_t*)((P + 16ull * cc[u]) & ~3ull);
-                const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)q;
-                raw[u][0] = v.x; raw[u][1] = v.y; raw[u][2] = v.z; raw[u][3] = v.w;
-                raw[u][4] = shv[u] ? q[4] : 0u;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (fr[u] == 0xFFFFFFFFu) break;
-            if (fr[u] != acc_f) {
-                if (acc_f != 0xFFFFFFFFu) atomicAdd(&fl.sum[acc_f], acc);
-                acc_f = fr[u];
-                acc = 0;
-            }
-            uint32_t w[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                w[i] = __builtin_amdgcn_alignbyte(raw[u][i + 1], raw[u][i], shv[u]);
-                acc = hsum_acc(w[i], acc);
-            }
-            *reinterpret_cast<uint4*>(p.frames + (uint64_t)(first + fr[u]) * p.stride + 16ull * cc[u]) =
-                make_uint4(w[0], w[1], w[2], w[3]);
-        }
-    }
-    if (acc_f != 0xFFFFFFFFu) atomicAdd(&fl.sum[acc_f], acc);
-    // this lane's frame: head chunks 0..3 and the last, partial chunk (the masked path)
-    uint32_t keep[4][4];
-    uint32_t sum = 0;
-    uint8_t* out = p.frames + (uint64_t)(first + lane) * p.stride;
-#pragma unroll
-    for (uint32_t c5 = 0; c5 < 5; ++c5) {
-        const uint32_t c = c5 < 4 ? c5 : cb_end;
-        const bool mine = c5 < 4 ? 4 * c < ndw : (cb_end >= 4 && 4 * cb_end < ndw);
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        if (mine) {
-            uint32_t raw[5] = {0u, 0u, 0u, 0u, 0u};
-            if (chunk_has_payload(f, c, ndw)) payload_raw(f, c, raw);
-            const uint32_t sh = (uint32_t)((f.pay - f.hdr_end) & 3u);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t k = 4 * c + i;
-                w[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh) & byte_mask(k, f.hdr_end, pay_end);
-                if (c5 < 4) w[i] |= hv[4 * c5 + i] & byte_mask(k, 0, f.hdr_end);
-                sum = hsum_acc(w[i] & byte_mask(k, l4s, pay_end), sum);
-            }
-            if (c5 == 4) {
-                uint32_t* o = reinterpret_cast<uint32_t*>(out) + 4 * c;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (4 * c + i < ndw) o[i] = w[i];
-            }
-        }
-        if (c5 < 4)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) keep[c5][i] = w[i];
-    }
-    __builtin_amdgcn_wave_barrier();  // every body sum is in its slot
-    uint32_t part = fold16(fold16(fl.sum[lane]) + fold16(sum));
-    uint32_t ck_at;
-    if (f.proto == kIpUdp || f.proto == kIpTcp) {
-        const uint32_t s = bswap32(f.src), t = bswap32(f.dst);
-        part += hsum(s) + hsum(t) + (f.proto << 8) + bswap16(f.l4hdr + f.plen);
-        ck_at = f.base + 20u + (f.proto == kIpUdp ? 6u : 16u);
-    } else {
-        ck_at = f.base + 22u;
-    }
-    const uint32_t ck_le = (csum || f.proto == kIpIcmp) ? (~fold16(part)) & 0xFFFFu : 0u;  // ICMP always
-    const uint32_t ck_dw = ck_at >> 2, ck_sh = (ck_at & 2u) * 8u;
-#pragma unroll
-    for (uint32_t c = 0; c < 4; ++c)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (4 * c + i == ck_dw) keep[c][i] |= ck_le << ck_sh;
-            s_row[16 * lane + 4 * c + i] = keep[c][i];
-        }
-    __builtin_amdgcn_wave_barrier();
-    // the tile's head chunks, four lanes per frame: one store instruction covers 16 frames' 64 bytes
-#pragma unroll
-    for (uint32_t r = 0; r < 4; ++r) {
-        const uint32_t fr = 16 * r + (lane >> 2), c = lane & 3u;
-        const uint32_t nd = fl.ndw[fr];
-        if (4 * c < nd) {
-            const uint32_t* src = &s_row[16 * fr + 4 * c];
-            uint32_t* o = reinterpret_cast<uint32_t*>(p.frames + (uint64_t)(first + fr) * p.stride) + 4 * c;
-            if (4 * c + 4 <= nd) {
-                *reinterpret_cast<uint4*>(o) = make_uint4(src[0], src[1], src[2], src[3]);
-            } else {
-#pragma unroll
-                for (uint32_t i = 0; i < 3; ++i)
-                    if (4 * c + i < nd) o[i] = src[i];
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();  // the LDS rows are rewritten for the next tile
-}
+// Tried and removed (round 4; in git history up to commit 68eed30): software pipelining of build_big across the steps of a tile (big_load /
+// big_finish, two load buffers), and a tile-flat build with every per-frame step done once by the
+// lane owning the frame (flat_tile). Both bit-exact, both slower.
 
 // Bytes [0, n) of a dword as a mask, n clamped to 0..4.
 __device__ __forceinline__ uint32_t prefix_mask(int32_t n) {
@@ -846,10 +544,10 @@ __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t s
 #define HALO_TXB_SPLIT 1  // 2 measured neutral: 0.2032 / 0.2021 ms against 0.2021 / 0.2044 (profiles/r04/r4h)
 #endif
 template <int G>
-constexpr uint32_t kSplit = (G >= 16 && !HALO_TXB_FLAT && !HALO_TXB_PIPE) ? HALO_TXB_SPLIT : 1;
+constexpr uint32_t kSplit = G >= 16 ? HALO_TXB_SPLIT : 1;
 
 template <int G, int U>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G == 1 ? HALO_TXB_G1_WAVES : (G >= 16 && HALO_TXB_PIPE) ? HALO_TXB_PIPE_WAVES : 4 * kSplit<G>)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(G == 1 ? HALO_TXB_G1_WAVES : 4 * kSplit<G>)))
 tx_build_kernel(const BuildParams p) {
 #ifndef HALO_TXB_G1_LDS_TRIM
 #define HALO_TXB_G1_LDS_TRIM 1
@@ -867,8 +565,6 @@ tx_build_kernel(const BuildParams p) {
     constexpr uint32_t kRow = G == 1 ? 17 : 16;
     __shared__ uint32_t s_hdr[kBlock / 64][kOwn * kRow + 1];
     __shared__ uint32_t s_ndw[kBlock / 64][G == 1 ? kTile : 1];  // G = 1: staged frame's dwords (0: none)
-    constexpr bool kFlat = G >= 16 && HALO_TXB_FLAT;
-    __shared__ FlatLds s_flat[kFlat ? kBlock / 64 : 1];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t nw = (gridDim.x * kBlock) >> 6;
     const uint32_t base = *p.ip_id;
@@ -989,9 +685,6 @@ tx_build_kernel(const BuildParams p) {
                 }
             }
             __builtin_amdgcn_wave_barrier();  // the region is rewritten for the next tile
-        } else if constexpr (kFlat) {
-            flat_tile<HALO_TXB_FLAT_U>(p, decode(d, p.payload), (mine >> 31) != 0, hv, first, lane, s_hdr[wv],
-                                       s_flat[wv]);
         } else {
             // this wave's frames (steps congruent to `part` mod S) at compact LDS slots
             constexpr uint32_t F = 64u / G;  // frames per step
@@ -1007,40 +700,6 @@ tx_build_kernel(const BuildParams p) {
                 s_meta[wv][slot] = mine;
             }
             __builtin_amdgcn_wave_barrier();
-            if constexpr (G >= 16 && HALO_TXB_BIG_PATH && HALO_TXB_PIPE && S == 1) {
-                // step k + 1's loads go out before step k's build waits for its own
-                auto frame_at = [&](uint32_t fl) {
-                    uint32_t dd[10];
-#pragma unroll
-                    for (int k = 0; k < 10; ++k) dd[k] = s_desc[wv][10 * fl + k];
-                    return decode(dd, p.payload);
-                };
-                // two buffers used alternately (the loop is unrolled by two): copying the next
-                // step's buffer into the current one would wait for its loads
-                BigLoad<U> ba, bb;
-                constexpr uint32_t F = 64u / G;
-                auto finish = [&](uint32_t fl, const BigLoad<U>& b) {
-                    big_finish<G, U>(p, frame_at(fl), &s_hdr[wv][kRow * fl], j,
-                                     p.frames + (uint64_t)(first + fl) * p.stride, b);
-                };
-                uint32_t m0 = s_meta[wv][g];
-                if (m0 >> 31) big_load<G, U>(frame_at(g), j, ba);
-#pragma unroll 1
-                for (uint32_t step = 0; step < (uint32_t)G; step += 2) {
-                    const uint32_t f0 = step * F + g, f1 = f0 + F, f2 = f1 + F;
-                    const uint32_t m1 = s_meta[wv][f1];
-                    // (the empty asm keeps the compiler from holding a decoded frame in registers
-                    // across the other frame's build: it re-reads the descriptor from LDS)
-                    if (m1 >> 31) big_load<G, U>(frame_at(f1), j, bb);
-                    asm volatile("" ::: "memory");
-                    if (m0 >> 31) finish(f0, ba);
-                    const uint32_t m2 = step + 2 < (uint32_t)G ? s_meta[wv][f2] : 0u;
-                    if (m2 >> 31) big_load<G, U>(frame_at(f2), j, ba);
-                    asm volatile("" ::: "memory");
-                    if (m1 >> 31) finish(f1, bb);
-                    m0 = m2;
-                }
-            } else
 #pragma unroll 1
             for (uint32_t step = 0; step < (uint32_t)G / S; ++step) {
                 const uint32_t sl = step * F + g;                // this group's frame's LDS slot
