@@ -189,12 +189,20 @@ func NewCtx(device int) (*Ctx, error) {
 // resident on the GPU instead of a launch per batch (halo_rx_host_ctx_set_resident): the frames are
 // packed into pinned staging and one request line is written, so a PacketHandle-sized batch costs
 // ~8 us instead of ~33-37 us (DESIGN.md §13.1). The kernel keeps 8 CUs while batches keep coming
-// and leaves 20 ms after the last one. maxBytes bounds the staging (0: min(1516 * maxFrames, 4 MiB)).
+// and leaves 20 ms after the last one. maxBytes bounds the staging (0: min(1516 * maxFrames, 64 MiB)).
 func (x *Ctx) SetResident(maxFrames int, maxBytes uint64) error {
 	x.mu.Lock()
 	defer x.mu.Unlock()
 	return halo(C.halo_rx_host_ctx_set_resident(x.c, C.uint32_t(maxFrames), C.uint64_t(maxBytes)))
 }
+
+// DeviceSynchronize waits for all work on `device` after stopping the library's resident consumers
+// there (halo_rx_device_synchronize). A plain hipDeviceSynchronize from the caller would wait for
+// those kernels too, which end only 20 ms after their last request.
+func DeviceSynchronize(device int) error { return halo(C.halo_rx_device_synchronize(C.int(device))) }
+
+// Release frees the device-wide state of the library on `device` (halo_rx_release).
+func Release(device int) error { return halo(C.halo_rx_release(C.int(device))) }
 
 // Close frees the context.
 func (x *Ctx) Close() {

@@ -222,6 +222,8 @@ _u8p = ctypes.c_void_p
 _PROTOS = {
     "halo_rx_version": (ctypes.c_char_p, []),
     "halo_rx_init": (ctypes.c_int, [ctypes.c_int]),
+    "halo_rx_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
+    "halo_rx_release": (ctypes.c_int, [ctypes.c_int]),
     "halo_rx_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "halo_rx_status_name": (ctypes.c_char_p, [ctypes.c_int]),
     "halo_rx_parse_batch_device": (ctypes.c_int, [
@@ -355,6 +357,13 @@ def strerror(code: int) -> str:
 def check(fn: str, code: int) -> None:
     if code != HALO_OK:
         raise HaloError(fn, code)
+
+
+def device_synchronize(device: int = 0) -> None:
+    """hipDeviceSynchronize for `device` after parking this library's resident consumers there
+    (halo_rx_device_synchronize): use it instead of torch.cuda.synchronize() while a persistent ring
+    or a resident host context is live, which a plain device sync would wait on."""
+    check("halo_rx_device_synchronize", lib.halo_rx_device_synchronize(device))
 
 
 def ptr(x) -> int | None:

@@ -5,6 +5,9 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <memory>
+#include <vector>
+
 #include "halo_limits.h"
 #include "halo_rx.h"
 #include "host_logic.h"
@@ -24,7 +27,7 @@ struct RxParams {
     uint32_t mac_hi;  // own MAC bytes 4..5
     uint32_t own_ip;  // IpAddrToU(NetIf.IpAddr)
     halo_rx_result_t* out;
-    uint32_t* hist;      // the launch's partial histograms (hist_slots), or null
+    uint32_t* hist;      // the device's histogram tree set (hist_trees), or null
     uint32_t* hist_out;  // the caller's counters the last block of the launch adds into
     // fused NAT flow-key hash of every record (halo_rx_parse_flow_batch_device), or null
     uint64_t* flow_hash;
@@ -58,15 +61,29 @@ enum SynthSlot : uint32_t {
 
 int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 
-// Partial status histograms of an rx launch (flush_hist, rx_parse.hip): kHistSlots level-1 slots
-// (one per block modulo kHistSlots) then kHistSlots / kHistFan level-2 slots, kHistStride 64-bit
-// words each (arrivals << 40 | count, one per status), zero between launches. One array per
-// (device, stream) the library has parsed on with a histogram, allocated at first use and kept
-// for the life of the process (135 KB each; a caller cycling through many short-lived streams with
-// histograms on grows this set): launches on one stream run in order, so they can share it.
+// Partial status histograms of an rx launch (flush_hist, rx_parse.hip). A tree is kHistSlots
+// level-1 slots (one per block modulo kHistSlots) then kHistSlots / kHistFan level-2 slots,
+// kHistStride 64-bit words each (arrivals << 40 | count, one per status), zero between launches.
+// Trees belong to HSA queues, not to streams: a device's tree set holds kHistTrees trees and a key
+// word per tree, and a launch's blocks take the tree whose key is their queue (queue_ptr), claiming
+// a free key on the queue's first launch; keys are never released, so every block of every launch
+// on a queue agrees on its tree. Sharing a tree between launches of one queue is safe because
+// every HIP dispatch carries the AQL barrier bit (profiles/r05/queue_probe.log: null, created and
+// per-thread streams, graph replays): a packet starts only after every earlier packet of its queue
+// has completed, so no two launches are ever inside one tree. hist_trees checks the bit once per
+// device with a probe dispatch; without it the keys are poisoned and launches add straight into the
+// caller's counters (so do launches beyond kHistTrees queues). Streams that share a queue are
+// serialised by those barriers; hipStreamPerThread, graph replays on several streams at once and
+// streams of other devices need no host-side key at all.
 constexpr uint32_t kHistSlots = 1024, kHistFan = 32, kHistStride = 16;
 constexpr uint32_t kHistWords = (kHistSlots + kHistSlots / kHistFan) * kHistStride;  // 64-bit words
-uint32_t* hist_slots(hipStream_t s);  // nullptr: allocation failed
+constexpr uint32_t kHistTrees = 16, kHistKeyWords = 16;  // keys first (one 128 B line), then trees
+constexpr uint64_t kHistSetBytes = 8ull * (kHistKeyWords + (uint64_t)kHistTrees * kHistWords);
+// The tree set of `device`, allocated and zeroed at first use (halo_rx_init does it ahead of any
+// capture); nullptr when that fails, or when it is first needed inside a stream capture.
+uint32_t* hist_trees(int device, hipStream_t capture_probe);
+int stream_device(hipStream_t s);  // the device a launch on `s` runs on (-1: unknown)
+void hist_trees_release(int device);  // frees the set (the caller has drained the device)
 
 // The resident small-poll consumer of a ring attached with HALO_RING_PERSISTENT (ring_rx.hip
 // drives it, rx_parse.hip runs it): kSvcGroups workgroups that wait on this control block, in
@@ -144,6 +161,9 @@ void resident_destroy(Resident* s);
 int resident_request(Resident* s, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif, halo_rx_result_t* dout,
                      uint32_t uni_off, uint32_t uni_stride, uint32_t uni_len);
 void resident_set_timeout(Resident* s, uint64_t us);  // 0: the default (2 s)
+// New frame / offset / length arrays for the next launch of the consumer (the owner reallocated
+// them). The caller holds a ParkResidents on the device, so the consumer's kernel has ended.
+void resident_set_arrays(Resident* s, const uint8_t* d_data, const uint32_t* d_off, const uint16_t* d_len);
 ResidentStats resident_stats(const Resident* s);
 // While one lives, the resident consumers of `device` are stopped (their kernels have ended) and new
 // requests take the launch path. Every library call that frees device or pinned memory or
@@ -159,6 +179,12 @@ class ParkResidents {
 
   private:
     int device_;
+};
+// The resident consumers of every device this library has launched on, and of `also`, parked for a
+// scope: a host free (hipHostFree) waits for kernels on every device, not only the owner's.
+struct ParkUsed {
+    explicit ParkUsed(int also = -1);
+    std::vector<std::unique_ptr<ParkResidents>> parks;
 };
 // hipDeviceSynchronize on `device` under a ParkResidents.
 int drain_device(int device);

@@ -243,6 +243,15 @@ uint32_t pack_chunk(const uint8_t* bytes, const uint64_t* offsets, const uint16_
     return cnt;
 }
 
+uint64_t pack_need(const uint16_t* lens, uint64_t n, uint32_t cap) {
+    uint64_t need = 0;
+    for (uint64_t i = 0; i < n; ++i) {  // vectorisable
+        const uint32_t L = lens[i];
+        need += L <= cap ? ((L + 3u) & ~3u) : 0u;
+    }
+    return need;
+}
+
 bool span_aligned(const uint64_t* offsets, const uint16_t* lens, uint32_t cnt, uint64_t* lo_out, uint64_t* hi_out) {
     uint64_t lo = ~0ull, hi = 0, mis = 0;
     for (uint32_t j = 0; j < cnt; ++j) {  // vectorisable

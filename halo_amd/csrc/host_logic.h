@@ -85,6 +85,9 @@ uint32_t plan_direct(const uint64_t* offsets, const uint16_t* lens, uint64_t n, 
 uint32_t pack_chunk(const uint8_t* bytes, const uint64_t* offsets, const uint16_t* lens, uint64_t n, uint64_t next,
                     uint32_t chunk_frames, uint64_t chunk_bytes, uint32_t cap, uint8_t* staging, uint32_t* h_off,
                     uint16_t* h_len, uint64_t* used);
+// The staging bytes pack_chunk would use for frames [0, n) (no copy): a batch is checked against
+// a staging area before any byte is packed.
+uint64_t pack_need(const uint16_t* lens, uint64_t n, uint32_t cap);
 // The byte span [*lo, *hi) of cnt frames and whether their offsets agree modulo 4.
 bool span_aligned(const uint64_t* offsets, const uint16_t* lens, uint32_t cnt, uint64_t* lo, uint64_t* hi);
 

@@ -59,16 +59,17 @@ int sync_used_devices() {
     return rc;
 }
 
-// The resident consumers of every device this library launched on, parked for a scope.
-struct ParkUsed {
-    std::vector<std::unique_ptr<ParkResidents>> parks;
-    ParkUsed() {
-        const uint64_t used = g_devices_used.load(std::memory_order_relaxed);
-        for (int d = 0; d < 64; ++d)
-            if ((used >> d) & 1) parks.emplace_back(new ParkResidents(d));
-    }
-};
 
+}  // namespace
+
+ParkUsed::ParkUsed(int also) {
+    uint64_t used = g_devices_used.load(std::memory_order_relaxed);
+    if (also >= 0 && also < 64) used |= 1ull << also;
+    for (int d = 0; d < 64; ++d)
+        if ((used >> d) & 1) parks.emplace_back(new ParkResidents(d));
+}
+
+namespace {
 // True while the runtime still maps host address p for the device.
 bool runtime_maps(void* p) {
     void* d = nullptr;
@@ -144,7 +145,25 @@ extern "C" HALO_API int halo_rx_init(int device) {
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return HALO_E_NODEV;
     if (device < 0 || device >= count) return HALO_E_NODEV;
     if (hipSetDevice(device) != hipSuccess) return HALO_E_NODEV;
-    return halo::check_device();
+    const int rc = halo::check_device();
+    if (rc) return rc;
+    return halo::hist_trees(device, nullptr) ? HALO_OK : HALO_E_NOMEM;
+}
+
+extern "C" HALO_API int halo_rx_device_synchronize(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return HALO_E_NODEV;
+    return halo::drain_device(device);
+}
+
+extern "C" HALO_API int halo_rx_release(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return HALO_E_NODEV;
+    halo::ParkResidents park(device);  // hipFree waits for every kernel on the device
+    const int rc = halo::drain_device(device);
+    if (rc) return rc;
+    halo::hist_trees_release(device);
+    return HALO_OK;
 }
 
 // ---- host-memory batch path ---------------------------------------------------------------
@@ -338,6 +357,8 @@ int resident_batch(halo_rx_host_ctx* c, const uint8_t* bytes, const uint64_t* of
     auto& R = c->res;
     const auto t0 = clk::now();
     uint64_t used = 0;
+    // checked before any byte is copied: a batch that does not fit is staged once, by the chunked path
+    if (halo::pack_need(lens, n, cap) > R.max_bytes) return 1;
     if (halo::pack_chunk(bytes, offsets, lens, n, 0, n, R.max_bytes, cap, R.h_bytes, R.h_off, R.h_len, &used) != n)
         return 1;
     uint32_t ulen = lens[0], ustride = 0;
@@ -559,7 +580,8 @@ extern "C" HALO_API int halo_rx_host_ctx_set_resident(halo_rx_host_ctx_t* ctx, u
     halo::ParkResidents park(ctx->device);  // frees and pinned allocations below
     free_resident(ctx->res);
     if (max_frames == 0) return HALO_OK;
-    if (max_bytes == 0) max_bytes = std::min<uint64_t>(1516ull * max_frames, 4ull << 20);
+    // default: room for max_frames full-MTU frames, so a PacketHandle batch of 1514 B frames is served
+    if (max_bytes == 0) max_bytes = std::min<uint64_t>(1516ull * max_frames, 64ull << 20);
     max_bytes = (max_bytes + 3) & ~3ull;
     auto& R = ctx->res;
     bool ok = pinned_mapped(&R.h_bytes, &R.d_bytes, max_bytes + 64) &&  // + a dword tail any load may cover

@@ -108,7 +108,7 @@ int resident_create(int device, const uint8_t* d_data, const uint32_t* d_off, co
 
 void resident_destroy(Resident* s) {
     if (!s) return;
-    ParkResidents park(s->device);  // hipFree / hipHostFree below wait for every kernel on the device
+    ParkUsed park(s->device);  // hipFree / hipHostFree below wait for kernels on every device
     {
         std::lock_guard<std::mutex> g(g_live_mu);
         g_live.erase(std::remove(g_live.begin(), g_live.end(), s), g_live.end());
@@ -126,6 +126,14 @@ void resident_destroy(Resident* s) {
 void resident_set_timeout(Resident* s, uint64_t us) {
     std::lock_guard<std::mutex> lk(s->mu);
     s->timeout_us = us ? us : 2000000;
+}
+
+void resident_set_arrays(Resident* s, const uint8_t* d_data, const uint32_t* d_off, const uint16_t* d_len) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    stop_locked(s);  // already parked by the caller: a no-op unless it was relaunched since
+    s->d_data = d_data;
+    s->d_off = d_off;
+    s->d_len = d_len;
 }
 
 ResidentStats resident_stats(const Resident* s) {

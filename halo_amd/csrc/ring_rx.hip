@@ -581,6 +581,9 @@ int alloc_small(halo_rx_ring* r, uint64_t bytes) {
         r->h_sres = nullptr;  // allocated on first use: only for callers whose array is not mapped
         r->d_sres = nullptr;
         r->small_frames = 0;
+        r->d_soff = nullptr;
+        r->d_slen = nullptr;
+        if (r->svc) halo::resident_set_arrays(r->svc, r->d_data, nullptr, nullptr);  // freed above
         if (hipHostMalloc((void**)&r->h_soff, 4ull * frames, hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc((void**)&r->h_slen, 2ull * frames, hipHostMallocDefault) != hipSuccess)
             return HALO_E_NOMEM;
@@ -588,6 +591,7 @@ int alloc_small(halo_rx_ring* r, uint64_t bytes) {
         r->d_slen = static_cast<uint16_t*>(device_view(r->h_slen, 2ull * frames));
         if (!r->d_soff || !r->d_slen) return HALO_E_NOMEM;
         r->small_frames = frames;
+        if (r->svc) halo::resident_set_arrays(r->svc, r->d_data, r->d_soff, r->d_slen);
     }
     r->small = bytes;
     return HALO_OK;

@@ -34,7 +34,6 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
-#include <map>
 #include <mutex>
 
 #include "device_util.h"
@@ -277,11 +276,28 @@ __device__ __forceinline__ void frame_at(const RxParams& p, uint64_t i, const ui
 struct Hist {
     uint32_t* s;  // __shared__ [HALO_RX_STATUS_COUNT]
     uint32_t ok;
+    // status threads: the key word the launch queue's tree most likely has (flush_hist), loaded when
+    // the block starts so that its latency hides under the frame loads instead of ending the block
+    unsigned long long key;
     __device__ __forceinline__ void add(uint32_t status) {
         if (status == HALO_RX_OK) ++ok;
         else atomicAdd(&s[status], 1u);
     }
 };
+
+// The launch's HSA queue and the tree-set slot its key is looked up from first.
+__device__ __forceinline__ unsigned long long launch_queue() {
+    return (unsigned long long)(uintptr_t)(const void*)__builtin_amdgcn_queue_ptr();
+}
+__device__ __forceinline__ uint32_t tree_slot0(unsigned long long q) {
+    return ((uint32_t)(q >> 6) ^ (uint32_t)(q >> 17)) & (kHistTrees - 1u);
+}
+__device__ __forceinline__ Hist hist_open(const RxParams& p, uint32_t* s_hist) {
+    Hist h{s_hist, 0, 0};
+    if (p.hist && threadIdx.x < HALO_RX_STATUS_COUNT)
+        h.key = reinterpret_cast<const unsigned long long*>(p.hist)[tree_slot0(launch_queue())];
+    return h;
+}
 
 // 16-byte chunks per lane issued before the header is parsed (a lane-per-frame lane needs its
 // first 64 bytes). Eight for groups would let a 570 B frame finish in one round trip, but costs
@@ -487,29 +503,60 @@ __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, boo
 }
 
 // The block's counts reach the caller's counters through a two-level tree of partial histograms
-// (p.hist, hist_slots) instead of device-scope atomics on the caller's 14 counters: those serialise
+// (p.hist, hist_trees) instead of device-scope atomics on the caller's 14 counters: those serialise
 // at the memory side, ~10 ns each, and 16384 one-wave blocks cost 170 us on a 21 us launch (bench
 // r4b). Every word of the tree is a 64-bit (arrivals << 40 | count) pair, one per status: block b
 // adds (1 << 40 | its count) to status k of level-1 slot b % 1024 (16 blocks per slot for 1M
 // frames), and the add that brings the arrivals to the slot's block count returns the slot's final
 // count, so that thread alone moves it on — to level-2 slot (b % 1024) / 32, whose last arrival
 // adds it to the caller's counter (at most 32 x 14 atomics on them per launch) — and zeroes the word
-// for the next launch on the stream. Each word carries its own completion, so no fence is needed: a
+// for the next launch on the queue. Each word carries its own completion, so no fence is needed: a
 // __threadfence per block (agent-scope release / acquire, L2 writeback and invalidate across the
 // XCDs on gfx950) cost 0.55 ms per 1M-frame launch (bench r4i), and a separate finalize launch
 // ~10 us (r4e). Every block of a kernel that counts calls this once, with the whole block.
+// The tree is the one of the launch's HSA queue (halo_common.h): the words assume one launch at a
+// time per tree, and the dispatch packet's barrier bit is what guarantees it.
+#ifndef HALO_HIST_HDR
+#define HALO_HIST_HDR 0  // measurement knob: 1 = every block re-reads its dispatch packet's barrier bit
+#endif
+// key0: the word at the queue's first probe slot as the block read it when it started (Hist::key).
+// A key never changes once set, so a stale copy can only read 0, and then the CAS (performed at
+// memory) returns the real key.
+__device__ __forceinline__ unsigned long long* launch_tree(uint32_t* set_u32, unsigned long long key0) {
+#if HALO_HIST_HDR
+    // 100 us per 1M-frame launch: the packet lives in host memory (bench_hist, profiles/r05)
+    const uint16_t hdr = *static_cast<const uint16_t*>((const void*)__builtin_amdgcn_dispatch_ptr());
+    if (!((hdr >> 8) & 1u)) return nullptr;  // HSA_PACKET_HEADER_BARRIER
+#endif
+    unsigned long long* set = reinterpret_cast<unsigned long long*>(set_u32);
+    const unsigned long long q = launch_queue();
+    const uint32_t k0 = tree_slot0(q);
+    if (key0 == q) return set + kHistKeyWords + (uint64_t)k0 * kHistWords;
+    for (uint32_t j = 0; j < kHistTrees; ++j) {
+        const uint32_t k = (k0 + j) & (kHistTrees - 1u);
+        unsigned long long key = j ? set[k] : key0;
+        if (key == 0) key = atomicCAS(set + k, 0ull, q);  // 0: claimed now; q: claimed by another block
+        if (key == 0 || key == q) return set + kHistKeyWords + (uint64_t)k * kHistWords;
+    }
+    return nullptr;  // every key taken by another queue, or poisoned (hist_trees: no barrier bits)
+}
+
 __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     if (!p.hist) return;
+    const uint32_t t = threadIdx.x;
     uint32_t ok = hist.ok;
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) ok += __shfl_xor(ok, m, 64);
     if ((threadIdx.x & 63u) == 0 && ok) atomicAdd(&hist.s[HALO_RX_OK], ok);
     __syncthreads();
-    const uint32_t t = threadIdx.x;
     if (t >= HALO_RX_STATUS_COUNT) return;
-    constexpr unsigned long long kOne = 1ull << 40, kCount = kOne - 1;
     const uint32_t s = blockIdx.x & (kHistSlots - 1u), g = gridDim.x;
-    unsigned long long* tree = reinterpret_cast<unsigned long long*>(p.hist);
+    unsigned long long* tree = launch_tree(p.hist, hist.key);  // wave 0 only: one request for its lanes
+    if (!tree) {  // no tree this launch can own alone: straight into the caller's counters
+        if (hist.s[t]) atomicAdd(&p.hist_out[t], hist.s[t]);
+        return;
+    }
+    constexpr unsigned long long kOne = 1ull << 40, kCount = kOne - 1;
     unsigned long long* l1 = tree + s * kHistStride + t;
     unsigned long long now = atomicAdd(l1, kOne | hist.s[t]) + (kOne | hist.s[t]);
     if ((now >> 40) != g / kHistSlots + (g % kHistSlots > s)) return;
@@ -529,7 +576,7 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
-    Hist hist{s_hist, 0};
+    Hist hist = hist_open(p, s_hist);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp_base = lane & ~(uint32_t)(G - 1);
@@ -622,7 +669,7 @@ rx_lane_kernel(const RxParams p) {
     __shared__ uint4 s_rec[HALO_RX_LANE_BLOCK / 64][128];  // per wave: 64 records of 32 B
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
-    Hist hist{s_hist, 0};
+    Hist hist = hist_open(p, s_hist);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = threadIdx.x >> 6;
 #if HALO_RX_LANE_XCD
@@ -678,7 +725,7 @@ __global__ void __launch_bounds__(HALO_RX_LANE_BLOCK) rx_lane_multi_kernel(const
     __shared__ uint4 s_rec[HALO_RX_LANE_BLOCK / 64][128];
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
-    Hist hist{s_hist, 0};
+    Hist hist = hist_open(mp.p, s_hist);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -786,7 +833,7 @@ __global__ void __launch_bounds__(64 * kSvcWaves) ring_service_kernel(RingServic
         p.mac_hi = s_cmd[5];
         p.own_ip = s_cmd[6];
         p.out = reinterpret_cast<halo_rx_result_t*>((uint64_t)s_cmd[7] | ((uint64_t)s_cmd[8] << 32));
-        Hist hist{s_hist, 0};
+        Hist hist{s_hist, 0, 0};  // the consumer keeps no histogram
         if (s_cmd[11]) {  // one length, consecutive records: the strided layout, no array reads
             p.bytes = data + 4ull * s_cmd[9];
             p.stride = 4ull * s_cmd[10];
@@ -901,7 +948,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALO_R
     __shared__ uint16_t s_len[4][kMixWindow];
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
-    Hist hist{s_hist, 0};
+    Hist hist = hist_open(p, s_hist);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = threadIdx.x >> 6;
     constexpr bool L3 = kL3<LAYOUT>;
@@ -1138,7 +1185,7 @@ rx_stream_kernel(const RxParams p) {
     __shared__ uint32_t s_base[kW][kStreamStep / 16];  // per wave: P at each 16-byte sub-chunk
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
-    Hist hist{s_hist, 0};
+    Hist hist = hist_open(p, s_hist);
     constexpr bool L3 = kL3<LAYOUT>;
     constexpr uint32_t O = kIpOff<L3>;
     constexpr uint32_t kSeg = O + 20u;        // L4 segment start in the frame (34 or 20)
@@ -1410,7 +1457,7 @@ int launch_parse(const RxParams& p_in, int layout, uint32_t max_len, bool unifor
     // wastes < 1/4; strided frames with their own lengths may be anything below the stride
     RxParams p = p_in;
     p.hist_out = p.hist;
-    if (p.hist && !(p.hist = hist_slots(s))) return HALO_E_NOMEM;  // the kernel counts into the slots
+    if (p.hist && !(p.hist = hist_trees(stream_device(s), s))) return HALO_E_NOMEM;  // counts go through a tree
     const bool dense = layout == 0 || layout == 3 || (layout == 2 && p.stride <= max_len + max_len / 4 + 64);
     const int v = pick_variant(max_len, uniform, dense, p.flags);
     hipError_t e;
@@ -1447,22 +1494,81 @@ int fill_common(RxParams& p, uint32_t n, uint32_t flags, const halo_rx_netif_t* 
 
 }  // namespace
 
-uint32_t* hist_slots(hipStream_t s) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, uint32_t*> slots;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> g(mu);
-    auto& p = slots[{dev, s}];
-    if (!p) {
-        const size_t bytes = sizeof(uint64_t) * kHistWords;
-        if (hipMalloc((void**)&p, bytes) != hipSuccess || hipMemsetAsync(p, 0, bytes, s) != hipSuccess) {
-            (void)hipGetLastError();
-            if (p) (void)hipFree(p);
-            p = nullptr;
-        }
+int stream_device(hipStream_t s) {
+    int dev = -1;
+    if (s != nullptr && s != hipStreamPerThread) {
+        if (hipStreamGetDevice(s, &dev) == hipSuccess) return dev;
+        (void)hipGetLastError();
+        return -1;
     }
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return dev;
+}
+
+namespace {
+std::mutex g_trees_mu;
+uint32_t* g_trees[64];
+
+// Writes its own AQL packet header (the barrier bit is bit 8) to *out.
+__global__ void dispatch_header_probe(unsigned long long* out) {
+    if (threadIdx.x == 0) *out = *static_cast<const volatile uint16_t*>((const void*)__builtin_amdgcn_dispatch_ptr());
+}
+
+// flush_hist relies on every dispatch carrying the barrier bit (the runtime's in-order streams do:
+// profiles/r05/queue_probe.log) instead of re-reading the packet in every block, which costs 4x the
+// launch. Checked once per device on the null stream and a fresh stream; without the bit the keys
+// are poisoned, and every launch adds straight into the caller's counters (slow, exact).
+bool barrier_bits_set(unsigned long long* scratch) {
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+    hipLaunchKernelGGL(dispatch_header_probe, dim3(1), dim3(64), 0, nullptr, scratch);
+    hipLaunchKernelGGL(dispatch_header_probe, dim3(1), dim3(64), 0, st, scratch + 1);
+    unsigned long long h[2] = {0, 0};
+    const bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess &&
+                    hipStreamSynchronize(nullptr) == hipSuccess &&
+                    hipMemcpy(h, scratch, sizeof h, hipMemcpyDeviceToHost) == hipSuccess;
+    (void)hipStreamDestroy(st);
+    return ok && ((h[0] >> 8) & 1u) && ((h[1] >> 8) & 1u);
+}
+}  // namespace
+
+uint32_t* hist_trees(int device, hipStream_t capture_probe) {
+    if (device < 0 || device >= 64) return nullptr;
+    std::lock_guard<std::mutex> g(g_trees_mu);
+    uint32_t*& p = g_trees[device];
+    if (p) return p;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(capture_probe, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        (void)hipGetLastError();
+        return nullptr;  // no allocation inside a capture: halo_rx_init(device) makes the set beforehand
+    }
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != device && hipSetDevice(device) != hipSuccess) return nullptr;
+    void* m = nullptr;
+    bool ok = hipMalloc(&m, kHistSetBytes) == hipSuccess;
+    const bool barriers = ok && barrier_bits_set(static_cast<unsigned long long*>(m) + kHistKeyWords);
+    ok = ok && hipMemsetAsync(m, 0, kHistSetBytes, nullptr) == hipSuccess &&
+         (barriers || hipMemsetAsync(m, 0xFF, 8ull * kHistTrees, nullptr) == hipSuccess) &&
+         hipStreamSynchronize(nullptr) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
+        if (m) (void)hipFree(m);
+        m = nullptr;
+    }
+    if (cur != device) (void)hipSetDevice(cur);
+    p = static_cast<uint32_t*>(m);
     return p;
+}
+
+void hist_trees_release(int device) {
+    if (device < 0 || device >= 64) return;
+    std::lock_guard<std::mutex> g(g_trees_mu);
+    if (g_trees[device]) (void)hipFree(g_trees[device]);
+    g_trees[device] = nullptr;
 }
 }  // namespace halo
 
@@ -1602,7 +1708,7 @@ extern "C" HALO_API int halo_rx_parse_batches_device(const halo_rx_batch_desc_t*
     mp.p.n = 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     mp.p.hist_out = d_status_hist;
-    if (d_status_hist && !(mp.p.hist = halo::hist_slots(s))) return HALO_E_NOMEM;
+    if (d_status_hist && !(mp.p.hist = halo::hist_trees(halo::stream_device(s), s))) return HALO_E_NOMEM;
     constexpr uint32_t wpb = HALO_RX_LANE_BLOCK / 64;
     const dim3 grid(halo::grid_for(windows * 64u, 64, HALO_RX_LANE_MAX_BLOCKS * 4 / wpb, wpb));
     if (flags & HALO_RX_L3_START)

@@ -198,8 +198,19 @@ typedef void* halo_stream_t; /* a hipStream_t (NULL = the device's null stream) 
 
 /* ---- device / library -------------------------------------------------------------- */
 HALO_API const char* halo_rx_version(void);
-/* Selects `device` for the calling thread and checks that it is a gfx950 part. */
+/* Selects `device` for the calling thread, checks that it is a gfx950 part and makes the device's
+ * status-histogram trees (2.2 MB, zeroed): call it before capturing histogram-on parses in a
+ * hipGraph, since a capture cannot allocate. Idempotent. */
 HALO_API int halo_rx_init(int device);
+/* Waits for all work on `device` the way hipDeviceSynchronize does, after stopping this library's
+ * resident consumers on it (rings attached with HALO_RING_PERSISTENT, host contexts with
+ * halo_rx_host_ctx_set_resident). A caller's own hipDeviceSynchronize / torch.cuda.synchronize()
+ * waits for those kernels too, and they end only 20 ms after their last request (never, while
+ * another thread keeps them busy); this call does not. The consumers restart on their next request. */
+HALO_API int halo_rx_device_synchronize(int device);
+/* Frees the device-wide state halo_rx_init made (after halo_rx_device_synchronize). Rings, contexts
+ * and route tables stay valid; the next histogram-on call makes the trees again. */
+HALO_API int halo_rx_release(int device);
 HALO_API const char* halo_rx_strerror(int code);
 HALO_API const char* halo_rx_status_name(int status);
 
@@ -269,7 +280,7 @@ HALO_API int halo_rx_host_ctx_set_zero_copy(halo_rx_host_ctx_t* ctx, int enable)
  * gathered into batches of a few frames to a few thousand, engine/engine.go:339-385, and of the
  * single-frame Parse* wrappers an Ipv4PktFwdHook calls, engine/engine.go:132). Batches of at most
  * `max_frames` frames (<= 16384; 0 turns the path off) whose frames fit `max_bytes` of staging
- * (0: min(1516 * max_frames, 4 MiB); at most 64 MiB) are copied into pinned staging this context
+ * (0: min(1516 * max_frames, 64 MiB); at most 64 MiB) are copied into pinned staging this context
  * owns, and a kernel resident on 8 CUs — waiting on a control block in pinned memory — parses them
  * there and writes the records into `out` (directly when `out` lies in a live registration): no
  * launch and no stream synchronisation per call. The kernel leaves 20 ms after its last request and

@@ -369,7 +369,7 @@ ORA_API int ora_rx_batch(const uint8_t* bytes, const uint32_t* offsets_dw, const
                          uint32_t len, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
                          halo_rx_result_t* out, uint32_t* hist, int threads) {
     if (threads < 1) threads = 1;
-    if (threads > 256) threads = 256;
+    if (threads > 1024) threads = 1024;
     ora_job_t* jobs = (ora_job_t*)calloc((size_t)threads, sizeof(ora_job_t));
     pthread_t* tid = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
     if (!jobs || !tid) { free(jobs); free(tid); return -1; }

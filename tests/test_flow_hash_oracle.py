@@ -79,3 +79,51 @@ def test_c_oracle_flow_keys_match_fixtures(oracle_lib, golden, kind, nat_type):
         assert len(want) == len(recs)
         assert [f"{int(x):016x}" for x in h] == [f["hash"] for f in want]
         assert list(map(int, b)) == [f["bucket"][nb_i] for f in want]
+
+
+def _canonical():
+    """tests/golden/xxh3_canonical.npz: values from the canonical xxHash library (gen_golden_xxh3_canonical.py)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "xxh3_canonical.npz"))
+    stream = np.fromfile(os.path.join(ROOT, "tests", "golden", "hash_stream.bin"), dtype=np.uint8)
+    return z, stream
+
+
+def test_c_oracle_equals_canonical_xxhash_every_length_0_to_4096_and_long(oracle_lib):
+    """the C oracle == canonical libxxhash on every length 0..4096 and 300 random
+    lengths up to 9000 (unaligned offsets)."""
+    z, stream = _canonical()
+    got = oracle_lib.xxh3_batch(stream, z["str_off"].astype(np.uint64), z["str_len"])
+    bad = np.nonzero(got != z["str_hash"])[0]
+    assert bad.size == 0, [int(z["str_len"][i]) for i in bad[:8]]
+    assert set(range(4097)) <= set(z["str_len"].tolist()) and int(z["str_len"].max()) <= 9000
+
+
+def test_python_restatement_equals_canonical_xxhash_sample():
+    from oracle import ref_xxh3_py as X
+
+    z, stream = _canonical()
+    b = stream.tobytes()
+    for i in list(range(0, 300)) + list(range(300, len(z["str_len"]), 97)):
+        o, n = int(z["str_off"][i]), int(z["str_len"][i])
+        assert X.xxh3_64(b[o:o + n]) == int(z["str_hash"][i]), n
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("nat_type", [0, 1])
+def test_c_oracle_nat_keys_equal_canonical_xxhash(oracle_lib, golden, kind, nat_type):
+    """The 13-byte NAT keys of the golden frames' records: the key bytes the oracle hashes and the
+    canonical library's hash of them."""
+    from oracle import ref_xxh3_py as X
+    from tests.helpers import golden_arrays
+
+    z, _ = _canonical()
+    sel = (z["flow_kind"] == kind) & (z["flow_nat"] == nat_type)
+    gmeta, blob = golden
+    data, offs, lens, _ = golden_arrays(gmeta, blob)
+    recs, _ = oracle_lib.rx_batch(data, lens, oracle_lib.NetIf.make(), 1, offsets_dw=offs)
+    assert int(sel.sum()) == len(recs)
+    h, _ = oracle_lib.flow_hash_batch(recs, kind, nat_type, 1024)
+    assert np.array_equal(np.asarray(h, np.uint64), z["flow_hash"][sel])
+    for r, key in zip(recs[:64], z["flow_key"][sel][:64]):
+        rec = {k: int(r[k]) for k in ("ip_proto", "src_ip", "dst_ip", "sport", "dport")}
+        assert X.nat_flow_key(rec, kind, nat_type) == key.tobytes()

@@ -189,3 +189,44 @@ def test_fused_parse_flow_hash(dev, oracle_lib, golden, variant):
                 assert np.array_equal(h.cpu().numpy().view(np.uint64), wh), (variant, compact, kind, nat)
                 if buckets:
                     assert np.array_equal(b.cpu().numpy().view(np.uint32), wb)
+
+
+def test_xxh3_canonical_every_length(dev):
+    """halo_xxh3_64_batch_device == the canonical xxHash library (committed values,
+    tests/gen_golden_xxh3_canonical.py) on every length 0..4096 and 300 lengths up to 9000."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "xxh3_canonical.npz"))
+    stream = np.fromfile(os.path.join(ROOT, "tests", "golden", "hash_stream.bin"), dtype=np.uint8)
+    got = _xxh3_dev(dev, stream, z["str_off"].astype(np.uint64), z["str_len"])
+    bad = np.nonzero(got != z["str_hash"])[0]
+    assert bad.size == 0, [int(z["str_len"][i]) for i in bad[:8]]
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("nat_type", [0, 1])
+def test_flow_hash_golden_records_equal_canonical(dev, golden, kind, nat_type):
+    """NAT flow keys of the GPU-parsed golden frames, hashed on the GPU (standalone and fused into
+    the parse) == the canonical library's XXH3 of the 13-byte keys."""
+    import torch
+
+    from halo_amd import _lib, hashcode, protocol
+    from halo_amd._lib import NetIf
+    from tests.helpers import golden_arrays
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "xxh3_canonical.npz"))
+    want = z["flow_hash"][(z["flow_kind"] == kind) & (z["flow_nat"] == nat_type)]
+    meta, blob = golden
+    data, offs, lens, _ = golden_arrays(meta, blob)
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(offs.view(np.int32)).to(dev)
+    ln = torch.from_numpy(lens.view(np.int16)).to(dev)
+    out = protocol.parse_frames_batch(d, o, ln, netif=NetIf.make())
+    h, _ = hashcode.flow_hash(out, kind, nat_type, 0)
+    n = int(ln.numel())
+    rec = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    hf = torch.zeros(n, dtype=torch.int64, device=dev)
+    _lib.check("fused", _lib.lib.halo_rx_parse_flow_batch_device(
+        d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, 1, NetIf.make(), 0, rec.data_ptr(), None, kind, nat_type,
+        hf.data_ptr(), 0, None, torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert np.array_equal(h.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(hf.cpu().numpy().view(np.uint64), want)

@@ -367,6 +367,112 @@ def test_histogram_tree_across_grid_sizes_and_launches(dev, variant):
         assert want[1:].sum() > 0 or n < 64
 
 
+def _hist_batches(dev, specs):
+    """Device batches for the histogram concurrency tests: (frames, expected histogram per parse)."""
+    import torch
+
+    from halo_amd import protocol, synth
+    from halo_amd._lib import NetIf
+
+    out = []
+    for n, length in specs:
+        lay = synth.layout(n, length=length, mutate_shift=3)
+        fr = synth.frames_device(lay, NetIf.make(), device=dev)
+        rec = protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                          max_len_hint=length)
+        torch.cuda.synchronize()
+        want = np.bincount(protocol.records(rec)["status"], minlength=14)
+        assert want[1:].sum() > 0
+        out.append((fr, length, want))
+    return out
+
+
+def test_histogram_tree_two_threads_on_per_thread_stream(dev):
+    """hipStreamPerThread is ONE handle value for a different stream on every host
+    thread, so two threads' histogram-on parses run at once under the same handle. The trees belong
+    to HSA queues (claimed on the device from the dispatch packet's queue, used only under the
+    packet's barrier bit), so two threads x 150 parses each, every thread into its own histogram,
+    must count exactly 150 x the records' statuses."""
+    import ctypes
+    import threading
+
+    import torch
+
+    from halo_amd import _lib
+    from halo_amd._lib import NetIf
+
+    per_thread = ctypes.c_void_p(2)  # hipStreamPerThread
+    hip_sync = _lib.lib.hipStreamSynchronize  # the HIP runtime libhalo_rx.so is linked against
+    hip_sync.restype, hip_sync.argtypes = ctypes.c_int, [ctypes.c_void_p]
+    batches = _hist_batches(dev, [(1 << 18, 64), (70001, 200)])
+    reps = 150
+    hists = [torch.zeros(14, dtype=torch.int32, device=dev) for _ in batches]
+    outs = [torch.empty((fr["lens"].numel(), 32), dtype=torch.uint8, device=dev) for fr, _, _ in batches]
+    netif = NetIf.make()
+    errors = []
+
+    def run(k):
+        try:
+            fr, length, _ = batches[k]
+            for _ in range(reps):
+                rc = _lib.lib.halo_rx_parse_batch_device(
+                    _lib.ptr(fr["bytes"]), _lib.ptr(fr["offsets_dw"]), _lib.ptr(fr["lens"]), fr["lens"].numel(), 1,
+                    netif, length, _lib.ptr(outs[k]), _lib.ptr(hists[k]), per_thread)
+                _lib.check("halo_rx_parse_batch_device", rc)
+            # the thread's own stream: a device-wide sync after the thread has exited does not wait
+            # for its per-thread stream (seen on ROCm 7: counts still rising after it)
+            assert hip_sync(per_thread) == 0
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(len(batches))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    _lib.device_synchronize(0)
+    assert not errors, errors
+    for k, (_, _, want) in enumerate(batches):
+        assert np.array_equal(hists[k].cpu().numpy().astype(np.int64), reps * want), k
+
+
+def test_histogram_tree_graph_replayed_on_two_streams(dev):
+    """a histogram-on parse captured in a hipGraph (no allocation inside the capture:
+    halo_rx_init made the trees) and replayed on two streams at once, several times — both replays of
+    one graph share their arguments, so only the per-queue trees keep them apart. Histogram ==
+    2 x replays x the records' statuses; afterwards an ordinary launch still counts exactly."""
+    import torch
+
+    from halo_amd import protocol
+    from halo_amd._lib import NetIf
+
+    [(fr, length, want)] = _hist_batches(dev, [(1 << 20, 64)])
+    hist = torch.zeros(14, dtype=torch.int32, device=dev)
+    out = torch.empty((fr["lens"].numel(), 32), dtype=torch.uint8, device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                    max_len_hint=length, hist=hist, out=out)
+    torch.cuda.synchronize()
+    hist.zero_()
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    reps = 20
+    for _ in range(reps):
+        with torch.cuda.stream(s1):
+            g.replay()
+        with torch.cuda.stream(s2):
+            g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(hist.cpu().numpy().astype(np.int64), 2 * reps * want)
+    hist.zero_()
+    protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
+                                max_len_hint=length, hist=hist, out=out)
+    torch.cuda.synchronize()
+    assert np.array_equal(hist.cpu().numpy().astype(np.int64), want)
+    del g
+
+
 def test_config5_full_size_4M_9000B(dev, oracle_lib):
     """BASELINE config 5 at full size: 4M x 9000 B TCP, strided, 37.7 GB in one call (frame
     addresses past 2^32 and 2^35). Reference verdict (caps kept): ETH_LEN for every frame. Jumbo

@@ -543,3 +543,38 @@ def test_small_polls_of_changing_sizes(dev, oracle_lib, persistent):
     if persistent:
         assert st["service_requests"] - before["service_requests"] >= served
     cons.close()
+
+
+def test_persistent_consumer_after_small_poll_growth(dev, oracle_lib):
+    """growing the small-poll arrays (halo_rx_ring_set_small_poll above the 4 MiB
+    default on a ring large enough for them to grow) frees the pinned offset / length arrays the
+    resident consumer was created over. The consumer must relaunch over the new ones: ragged polls
+    (42..64 B, read through the arrays) before and after two growths, each == the oracle."""
+    from halo_amd import _lib
+    from halo_amd._lib import NetIf
+    from halo_amd.ring import RingBuffer, RingConsumer
+
+    O = oracle_lib
+    onetif = O.NetIf.make()
+    rng = np.random.default_rng(31)
+    ring = RingBuffer(1 << 24)
+    cons = RingConsumer(ring, capacity=1514, persistent=True)
+    assert cons.max_frames > (4 << 20) // 8  # room for the arrays to grow past the default's
+    for it, small_poll in enumerate([None, 8 << 20, 16 << 20]):
+        if small_poll is not None:
+            _lib.check("halo_rx_ring_set_small_poll", _lib.lib.halo_rx_ring_set_small_poll(cons._h, small_poll))
+        for rep in range(2):
+            k = int(rng.integers(500, 3000))
+            lens = rng.integers(42, 65, size=k).astype(np.uint16)
+            kinds = rng.integers(0, 3, size=k).astype(np.uint8)
+            offs = np.concatenate([[0], np.cumsum((lens.astype(np.int64) + 3) & ~3)[:-1]]).astype(np.uint32) // 4
+            data = O.synth_batch(7000 + 10 * it + rep, 0, lens, kinds, onetif, offsets_dw=offs)
+            assert ring.write_batch(data, offs.astype(np.uint64) * 4, lens) == k
+            want, _ = O.rx_batch(data, lens, onetif, 1, offsets_dw=offs)
+            got, d, _ = cons.poll(NetIf.make())
+            assert d["n_frames"] == k
+            assert_records_equal(got.copy(), want, None, f"growth {it} poll {rep}")
+            cons.commit()
+    st = cons.stats()
+    assert st["service_requests"] >= 6 and st["small_polls"] >= 6, st
+    cons.close()
