@@ -834,8 +834,41 @@ def ring_secondary(dev, netif, steps, warmup, d: Dist, with_cpu: bool = False):
     res["ring_scan_device_1M_64B"] = {
         "records": got_n, "mrecords_per_s": round(n * steps / w / 1e6, 1), "kernel_ms": round(k, 4),
         "roofline": roofline(alg, k, load_traffic("ring_scan_1M_64B")), "alg_bytes_per_launch": alg,
-        "what": "record boundaries of a 68 MB ring span (4 kernels: tile maps by pointer jumping, superblock "
-                "compose, chain, emit)"}
+        "what": "record boundaries of a 68 MB ring span (3 kernels: every tile walks from its guessed entry, "
+                "one workgroup links and verifies the tiles, every tile copies its records out)"}
+    # the same bytes moved by a no-work kernel: the span in, 6 B per record out
+    with_probe(res["ring_scan_device_1M_64B"]["roofline"], size_matched_probe(dev, used, n * 6, d, nbuf=1), k)
+    assert got_n == n, got_n
+    del span, d_off, d_len, ws
+    torch.cuda.empty_cache()
+
+    # (a') the walk over an IMIX ring (64 / 570 / 1500 B 7:4:1, TCP / UDP / ICMP): 256k records, 92 MB
+    ni = 1 << 18
+    fi = make_batches(dev, netif, n=ni, rotate=1, rank=0, size_mode=1, proto_mode=3)[0]
+    li = fi["layout"]
+    hi = fi["bytes"].cpu().numpy()
+    del fi
+    ring_i = RingBuffer(128 << 20)
+    assert ring_i.write_batch(hi, li["offsets_dw"].astype(np.uint64) * 4, li["lens"]) == ni
+    used_i = ring_i.head - ring_i.tail
+    span = torch.from_numpy(ring_i.data[:used_i].copy()).to(dev)
+    del ring_i, hi
+    d_off = torch.empty(ni, dtype=torch.int32, device=dev)
+    d_len = torch.empty(ni, dtype=torch.int16, device=dev)
+    info = torch.zeros(24, dtype=torch.uint8, device=dev)
+    ws_bytes = _lib.lib.halo_rx_ring_scan_workspace(used_i, 1514)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    arr = (ctypes.c_void_p * 1)(span.data_ptr())
+    w, k = time_native(bench_lib().halo_bench_ring_scan_steps, 1, arr, used_i, 128 << 20, 1514, d_off.data_ptr(),
+                       d_len.data_ptr(), info.data_ptr(), ws.data_ptr(), ws_bytes, steps=steps, warmup=warmup, d=d)
+    got_i = int(info.cpu().numpy().view(_lib.RING_SCAN_DTYPE)[0]["n_frames"])
+    assert got_i == ni, got_i
+    alg = used_i + ni * 6
+    res["ring_scan_device_imix_256k"] = {
+        "records": got_i, "mrecords_per_s": round(ni * steps / w / 1e6, 1), "kernel_ms": round(k, 4),
+        "span_bytes": used_i, "roofline": roofline(alg, k, load_traffic("ring_scan_imix_256k")),
+        "alg_bytes_per_launch": alg, "what": "the same walk over a 256k-record IMIX ring (64/570/1500 B 7:4:1)"}
+    with_probe(res["ring_scan_device_imix_256k"]["roofline"], size_matched_probe(dev, used_i, ni * 6, d, nbuf=1), k)
     del span, d_off, d_len, ws
     torch.cuda.empty_cache()
 

@@ -12,19 +12,18 @@
 //
 // Record boundaries on the GPU. Walking records is a chain: the record whose length field is span
 // dword a continues at a + ceil((4 + len) / 4) (u32 length + bytes, 4-byte aligned:
-// mem/ring_buffer.go:47-50) unless ReadPacket would return false there. It is resolved in parallel:
-//   1. tile maps   — the span is cut into 4096-dword tiles. For EVERY dword position of a tile,
-//                    12 rounds of pointer jumping in LDS find where a walk starting there leaves the
-//                    tile (or stops) and how many records it takes. A walk can only enter a tile at
-//                    one of its first W positions (W = dwords of the longest record the receive
-//                    buffer accepts), so those W results are the tile's map.
-//   2. superblocks — the maps of S consecutive tiles are composed (S x W entries staged in LDS).
-//   3. chain       — one workgroup runs the superblock maps from the span's start: the entry and
-//                    the number of records before every superblock.
-//   4. emit        — every tile follows at most S-1 tile maps from its superblock's entry to its
-//                    own, finds its records from that entry by one parallel pass over the links
-//                    of its record positions (a serial walk in LDS only behind a record decoy) and
-//                    writes (dword offset, length).
+// mem/ring_buffer.go:47-50) unless ReadPacket would return false there. It is resolved over
+// 4096-dword tiles by guess and verify:
+//   A. guess  — every tile guesses where the walk enters it (the first position that passes
+//               ReadPacket's checks and whose chain does not stop inside the tile; tile 0: the
+//               span's start), walks from there and keeps its records and a summary;
+//   B. link   — one workgroup checks the guesses by induction from tile 0 (tile t's guess is right
+//               iff the verified walk through tile t - 1 enters t there), walks a tile again from
+//               its real entry where the guess was wrong, and prefix-sums the records;
+//   C. copy   — every tile writes its records as (dword offset, length) at its place.
+// HALO_RING_MAPS=1 builds the previous resolution instead (tile maps of every entry position by
+// pointer jumping, composed into superblocks, chained by one workgroup, expanded back down, then
+// emitted): 0.19 ms against 0.04 for 1M 64 B records, kept for comparison.
 // Every step applies ReadPacket's checks in ReadPacket's order, so the frames taken, the stop and
 // the new tail are those of repeated ReadPacket calls (tests/test_gpu_ring.py, against the oracle,
 // which tests/test_ring_oracle.py checks against the reference's own cgo/ring_buffer.h).
@@ -73,6 +72,9 @@ struct Scan {
     uint2* sb_entry;        // [n_sb]: (entry | kMapStop, records before the superblock)
     uint2* tile_entry;      // [n_tiles]: (entry | kMapStop, records before the tile)
     uint32_t* total;        // records the walk takes before it stops (max_frames ignored)
+    struct RingCtl* ctl;    // (guess path) total and the tile the walk ends in; total aliases it
+    uint2* sum;             // (guess path) [n_tiles]: (guess | exit << 16, records | why << 12 | longest << 16)
+    uint32_t* tmp;          // (guess path) [n_tiles][kTile / 2]: a tile's records, position | length << 16
     halo_rx_ring_scan_t* info;
     uint32_t* off_dw;       // frame i's bytes start at span dword off_dw[i]
     uint16_t* lens;
@@ -276,138 +278,486 @@ __global__ void __launch_bounds__(kThreads) ring_expand_kernel(const uint2* pare
     }
 }
 
-// 5. Emit: one wave per tile. The lanes tabulate every position's next record position (or its
-// stop reason) in LDS and list, in order, the positions from the tile's entry on that pass
-// ReadPacket's checks; one pass over those candidates' links finds the chain (a serial walk, one
-// dependent LDS read per record, only behind a record decoy); the lanes then write the records'
-// (offset, length) pairs.
-constexpr uint32_t kEmitWaves = kThreads / 64;
+// Tile tables. nxt[q]: the position of the record after the one whose length
+// field is tile position q (bits 0-12; >= kTile: the next tile's position + kTile) with that
+// length's low two bits (bits 13-14: with the record's dwords they give the length back), or
+// kLdsStop | ReadPacket's reason when q fails its checks. list: the positions >= lo that pass.
+constexpr uint32_t kListMax = kTile / 2;  // records of >= 2 dwords: at most this many per tile
+constexpr uint32_t kNone = 0xFFFFu;      // tile summary: no position of the tile passes the checks
+constexpr uint32_t kPosMask = 0x1FFFu;   // kTile + W - 1 < 2^13
+constexpr uint32_t kGuessTries = 4;      // chains a tile tries as its guessed entry
+static_assert(kTile + (kMaxCapacity + 7) / 4 <= kPosMask + 1, "nxt positions fit 13 bits");
+
+// The length field of the record at tabulated position q (it passed the checks): its dwords and
+// the low bits kept in nxt[q].
+__device__ __forceinline__ uint32_t nxt_len(uint32_t q, uint32_t v) {
+    const uint32_t dw = (v & kPosMask) - q, r = (v >> 13) & 3u;
+    return ((dw - 1u - (r != 0u)) << 2) | r;
+}
+
+// One tile's tables, shared by the workgroup that walks it (12 KB: eight 4-wave workgroups per CU;
+// a set per wave held the guess kernel at three waves per SIMD, 31 us for 1M 64 B records).
+struct TileTab {
+    uint16_t nxt[kTile];
+    uint16_t list[kListMax];
+    uint32_t part[16];  // per-wave candidate counts, then the first link break
+    uint32_t cq[2];     // the walk's records and end, from the wave that walked serially
+};
+
+// Tabulates tile t (nxt, and list = the positions >= lo that pass, in order) with the whole
+// workgroup of W waves; returns how many pass (list holds the first kListMax). Lane l of wave w
+// takes the 16-byte chunks w * kTile / W + 256 u + 4 l: the tile's bytes are read once, with every
+// load of a lane in flight together.
+template <int W>
+__device__ __forceinline__ uint32_t tile_tabulate(const Scan& s, uint32_t t, TileTab& tb, uint32_t lo) {
+    constexpr uint32_t Q = kTile / (W * 256);  // 16-byte chunks per lane
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t tbase = t * kTile, wbase = w * (kTile / W);
+    uint4 v[Q];
+    if (tbase + kTile <= s.n_dw) {  // uniform
+#pragma unroll
+        for (uint32_t u = 0; u < Q; ++u) {
+            const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + tbase + wbase + 256 * u + 4 * lane);
+            v[u] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    } else {
+#pragma unroll
+        for (uint32_t u = 0; u < Q; ++u) v[u] = span_quad(s, tbase + wbase + 256 * u + 4 * lane);
+    }
+    uint32_t mine[Q];  // bit j: position q + j holds a record and is at or past lo
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < Q; ++u) {
+        const uint32_t q = wbase + 256 * u + 4 * lane;
+        const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        uint32_t nx[4];
+        mine[u] = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t why;
+            const uint32_t step = record_dwords(s, tbase + q + j, d[j], why);
+            nx[j] = step ? (q + j + step) | ((d[j] & 3u) << 13) : (kLdsStop | why);
+            mine[u] |= (step && q + j >= lo) ? 1u << j : 0u;
+        }
+        *reinterpret_cast<uint2*>(&tb.nxt[q]) = make_uint2(nx[0] | (nx[1] << 16), nx[2] | (nx[3] << 16));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cnt += (uint32_t)__popcll(__ballot((mine[u] >> j) & 1u));
+    }
+    if (lane == 0) tb.part[w] = cnt;
+    __syncthreads();
+    uint32_t n_act = 0, k = 0;  // this wave's first list slot: the candidates of the waves before
+#pragma unroll
+    for (uint32_t x = 0; x < (uint32_t)W; ++x) {
+        k += x < w ? tb.part[x] : 0u;
+        n_act += tb.part[x];
+    }
+    // ordered compaction (wave, then chunk, then lane, then j)
+#pragma unroll
+    for (uint32_t u = 0; u < Q; ++u) {
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t b = __ballot((mine[u] >> j) & 1u);
+            before += lane_rank(b);
+            total += (uint32_t)__popcll(b);
+        }
+        const uint32_t q = wbase + 256 * u + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t slot = k + before + (uint32_t)__builtin_popcount(mine[u] & ((1u << j) - 1u));
+            if (((mine[u] >> j) & 1u) && slot < kListMax) tb.list[slot] = (uint16_t)(q + j);
+        }
+        k += total;
+    }
+    __syncthreads();
+    return n_act;
+}
+
+// The first "break" at list index >= i0: the first listed candidate whose link does not reach the
+// next listed one (the last one always breaks). The chain through the listed candidates from
+// list[i0] is list[i0..F]; it goes on at nxt[list[F]].
+template <int W>
+__device__ __forceinline__ uint32_t first_break(TileTab& tb, uint32_t n_act, uint32_t i0) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    uint32_t f = ~0u;
+    for (uint32_t i = i0 + tid; i < n_act; i += 64 * W)
+        if ((tb.nxt[tb.list[i]] & kPosMask) != (i + 1 < n_act ? tb.list[i + 1] : 0xFFFFu)) {
+            f = i;
+            break;
+        }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) f = min(f, (uint32_t)__shfl_xor((int)f, m, 64));
+    if (lane == 0) tb.part[w] = f;
+    __syncthreads();
+    uint32_t F = n_act - 1;
+#pragma unroll
+    for (uint32_t x = 0; x < (uint32_t)W; ++x) F = min(F, tb.part[x]);
+    __syncthreads();  // part is rewritten by the next call
+    return F;
+}
+
+// The walk through a tabulated tile from `entry` = list[i0] (or a position that fails the checks
+// or is not listed: then it takes nothing), by the whole workgroup: list[i0 .. i0 + c) become its
+// records (at most `limit`) and q the position after the last one (>= kTile: it continues in the
+// next tile; < kTile: it stops there, nxt[q] says why). Fast path: in ring data the positions that
+// pass ReadPacket's checks are, almost always, exactly the record starts, each linking to the
+// next, so the walk is list[i0..F] — found by one parallel pass over the links instead of one
+// dependent LDS read per record. A position that passes the checks but is not on the chain (a
+// record decoy in a payload) shows up as a link that skips over it; wave 0 then walks serially from
+// where the links end.
+struct TileWalk {
+    uint32_t c, q;
+};
+template <int W>
+__device__ __forceinline__ TileWalk tile_walk(TileTab& tb, uint32_t n_act, uint32_t i0, uint32_t entry,
+                                              uint32_t limit) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    uint32_t c = 0, q = entry;
+    bool serial = n_act > kListMax;  // too many candidates to list: walk serially from the entry
+    if (!serial && i0 < n_act && tb.list[i0] == entry) {  // uniform
+        const uint32_t F = first_break<W>(tb, n_act, i0), M = F + 1 - i0;
+        c = min(M, limit);
+        q = c < M ? tb.list[i0 + c] : tb.nxt[tb.list[F]] & kPosMask;
+        // the chain goes on at a position past a decoy: continue serially from there
+        serial = c == M && c < limit && q < kTile && !(tb.nxt[q] & kLdsStop);
+    }
+    if (serial) {  // uniform
+        if (w == 0) {
+            // the lanes follow the same chain (values made scalar): uniform control flow around one
+            // dependent LDS read per record
+            while (c < limit && q < kTile) {
+                const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)tb.nxt[q]);
+                if (v & kLdsStop) break;
+                tb.list[i0 + c++] = (uint16_t)q;
+                q = v & kPosMask;
+            }
+            if (lane == 0) {
+                tb.cq[0] = c;
+                tb.cq[1] = q;
+            }
+        }
+        __syncthreads();
+        c = tb.cq[0];
+        q = tb.cq[1];
+    }
+    __syncthreads();  // cq / list are reused by the caller's next tile
+    return TileWalk{c, q};
+}
+
+__device__ __forceinline__ uint32_t len_dwords(uint32_t len) { return (len >> 2) + 1u + ((len & 3u) != 0u); }
+
+// (maps path) 5. Emit: one workgroup per tile, from its entry (ring_expand_kernel): the walk
+// through the tile and the records' (offset, length) pairs.
+constexpr uint32_t kTileWaves = kThreads / 64;
 __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
-    __shared__ __align__(8) uint16_t nxt[kEmitWaves][kTile];
-    __shared__ uint16_t list[kEmitWaves][kTile / 2];
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t t = blockIdx.x * kEmitWaves + w;
-    if (t >= s.n_tiles) return;  // wave-uniform
+    __shared__ TileTab tb;
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
     const uint32_t n = s.info->n_frames;
     const uint2 te = s.tile_entry[t];
     const uint32_t entry = te.x, base = te.y;
-    if (entry == kMapStop || base > n) return;  // wave-uniform
-    const uint32_t tbase = t * kTile;
-    uint32_t n_act = 0;  // positions at or past the entry that pass ReadPacket's checks
-    // the wave's 16 KB in two rounds of eight 16-byte loads in flight per lane
-    const bool whole = tbase + kTile <= s.n_dw;  // wave-uniform
-    for (uint32_t r0 = 0; r0 < kTile; r0 += 8 * 4 * 64) {
-        uint4 v[8];
-        if (whole) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + tbase + r0 + 4 * (lane + 64 * u));
-                v[u] = make_uint4(x.x, x.y, x.z, x.w);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = span_quad(s, tbase + r0 + 4 * (lane + 64 * u));
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t q = r0 + 4 * (lane + 64 * u);
-            const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-            uint32_t mine = 0;  // bit j: position q + j holds a record and is at or past the entry
-            uint32_t nx[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint32_t why;
-                const uint32_t step = record_dwords(s, tbase + q + j, d[j], why);
-                nx[j] = step ? q + j + step : (kLdsStop | why);
-                mine |= (step && q + j >= entry) ? 1u << j : 0u;
-            }
-            *reinterpret_cast<uint2*>(&nxt[w][q]) = make_uint2(nx[0] | (nx[1] << 16), nx[2] | (nx[3] << 16));
-            // ordered compaction of those positions (block order, then lane, then j)
-            uint32_t before = 0, total = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint64_t b = __ballot((mine >> j) & 1u);
-                before += lane_rank(b);
-                total += (uint32_t)__popcll(b);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = n_act + before + (uint32_t)__builtin_popcount(mine & ((1u << j) - 1u));
-                if (((mine >> j) & 1u) && k < kTile / 2) list[w][k] = (uint16_t)(q + j);
-            }
-            n_act += total;
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t limit = min(n - base, kTile / 2);  // records this tile may still take
-    uint32_t c = 0, q = entry;
-    // Fast path: in ring data the positions that pass ReadPacket's checks are, almost always,
-    // exactly the record starts. If the k-th such position from the entry on links to the
-    // (k+1)-th for k < F and the F-th does not, the walk is those F + 1 records — found by one
-    // parallel pass over the links instead of one dependent LDS read per record. A position that
-    // passes the checks but is not on the chain (a record decoy in a payload) shows up as a link
-    // that skips over it; the serial walk then takes over from where the links end.
-    bool serial = n_act > kTile / 2;  // too many candidates to list: walk serially from the entry
-    if (!serial && n_act && list[w][0] == entry) {
-        uint32_t F = n_act - 1;  // the last candidate's link always "fails" (no successor listed)
-        for (uint32_t i0 = 0; i0 < n_act; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            bool brk = false;
-            if (i < n_act) brk = nxt[w][list[w][i]] != (i + 1 < n_act ? list[w][i + 1] : 0xFFFFu);
-            const uint64_t b = __ballot(brk);
-            if (b) {
-                F = i0 + (uint32_t)__builtin_ctzll(b);
-                break;
-            }
-        }
-        const uint32_t M = F + 1;
-        c = min(M, limit);
-        q = c < M ? list[w][c] : nxt[w][list[w][F]];
-        // the chain goes on at a position past a decoy: continue serially from there
-        serial = c == M && c < limit && q < kTile && !(nxt[w][q] & kLdsStop);
-    } else if (!serial) {
-        c = 0;
-        q = entry;  // the entry itself fails ReadPacket's checks (or the tile has no record)
-    } else {
-        c = 0;
-        q = entry;
-    }
-    if (serial) {
-        // every lane follows the same chain (values made scalar): uniform control flow around
-        // one dependent LDS read per record
-        while (c < limit && q < kTile) {
-            const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt[w][q]);
-            if (v & kLdsStop) break;
-            list[w][c++] = (uint16_t)q;
-            q = v;
-        }
-    }
-    uint32_t v = q < kTile ? nxt[w][q] : 0u;
-    if (lane == 0) {
+    if (entry == kMapStop || base > n) return;  // uniform
+    const uint32_t n_act = tile_tabulate<kTileWaves>(s, t, tb, entry);
+    const TileWalk wk = tile_walk<kTileWaves>(tb, n_act, 0, entry, min(n - base, kListMax));
+    const uint32_t c = wk.c, q = wk.q, tbase = t * kTile;
+    if (tid == 0) {
+        const uint32_t v = q < kTile ? tb.nxt[q] : 0u;
         if (base + c == n && c) s.info->end_bytes = 4ull * (tbase + q);
         // where the walk ends inside this tile: say why, unless max_frames cut it (MAX, set)
         if (q < kTile && n == *s.total && (v & kLdsStop)) s.info->stop = v & 0xFFu;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
     uint32_t max_len = 0;
-    for (uint32_t j = lane; j < c; j += 64) {
-        const uint32_t a = tbase + list[w][j];
-        const uint32_t len = s.span[a];
-        s.off_dw[base + j] = a + 1;
+    for (uint32_t j = tid; j < c; j += kThreads) {
+        const uint32_t e = tb.list[j], len = nxt_len(e, tb.nxt[e]);
+        s.off_dw[base + j] = tbase + e + 1;
         s.lens[base + j] = (uint16_t)len;
         max_len = max(max_len, len);
     }
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) max_len = max(max_len, (uint32_t)__shfl_xor((int)max_len, m, 64));
-    if (lane == 0 && max_len) atomicMax(&s.info->max_len, max_len);
+    if ((tid & 63u) == 0 && max_len) atomicMax(&s.info->max_len, max_len);
 }
+
+// ---- the record walk by guess and verify (the default) ------------------------------------------
+// A. Every tile guesses its entry — the first position that passes ReadPacket's checks (tile 0:
+//    the span's start) — walks from it (tile_walk) and keeps the records it found in its slot of
+//    the workspace, with a summary: (guess, where the walk leaves or stops, records, why, longest).
+// B. One workgroup links the summaries: tile t's guess is right when the walk through tile t - 1
+//    (itself verified) enters tile t there. By induction from tile 0 every guess that matches is
+//    the real entry, so a chunk of 32768 tiles is settled by one comparison per tile and a prefix
+//    sum; a tile whose guess is wrong (a decoy in the record that straddles its start) is walked
+//    again by the workgroup from its real entry, and the linking goes on after it.
+// C. Every tile copies its records to (dword offset, length) at its place in the batch.
+// Three launches, each tile read once (the map path it replaces: seven launches and a serial chain
+// of map lookups between them, 0.19 ms for 1M 64 B records, profiles/r05/r5f).
+struct RingCtl {
+    uint32_t total;      // records the walk takes before it stops (max_frames ignored)
+    uint32_t last_tile;  // the tile the walk ends in
+};
+
+// A tile's walk into its workspace slot (position | length << 16) and its longest record.
+__device__ __forceinline__ uint32_t keep_records(const Scan& s, uint32_t t, const TileTab& tb, uint32_t i0,
+                                                 uint32_t c) {
+    uint32_t* tmp = s.tmp + (uint64_t)t * kListMax;
+    uint32_t mx = 0;
+    for (uint32_t j = threadIdx.x; j < c; j += blockDim.x) {
+        const uint32_t e = tb.list[i0 + j], len = nxt_len(e, tb.nxt[e]);
+        tmp[j] = e | (len << 16);
+        mx = max(mx, len);
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, m, 64));
+    return mx;  // the wave's
+}
+
+__global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
+    __shared__ TileTab tb;
+    __shared__ uint32_t s_mx[kTileWaves];
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    const uint32_t n_act = tile_tabulate<kTileWaves>(s, t, tb, 0);
+    // The guess: the first listed candidate whose chain of links does not stop inside the tile. The
+    // dword before a record is often a decoy — a frame's last bytes and zero padding make a small
+    // "length" (1.3 % of IMIX tiles, tools: a 570 B frame's last dword) — whose link lands nowhere;
+    // such a chain is skipped. If every try stops, the first candidate (the walk may really stop).
+    uint32_t i0 = 0;
+    if (t > 0 && n_act <= kListMax) {
+        for (uint32_t k = 0, tries = 0; k < n_act && tries < kGuessTries; ++tries) {  // uniform
+            const uint32_t F = first_break<kTileWaves>(tb, n_act, k), q = tb.nxt[tb.list[F]] & kPosMask;
+            if (!(q < kTile && (tb.nxt[q] & kLdsStop))) {
+                i0 = k;
+                break;
+            }
+            k = F + 1;
+        }
+    }
+    const uint32_t g = t == 0 ? 0u : n_act ? tb.list[i0] : kNone;
+    TileWalk wk{0, kNone};
+    if (g != kNone) wk = tile_walk<kTileWaves>(tb, n_act, i0, g, kListMax);  // uniform (tile 0: i0 = 0)
+    const uint32_t mx = keep_records(s, t, tb, i0, wk.c);
+    if ((tid & 63u) == 0) s_mx[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t m = 0;
+        for (uint32_t x = 0; x < kTileWaves; ++x) m = max(m, s_mx[x]);
+        const uint32_t why = wk.q < kTile ? tb.nxt[wk.q] & 0xFFu : 0u;
+        s.sum[t] = make_uint2(g | (wk.q << 16), wk.c | (why << 12) | (m << 16));
+    }
+}
+
+constexpr uint32_t kLinkThreads = 1024, kLinkWaves = kLinkThreads / 64, kLinkPer = 32;  // 512 MB spans in one pass
+constexpr uint32_t kLinkChunk = kLinkThreads * kLinkPer;
+
+__global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
+    __shared__ TileTab tb;
+    __shared__ uint32_t s_min[kLinkWaves], s_sum[kLinkWaves];
+    __shared__ uint32_t s_fix[4];  // the special tile's records, exit, why, longest record
+    __shared__ uint32_t s_cut[2];  // the tile (and records before it) max_frames cuts inside
+    __shared__ uint32_t s_last_q;  // the exit of the chunk's last tile
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t mf = s.max_frames;
+    // uniform state: the first tile not linked yet, its entry, the records before it
+    uint32_t lo = 0, e = 0, base = 0;
+    uint32_t why = HALO_RING_STOP_EMPTY, last = 0;
+    uint32_t mx = 0;  // the longest record of this thread's tiles that lie wholly before max_frames
+    bool done = false;
+    if (tid == 0) s_cut[0] = ~0u;
+    // a tile's records counted into the batch: all of them, the first ones (max_frames cuts inside
+    // it: its longest comes from its records at the end), or none
+    auto account = [&](uint32_t j, uint32_t b, uint32_t c, uint32_t m) {
+        if (b + c <= mf) mx = max(mx, m);
+        else if (b < mf) {
+            s_cut[0] = j;
+            s_cut[1] = b;
+        }
+    };
+    while (!done) {
+        // a chunk of kLinkChunk tiles from lo; thread tid holds tiles j0 .. j0 + kLinkPer - 1 and a
+        // mask of those that cannot be passed on their summary ("special": the entry the tile
+        // before leads to is not the guess, the walk stops inside, or the span's last tile)
+        const uint32_t t0 = lo, j0 = t0 + tid * kLinkPer;
+        uint2 sm[kLinkPer];
+        if (j0 + kLinkPer <= s.n_tiles && !(reinterpret_cast<uintptr_t>(s.sum) & 15u)) {  // two summaries a load
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkPer; k += 2) {
+                const uint4 v = *reinterpret_cast<const uint4*>(s.sum + j0 + k);
+                sm[k] = make_uint2(v.x, v.y);
+                sm[k + 1] = make_uint2(v.z, v.w);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkPer; ++k) sm[k] = j0 + k < s.n_tiles ? s.sum[j0 + k] : make_uint2(kNone, 0u);
+        }
+        uint32_t prev_q = 0;
+        if (j0 > t0 && j0 <= s.n_tiles) prev_q = s.sum[j0 - 1].x >> 16;
+        uint32_t mask = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kLinkPer; ++k) {
+            const uint32_t j = j0 + k, g = sm[k].x & 0xFFFFu, q = sm[k].x >> 16;
+            const uint32_t in = j == t0 ? e : prev_q - kTile;  // wraps (no match) when prev_q < kTile
+            if (j >= s.n_tiles || in != g || q < kTile || j == s.n_tiles - 1) mask |= 1u << k;
+            prev_q = q;
+        }
+        if (tid == kLinkThreads - 1) s_last_q = prev_q;
+        for (;;) {
+            // J: the first special tile at or after lo (none: the chunk's tiles from lo all pass)
+            uint32_t mm = lo <= j0 ? mask : lo - j0 < kLinkPer ? mask & (~0u << (lo - j0)) : 0u;
+            uint32_t first = mm ? j0 + (uint32_t)__builtin_ctz(mm) : ~0u;
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) first = min(first, (uint32_t)__shfl_xor((int)first, m, 64));
+            if (lane == 0) s_min[wv] = first;
+            __syncthreads();
+            uint32_t J = ~0u;
+            for (uint32_t k = 0; k < kLinkWaves; ++k) J = min(J, s_min[k]);
+            // the tiles in [lo, J): records before each, by an exclusive prefix over the block
+            uint32_t cnt = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkPer; ++k) cnt += j0 + k >= lo && j0 + k < J ? sm[k].y & 0xFFFu : 0u;
+            uint32_t x = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+                if (lane >= (uint32_t)o) x += y;
+            }
+            if (lane == 63) s_sum[wv] = x;
+            // J's summary and the exit of the tile before it, from the threads that hold them
+            if (J != ~0u) {
+#pragma unroll
+                for (uint32_t k = 0; k < kLinkPer; ++k) {
+                    if (j0 + k == J) {
+                        s_fix[0] = sm[k].x;
+                        s_fix[1] = sm[k].y;
+                    }
+                    if (j0 + k + 1 == J) s_fix[2] = sm[k].x >> 16;
+                }
+            }
+            __syncthreads();
+            uint32_t off = 0, total = 0;
+            for (uint32_t k = 0; k < kLinkWaves; ++k) {
+                if (k < wv) off += s_sum[k];
+                total += s_sum[k];
+            }
+            uint32_t b = base + off + x - cnt;
+#pragma unroll
+            for (uint32_t k = 0; k < kLinkPer; ++k) {
+                const uint32_t j = j0 + k, c = sm[k].y & 0xFFFu;
+                if (j >= lo && j < J) {
+                    s.tile_entry[j] = make_uint2(b, c);
+                    account(j, b, c, sm[k].y >> 16);
+                    b += c;
+                }
+            }
+            base += total;
+            if (J == ~0u) {  // through to the chunk's end: the next chunk starts where its last tile leads
+                e = s_last_q - kTile;
+                lo = t0 + kLinkChunk;
+                __syncthreads();
+                break;
+            }
+            const uint32_t jin = J == lo ? e : s_fix[2] - kTile;  // J's real entry
+            const uint2 sj = make_uint2(s_fix[0], s_fix[1]);
+            __syncthreads();  // s_fix / s_min / s_sum are rewritten below
+            if ((sj.x & 0xFFFFu) == jin) {  // uniform. The guess was right: the walk stops in J, or J is the last tile
+                if (tid == 0) {
+                    s_fix[0] = sj.y & 0xFFFu;
+                    s_fix[1] = sj.x >> 16;
+                    s_fix[2] = (sj.y >> 12) & 0xFu;
+                    s_fix[3] = sj.y >> 16;
+                }
+            } else {  // a decoy led the guess astray: walk J again from its real entry
+                const uint32_t n_act = tile_tabulate<kLinkWaves>(s, J, tb, jin);
+                const TileWalk wk = tile_walk<kLinkWaves>(tb, n_act, 0, jin, kListMax);
+                const uint32_t m = keep_records(s, J, tb, 0, wk.c);
+                if (lane == 0) s_min[wv] = m;
+                __syncthreads();
+                if (tid == 0) {
+                    uint32_t mm2 = 0;
+                    for (uint32_t k = 0; k < kLinkWaves; ++k) mm2 = max(mm2, s_min[k]);
+                    s_fix[0] = wk.c;
+                    s_fix[1] = wk.q;
+                    s_fix[2] = wk.q < kTile ? tb.nxt[wk.q] & 0xFFu : 0u;
+                    s_fix[3] = mm2;
+                }
+            }
+            __syncthreads();
+            const uint32_t c = s_fix[0], q = s_fix[1];
+            if (tid == 0) {
+                s.tile_entry[J] = make_uint2(base, c);
+                account(J, base, c, s_fix[3]);
+            }
+            base += c;
+            if (q < kTile || J == s.n_tiles - 1) {  // stopped in J, or left the span (EMPTY)
+                why = q < kTile ? s_fix[2] : HALO_RING_STOP_EMPTY;
+                last = J;
+                done = true;
+                break;
+            }
+            lo = J + 1;
+            e = q - kTile;
+            // the tile after J now has a known entry: is it special with it?
+            if (lo >= j0 && lo < j0 + kLinkPer) {
+                const uint32_t k = lo - j0, g = sm[k].x & 0xFFFFu, qq = sm[k].x >> 16;
+                const bool sp = lo >= s.n_tiles || e != g || qq < kTile || lo == s.n_tiles - 1;
+                mask = sp ? mask | (1u << k) : mask & ~(1u << k);
+            }
+            __syncthreads();  // s_fix is rewritten by the next round
+            if (lo >= t0 + kLinkChunk) break;  // the chunk is used up: the next one starts at lo
+        }
+    }
+    // the longest record taken: every whole tile's, and the cut tile's records before max_frames
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, m, 64));
+    __syncthreads();
+    if (lane == 0) s_min[wv] = mx;
+    uint32_t mc = 0;
+    if (s_cut[0] != ~0u) {
+        const uint32_t* tmp = s.tmp + (uint64_t)s_cut[0] * kListMax;
+        for (uint32_t j = tid; j < mf - s_cut[1]; j += kLinkThreads) mc = max(mc, tmp[j] >> 16);
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
+    if (lane == 0) s_sum[wv] = mc;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t m = 0;
+        for (uint32_t k = 0; k < kLinkWaves; ++k) m = max(m, max(s_min[k], s_sum[k]));
+        const uint32_t n = min(base, mf);
+        s.ctl->total = base;
+        s.ctl->last_tile = last;
+        halo_rx_ring_scan_t info;
+        info.n_frames = n;
+        info.stop = n < base ? HALO_RING_STOP_MAX : why;
+        info.end_bytes = 0;  // C: the position after record n - 1
+        info.max_len = m;
+        info.pad = 0;
+        *s.info = info;
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) ring_copy_kernel(const Scan s) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t t = blockIdx.x * kTileWaves + w;
+    if (t > s.ctl->last_tile) return;  // wave-uniform: tiles past the walk's end hold nothing
+    const uint32_t n = s.info->n_frames;
+    const uint2 te = s.tile_entry[t];
+    const uint32_t base = te.x;
+    if (base >= n) return;
+    const uint32_t cnt = min(te.y, n - base), tbase = t * kTile;
+    const uint32_t* tmp = s.tmp + (uint64_t)t * kListMax;
+    for (uint32_t j = lane; j < cnt; j += 64) {
+        const uint32_t v = tmp[j], pos = v & 0xFFFFu, len = v >> 16;
+        s.off_dw[base + j] = tbase + pos + 1;
+        s.lens[base + j] = (uint16_t)len;
+        if (base + j == n - 1) s.info->end_bytes = 4ull * (tbase + pos + len_dwords(len));
+    }
+}
+
+#ifndef HALO_RING_MAPS
+#define HALO_RING_MAPS 0  // 1: the tile-map walk (pointer jumping, compose, chain, expand, emit)
+#endif
 
 struct Geom {
     uint32_t n_dw, n_tiles, W, S, n_sb, n_ss;
     uint64_t tile_map_off, sb_map_off, ss_map_off, ss_entry_off, sb_entry_off, tile_entry_off, total_off, bytes;
+    uint64_t sum_off, tmp_off;
 };
 
 Geom geometry(uint64_t used, uint32_t cap) {
@@ -419,12 +769,19 @@ Geom geometry(uint64_t used, uint32_t cap) {
     g.n_sb = (g.n_tiles + g.S - 1) / g.S;
     g.n_ss = (g.n_sb + g.S - 1) / g.S;
     uint64_t o = 0;
-    g.tile_map_off = o;
-    o += (uint64_t)g.n_tiles * g.W * sizeof(uint2);
-    g.sb_map_off = o;
-    o += (uint64_t)g.n_sb * g.W * sizeof(uint2);
-    g.ss_map_off = o;
-    o += (uint64_t)g.n_ss * g.W * sizeof(uint2);
+    if (HALO_RING_MAPS) {
+        g.tile_map_off = o;
+        o += (uint64_t)g.n_tiles * g.W * sizeof(uint2);
+        g.sb_map_off = o;
+        o += (uint64_t)g.n_sb * g.W * sizeof(uint2);
+        g.ss_map_off = o;
+        o += (uint64_t)g.n_ss * g.W * sizeof(uint2);
+    } else {
+        g.sum_off = o;
+        o += (uint64_t)g.n_tiles * sizeof(uint2);
+        g.tmp_off = o;
+        o += (uint64_t)g.n_tiles * kListMax * sizeof(uint32_t);
+    }
     g.ss_entry_off = o;
     o += (uint64_t)g.n_ss * sizeof(uint2);
     g.sb_entry_off = o;
@@ -458,19 +815,26 @@ Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_
     s.sb_entry = reinterpret_cast<uint2*>(ws + g.sb_entry_off);
     s.tile_entry = reinterpret_cast<uint2*>(ws + g.tile_entry_off);
     s.total = reinterpret_cast<uint32_t*>(ws + g.total_off);
+    s.ctl = reinterpret_cast<RingCtl*>(ws + g.total_off);
+    s.sum = reinterpret_cast<uint2*>(ws + g.sum_off);
+    s.tmp = reinterpret_cast<uint32_t*>(ws + g.tmp_off);
     s.info = d_info;
     s.off_dw = d_off;
     s.lens = d_len;
     return s;
 }
 
-int launch_tile_maps(const Scan& s, uint32_t t0, uint32_t t1, hipStream_t st) {
-    if (t1 > t0) hipLaunchKernelGGL(ring_tile_map_kernel, dim3(t1 - t0), dim3(kThreads), 0, st, s, t0);
-    return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
-}
-
-int launch_finish(const Scan& s, hipStream_t st) {
+// The record walk of a span: tile maps, composed and chained (HALO_RING_MAPS), or the guess /
+// link / copy kernels.
+int launch_walk(const Scan& s, hipStream_t st) {
     const dim3 blk(kThreads);
+    if (!HALO_RING_MAPS) {
+        hipLaunchKernelGGL(ring_guess_kernel, dim3(s.n_tiles), blk, 0, st, s);
+        hipLaunchKernelGGL(ring_link_kernel, dim3(1), dim3(kLinkThreads), 0, st, s);
+        hipLaunchKernelGGL(ring_copy_kernel, dim3((s.n_tiles + kTileWaves - 1) / kTileWaves), blk, 0, st, s);
+        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+    }
+    hipLaunchKernelGGL(ring_tile_map_kernel, dim3(s.n_tiles), blk, 0, st, s, 0u);
     hipLaunchKernelGGL(ring_compose_kernel, dim3(s.n_sb), blk, 0, st, s.tile_map, s.n_tiles, s.sb_map, s.W, s.S);
     hipLaunchKernelGGL(ring_compose_kernel, dim3(s.n_ss), blk, 0, st, s.sb_map, s.n_sb, s.ss_map, s.W, s.S);
     hipLaunchKernelGGL(ring_chain_kernel, dim3(1), blk, 0, st, s);
@@ -478,7 +842,7 @@ int launch_finish(const Scan& s, hipStream_t st) {
                        s.sb_map, s.n_sb, s.sb_entry, s.W, s.S);
     hipLaunchKernelGGL(ring_expand_kernel, dim3((s.n_sb + kThreads - 1) / kThreads), blk, 0, st, s.sb_entry, s.n_sb,
                        s.tile_map, s.n_tiles, s.tile_entry, s.W, s.S);
-    hipLaunchKernelGGL(ring_emit_kernel, dim3((s.n_tiles + kEmitWaves - 1) / kEmitWaves), dim3(kThreads), 0, st, s);
+    hipLaunchKernelGGL(ring_emit_kernel, dim3(s.n_tiles), dim3(kThreads), 0, st, s);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 
@@ -688,8 +1052,7 @@ extern "C" HALO_API int halo_rx_ring_scan_device(const uint8_t* d_span, uint64_t
         return hipMemsetAsync(d_info, 0, sizeof(halo_rx_ring_scan_t), st) == hipSuccess ? HALO_OK : HALO_E_HIP;
     const Scan s = halo::make_scan(g, d_span, ring_size, capacity, max_frames ? max_frames : 0xFFFFFFFFu,
                                    static_cast<uint8_t*>(d_workspace), d_info, d_offsets_dw, d_lens);
-    if ((rc = halo::launch_tile_maps(s, 0, g.n_tiles, st))) return rc;
-    return halo::launch_finish(s, st);
+    return halo::launch_walk(s, st);
 }
 
 // The walk + parse stream, at the device's highest priority: its workgroups are placed ahead of
@@ -833,7 +1196,7 @@ extern "C" HALO_API int halo_rx_ring_poll(halo_rx_ring_t* r, uint32_t flags, con
         const Geom g = halo::geometry(avail, r->cap);
         const Scan sc = halo::make_scan(g, r->d_span + off, r->size, r->cap, r->max_frames - done, r->d_ws, r->d_info,
                                         r->d_off + done, r->d_len + done);
-        if ((rc = halo::launch_tile_maps(sc, 0, g.n_tiles, r->s_comp)) || (rc = halo::launch_finish(sc, r->s_comp))) break;
+        if ((rc = halo::launch_walk(sc, r->s_comp))) break;
         if (hipMemcpyAsync(r->h_info, r->d_info, sizeof *info, hipMemcpyDeviceToHost, r->s_comp) != hipSuccess ||
             hipStreamSynchronize(r->s_comp) != hipSuccess) { rc = HALO_E_HIP; break; }
         const halo_rx_ring_scan_t pi = *r->h_info;

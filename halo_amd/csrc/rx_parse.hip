@@ -314,6 +314,9 @@ constexpr int kRound0 = G == 8 ? HALO_RX_R0_G8 : 4;
 #ifndef HALO_RX_LATER_NT_G
 #define HALO_RX_LATER_NT_G 16
 #endif
+#ifndef HALO_RX_GROUP_XCD
+#define HALO_RX_GROUP_XCD 0  // measurement knob: XCD-contiguous block order in the group kernels
+#endif
 template <int G, int R0 = kRound0<G>>
 struct FrameState {
     static constexpr int kR0 = R0;
@@ -581,7 +584,15 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp_base = lane & ~(uint32_t)(G - 1);
     // frame indices fit in 32 bits (n is a u32): 32-bit loop state keeps the SGPR budget low
+#if HALO_RX_GROUP_XCD
+    // blocks are dealt round-robin over the 8 XCDs: give each XCD one contiguous range of the batch,
+    // so that the line two neighbouring waves' frames share is fetched into one L2 only
+    const uint32_t nb = gridDim.x, per = nb >> 3, rem = nb & 7u, xcd = blockIdx.x & 7u;
+    const uint32_t lblock = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (blockIdx.x >> 3);
+    const uint32_t wave = (lblock * blockDim.x + threadIdx.x) >> 6;
+#else
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+#endif
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t base = wave * FPW; base < p.n; base += nwaves * FPW) {
         const uint32_t i = base + lane / G;

@@ -54,7 +54,7 @@ struct BuildParams {
     uint16_t* lens;
     uint8_t* result;
     uint16_t* ip_id;
-    uint32_t* ws;                 // [0] rejections in the batch, [1 + t] rejections before / in tile t
+    uint32_t* ws;                 // [0] the seq of the last launch that saw a rejection, [1 + t] tile t's rejections
     uint32_t n, n_tiles, flags, stride;
     uint32_t mac_lo, mac_hi;      // the NetIf's MAC (BuildEthFrm srcMac), little-endian packed
     uint32_t seq;                 // this launch's sequence number (ws[0] = seq: a tile saw a rejection)
@@ -939,6 +939,13 @@ extern "C" HALO_API int halo_tx_build_batch_device(const halo_tx_build_desc_t* d
         hipLaunchKernelGGL((halo::tx_build_pair_kernel<HALO_TXB_BIG_U>),
                            dim3((uint32_t)(((uint64_t)n + 511u) / 512u * 64u)), blk, 0, s, p);  // runs of 8 tiles
     else hipLaunchKernelGGL((halo::tx_build_kernel<HALO_TXB_BIG_G, HALO_TXB_BIG_U>), grid, blk, 0, s, p);
-    hipLaunchKernelGGL(halo::tx_finish_kernel, dim3(p.n_tiles < 64u ? p.n_tiles : 64u), dim3(1024), 0, s, p);
+    // Launch 2 (one word in the common case) costs the same with 1, 8 or 64 blocks (25.2 / 25.2 /
+    // 25.0 us per 64 B call, profiles/r05/r5j): the gap between two dependent dispatches, not the
+    // grid. 64 keeps the renumbering after a rejection wide.
+#ifndef HALO_TXB_FINISH_BLOCKS
+#define HALO_TXB_FINISH_BLOCKS 64u
+#endif
+    hipLaunchKernelGGL(halo::tx_finish_kernel, dim3(p.n_tiles < HALO_TXB_FINISH_BLOCKS ? p.n_tiles : HALO_TXB_FINISH_BLOCKS),
+                       dim3(1024), 0, s, p);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }

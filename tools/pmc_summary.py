@@ -57,6 +57,10 @@ def alg_bytes():
             flen = max(60, 42 + plen)
             out[name] = ((40 + plen) * n, (flen + 3) * n)
             continue
+        if name.startswith("ring_scan"):  # the ring span (u32 length + frame, dword aligned) in; 6 B per record out
+            lens = lay["lens"].astype("int64")
+            out[name] = (int((4 + ((lens + 3) & ~3)).sum()), 6 * n)
+            continue
         if name.startswith("tx_"):  # + 16 B op in; 1 B result + 20 B of rewritten header out
             import bench
 
@@ -77,7 +81,7 @@ def main():
     only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     order = []
     for name, _kw, _n, _rot, launches, *_ in WORKLOADS:
-        if (only is None or name in only) and not name.startswith("ring_"):  # the ring walk is 7 kernels
+        if (only is None or name in only) and not name.startswith("ring_"):  # the ring walk: below
             order += [name] * launches
 
     def family(w):
@@ -120,12 +124,48 @@ def main():
         for d, cs in per.items():
             for c, v in cs.items():
                 res[amap[d]][c].append(v)
+    # the ring walk: three kernels per walk (guess, link, copy) — a workload's counters are summed
+    # over its walks' dispatches and divided by the walks; durations are kept per kernel
+    ring_order = []
+    for name, _kw, _n, _rot, launches, *_ in WORKLOADS:
+        if (only is None or name in only) and name.startswith("ring_"):
+            ring_order += [name] * launches
+
+    def ring_attr(rows):
+        disp = sorted({int(r["Dispatch_Id"]) for r in rows if "ring_" in r["Kernel_Name"]})
+        return {d: ring_order[k // 3] for k, d in enumerate(disp) if k // 3 < len(ring_order)}
+
+    ring = defaultdict(lambda: defaultdict(float))
+    ring_kernels = defaultdict(lambda: defaultdict(list))
+    amap = ring_attr(kt)
+    for r in kt:
+        d = int(r["Dispatch_Id"])
+        if d in amap:
+            short = r["Kernel_Name"].split("(")[0].split("::")[-1] if "(anonymous" not in r["Kernel_Name"].split("(")[0] else r["Kernel_Name"].split("::")[2].split("(")[0]
+            ring_kernels[amap[d]][short].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for step in ("kfetch", "kwrite", "ksq", "krd", "kwrq"):
+        rows = _rows(os.path.join(sess, step, "run_counter_collection.csv"))
+        amap = ring_attr(rows)
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            if d in amap:
+                ring[amap[d]][r["Counter_Name"]] += float(r["Counter_Value"])
+    for w in set(ring) | set(ring_kernels):
+        walks = ring_order.count(w)
+        for c, v in ring[w].items():
+            res[w][c].append(v / walks)
+        per = {k: round(sum(v) / len(v) / 1e3, 3) for k, v in ring_kernels[w].items()}
+        if per:
+            res[w]["duration_ns"].append(1e3 * sum(per.values()))
+            res[w]["kernel"] = [" + ".join(per)]
+            res[w]["kernels_us"] = [per]
     algs = alg_bytes()
     summary = {}
     for w, m in res.items():
-        avg = {k: (sum(v) / len(v) if v and not isinstance(v[0], str) else v[0]) for k, v in m.items()}
+        avg = {k: (sum(v) / len(v) if v and not isinstance(v[0], (str, dict)) else v[0]) for k, v in m.items()}
         rd_alg, wr_alg = algs[w]
         s = {"kernel": avg.get("kernel"), "vgpr": avg.get("vgpr"), "sgpr": avg.get("sgpr"),
+             **({"kernels_us": m["kernels_us"][0]} if "kernels_us" in m else {}),
              "launches": len(m.get("duration_ns", [])),
              "avg_duration_us": round(avg["duration_ns"] / 1e3, 3) if "duration_ns" in avg else None,
              "alg_read_bytes": rd_alg, "alg_write_bytes": wr_alg}

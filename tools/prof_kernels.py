@@ -33,6 +33,7 @@ WORKLOADS = [
     ("flow_hash_config2_compact", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
     # halo's packet ring (§8f row f1): the record walk over 1M 64 B records (68 MB span)
     ("ring_scan_1M_64B", dict(length=64), 1 << 20, 1, 20, 0, 1, 64),
+    ("ring_scan_imix_256k", dict(size_mode=1, proto_mode=3), 1 << 18, 1, 20, 0, 1, 1500),
     # transmit construction (§8f row f2, Build*): bench.tx_build_secondary's two workloads
     ("tx_build_udp_1M_64B", dict(length=64), 1 << 20, 1, 20, 0, 1, 22),
     ("tx_build_udp_256k_1514B", dict(length=64), 1 << 18, 1, 10, 0, 1, 1472),
