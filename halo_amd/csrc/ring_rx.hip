@@ -410,12 +410,12 @@ struct TileWalk {
 };
 template <int W>
 __device__ __forceinline__ TileWalk tile_walk(TileTab& tb, uint32_t n_act, uint32_t i0, uint32_t entry,
-                                              uint32_t limit) {
+                                              uint32_t limit, uint32_t known_F = ~0u) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
     uint32_t c = 0, q = entry;
     bool serial = n_act > kListMax;  // too many candidates to list: walk serially from the entry
     if (!serial && i0 < n_act && tb.list[i0] == entry) {  // uniform
-        const uint32_t F = first_break<W>(tb, n_act, i0), M = F + 1 - i0;
+        const uint32_t F = known_F != ~0u ? known_F : first_break<W>(tb, n_act, i0), M = F + 1 - i0;
         c = min(M, limit);
         q = c < M ? tb.list[i0 + c] : tb.nxt[tb.list[F]] & kPosMask;
         // the chain goes on at a position past a decoy: continue serially from there
@@ -483,7 +483,7 @@ __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
 //    the workspace, with a summary: (guess, where the walk leaves or stops, records, why, longest).
 // B. One workgroup links the summaries: tile t's guess is right when the walk through tile t - 1
 //    (itself verified) enters tile t there. By induction from tile 0 every guess that matches is
-//    the real entry, so a chunk of 32768 tiles is settled by one comparison per tile and a prefix
+//    the real entry, so a chunk of 16384 tiles is settled by one comparison per tile and a prefix
 //    sum; a tile whose guess is wrong (a decoy in the record that straddles its start) is walked
 //    again by the workgroup from its real entry, and the linking goes on after it.
 // C. Every tile copies its records to (dword offset, length) at its place in the batch.
@@ -518,12 +518,13 @@ __global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
     // dword before a record is often a decoy — a frame's last bytes and zero padding make a small
     // "length" (1.3 % of IMIX tiles, tools: a 570 B frame's last dword) — whose link lands nowhere;
     // such a chain is skipped. If every try stops, the first candidate (the walk may really stop).
-    uint32_t i0 = 0;
+    uint32_t i0 = 0, F0 = ~0u;  // the chosen chain: its first listed index and its first break
     if (t > 0 && n_act <= kListMax) {
         for (uint32_t k = 0, tries = 0; k < n_act && tries < kGuessTries; ++tries) {  // uniform
             const uint32_t F = first_break<kTileWaves>(tb, n_act, k), q = tb.nxt[tb.list[F]] & kPosMask;
             if (!(q < kTile && (tb.nxt[q] & kLdsStop))) {
                 i0 = k;
+                F0 = F;
                 break;
             }
             k = F + 1;
@@ -531,7 +532,7 @@ __global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
     }
     const uint32_t g = t == 0 ? 0u : n_act ? tb.list[i0] : kNone;
     TileWalk wk{0, kNone};
-    if (g != kNone) wk = tile_walk<kTileWaves>(tb, n_act, i0, g, kListMax);  // uniform (tile 0: i0 = 0)
+    if (g != kNone) wk = tile_walk<kTileWaves>(tb, n_act, i0, g, kListMax, F0);  // uniform (tile 0: i0 = 0)
     const uint32_t mx = keep_records(s, t, tb, i0, wk.c);
     if ((tid & 63u) == 0) s_mx[tid >> 6] = mx;
     __syncthreads();
@@ -543,22 +544,40 @@ __global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
     }
 }
 
-constexpr uint32_t kLinkThreads = 1024, kLinkWaves = kLinkThreads / 64, kLinkPer = 32;  // 512 MB spans in one pass
+constexpr uint32_t kLinkThreads = 1024, kLinkWaves = kLinkThreads / 64, kLinkPer = 16;  // 256 MB spans a chunk
 constexpr uint32_t kLinkChunk = kLinkThreads * kLinkPer;
+
+// B's second walk of tile J from its real entry `jin` (the guess was wrong): its records to the
+// workspace, and (records, exit, why, longest) to s_fix.
+__device__ __forceinline__ void relink_tile(const Scan& s, uint32_t J, uint32_t jin, TileTab& tb,
+                                                      uint32_t* s_part, uint32_t* s_fix) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t n_act = tile_tabulate<kLinkWaves>(s, J, tb, jin);
+    const TileWalk wk = tile_walk<kLinkWaves>(tb, n_act, 0, jin, kListMax);
+    const uint32_t m = keep_records(s, J, tb, 0, wk.c);
+    if (lane == 0) s_part[wv] = m;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t mm = 0;
+        for (uint32_t k = 0; k < kLinkWaves; ++k) mm = max(mm, s_part[k]);
+        s_fix[0] = wk.c;
+        s_fix[1] = wk.q;
+        s_fix[2] = wk.q < kTile ? tb.nxt[wk.q] & 0xFFu : 0u;
+        s_fix[3] = mm;
+    }
+}
 
 __global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
     __shared__ TileTab tb;
     __shared__ uint32_t s_min[kLinkWaves], s_sum[kLinkWaves];
-    __shared__ uint32_t s_fix[4];  // the special tile's records, exit, why, longest record
-    __shared__ uint32_t s_cut[2];  // the tile (and records before it) max_frames cuts inside
-    __shared__ uint32_t s_last_q;  // the exit of the chunk's last tile
+    __shared__ uint32_t s_q[kLinkThreads];  // each thread's last tile's exit (its successor's entry)
+    __shared__ uint32_t s_fix[4];           // the special tile's records, exit, why, longest record
+    __shared__ uint32_t s_cut[2];           // the tile (and records before it) max_frames cuts inside
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    const uint32_t mf = s.max_frames;
-    // uniform state: the first tile not linked yet, its entry, the records before it
-    uint32_t lo = 0, e = 0, base = 0;
+    const uint32_t mf = s.max_frames, nt = s.n_tiles;
+    uint32_t t0 = 0, e = 0, base = 0;  // the next tile to link, its entry, records before it (uniform)
     uint32_t why = HALO_RING_STOP_EMPTY, last = 0;
     uint32_t mx = 0;  // the longest record of this thread's tiles that lie wholly before max_frames
-    bool done = false;
     if (tid == 0) s_cut[0] = ~0u;
     // a tile's records counted into the batch: all of them, the first ones (max_frames cuts inside
     // it: its longest comes from its records at the end), or none
@@ -569,13 +588,16 @@ __global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
             s_cut[1] = b;
         }
     };
-    while (!done) {
-        // a chunk of kLinkChunk tiles from lo; thread tid holds tiles j0 .. j0 + kLinkPer - 1 and a
-        // mask of those that cannot be passed on their summary ("special": the entry the tile
-        // before leads to is not the guess, the walk stops inside, or the span's last tile)
-        const uint32_t t0 = lo, j0 = t0 + tid * kLinkPer;
+    for (;;) {
+        // A chunk of kLinkChunk tiles from t0, kLinkPer summaries a thread in registers: the first
+        // tile that cannot be passed on its summary ("special": the entry the tile before leads to
+        // is not the guess, the walk stops inside, or the span's last tile) and the records of the
+        // ones before it. After a special tile the next chunk starts behind it (a re-read of the
+        // summaries, from the L2): keeping the chunk's state across a tile's second walk instead
+        // spilled at 1024 threads (70 us, profiles/r05/r5k).
+        const uint32_t j0 = t0 + tid * kLinkPer;
         uint2 sm[kLinkPer];
-        if (j0 + kLinkPer <= s.n_tiles && !(reinterpret_cast<uintptr_t>(s.sum) & 15u)) {  // two summaries a load
+        if (j0 + kLinkPer <= nt && !(reinterpret_cast<uintptr_t>(s.sum) & 15u)) {  // two summaries a load
 #pragma unroll
             for (uint32_t k = 0; k < kLinkPer; k += 2) {
                 const uint4 v = *reinterpret_cast<const uint4*>(s.sum + j0 + k);
@@ -584,123 +606,89 @@ __global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
             }
         } else {
 #pragma unroll
-            for (uint32_t k = 0; k < kLinkPer; ++k) sm[k] = j0 + k < s.n_tiles ? s.sum[j0 + k] : make_uint2(kNone, 0u);
+            for (uint32_t k = 0; k < kLinkPer; ++k) sm[k] = j0 + k < nt ? s.sum[j0 + k] : make_uint2(kNone, 0u);
         }
         uint32_t prev_q = 0;
-        if (j0 > t0 && j0 <= s.n_tiles) prev_q = s.sum[j0 - 1].x >> 16;
-        uint32_t mask = 0;
+        if (j0 > t0 && j0 <= nt) prev_q = s.sum[j0 - 1].x >> 16;
+        uint32_t first = ~0u;
 #pragma unroll
         for (uint32_t k = 0; k < kLinkPer; ++k) {
             const uint32_t j = j0 + k, g = sm[k].x & 0xFFFFu, q = sm[k].x >> 16;
             const uint32_t in = j == t0 ? e : prev_q - kTile;  // wraps (no match) when prev_q < kTile
-            if (j >= s.n_tiles || in != g || q < kTile || j == s.n_tiles - 1) mask |= 1u << k;
+            const bool special = j >= nt || in != g || q < kTile || j == nt - 1;
+            if (special && first == ~0u) first = j;
             prev_q = q;
         }
-        if (tid == kLinkThreads - 1) s_last_q = prev_q;
-        for (;;) {
-            // J: the first special tile at or after lo (none: the chunk's tiles from lo all pass)
-            uint32_t mm = lo <= j0 ? mask : lo - j0 < kLinkPer ? mask & (~0u << (lo - j0)) : 0u;
-            uint32_t first = mm ? j0 + (uint32_t)__builtin_ctz(mm) : ~0u;
+        s_q[tid] = prev_q;
+        // block: the first special tile J (every chunk that reaches the span's last tile has one)
 #pragma unroll
-            for (int m = 1; m < 64; m <<= 1) first = min(first, (uint32_t)__shfl_xor((int)first, m, 64));
-            if (lane == 0) s_min[wv] = first;
-            __syncthreads();
-            uint32_t J = ~0u;
-            for (uint32_t k = 0; k < kLinkWaves; ++k) J = min(J, s_min[k]);
-            // the tiles in [lo, J): records before each, by an exclusive prefix over the block
-            uint32_t cnt = 0;
+        for (int m = 1; m < 64; m <<= 1) first = min(first, (uint32_t)__shfl_xor((int)first, m, 64));
+        if (lane == 0) s_min[wv] = first;
+        __syncthreads();
+        uint32_t J = ~0u;
+        for (uint32_t k = 0; k < kLinkWaves; ++k) J = min(J, s_min[k]);
+        // an exclusive prefix of the records of the tiles before J
+        uint32_t cnt = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < kLinkPer; ++k) cnt += j0 + k >= lo && j0 + k < J ? sm[k].y & 0xFFFu : 0u;
-            uint32_t x = cnt;
+        for (uint32_t k = 0; k < kLinkPer; ++k) cnt += j0 + k < J ? sm[k].y & 0xFFFu : 0u;
+        uint32_t x = cnt;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-                if (lane >= (uint32_t)o) x += y;
-            }
-            if (lane == 63) s_sum[wv] = x;
-            // J's summary and the exit of the tile before it, from the threads that hold them
-            if (J != ~0u) {
-#pragma unroll
-                for (uint32_t k = 0; k < kLinkPer; ++k) {
-                    if (j0 + k == J) {
-                        s_fix[0] = sm[k].x;
-                        s_fix[1] = sm[k].y;
-                    }
-                    if (j0 + k + 1 == J) s_fix[2] = sm[k].x >> 16;
-                }
-            }
-            __syncthreads();
-            uint32_t off = 0, total = 0;
-            for (uint32_t k = 0; k < kLinkWaves; ++k) {
-                if (k < wv) off += s_sum[k];
-                total += s_sum[k];
-            }
-            uint32_t b = base + off + x - cnt;
-#pragma unroll
-            for (uint32_t k = 0; k < kLinkPer; ++k) {
-                const uint32_t j = j0 + k, c = sm[k].y & 0xFFFu;
-                if (j >= lo && j < J) {
-                    s.tile_entry[j] = make_uint2(b, c);
-                    account(j, b, c, sm[k].y >> 16);
-                    b += c;
-                }
-            }
-            base += total;
-            if (J == ~0u) {  // through to the chunk's end: the next chunk starts where its last tile leads
-                e = s_last_q - kTile;
-                lo = t0 + kLinkChunk;
-                __syncthreads();
-                break;
-            }
-            const uint32_t jin = J == lo ? e : s_fix[2] - kTile;  // J's real entry
-            const uint2 sj = make_uint2(s_fix[0], s_fix[1]);
-            __syncthreads();  // s_fix / s_min / s_sum are rewritten below
-            if ((sj.x & 0xFFFFu) == jin) {  // uniform. The guess was right: the walk stops in J, or J is the last tile
-                if (tid == 0) {
-                    s_fix[0] = sj.y & 0xFFFu;
-                    s_fix[1] = sj.x >> 16;
-                    s_fix[2] = (sj.y >> 12) & 0xFu;
-                    s_fix[3] = sj.y >> 16;
-                }
-            } else {  // a decoy led the guess astray: walk J again from its real entry
-                const uint32_t n_act = tile_tabulate<kLinkWaves>(s, J, tb, jin);
-                const TileWalk wk = tile_walk<kLinkWaves>(tb, n_act, 0, jin, kListMax);
-                const uint32_t m = keep_records(s, J, tb, 0, wk.c);
-                if (lane == 0) s_min[wv] = m;
-                __syncthreads();
-                if (tid == 0) {
-                    uint32_t mm2 = 0;
-                    for (uint32_t k = 0; k < kLinkWaves; ++k) mm2 = max(mm2, s_min[k]);
-                    s_fix[0] = wk.c;
-                    s_fix[1] = wk.q;
-                    s_fix[2] = wk.q < kTile ? tb.nxt[wk.q] & 0xFFu : 0u;
-                    s_fix[3] = mm2;
-                }
-            }
-            __syncthreads();
-            const uint32_t c = s_fix[0], q = s_fix[1];
-            if (tid == 0) {
-                s.tile_entry[J] = make_uint2(base, c);
-                account(J, base, c, s_fix[3]);
-            }
-            base += c;
-            if (q < kTile || J == s.n_tiles - 1) {  // stopped in J, or left the span (EMPTY)
-                why = q < kTile ? s_fix[2] : HALO_RING_STOP_EMPTY;
-                last = J;
-                done = true;
-                break;
-            }
-            lo = J + 1;
-            e = q - kTile;
-            // the tile after J now has a known entry: is it special with it?
-            if (lo >= j0 && lo < j0 + kLinkPer) {
-                const uint32_t k = lo - j0, g = sm[k].x & 0xFFFFu, qq = sm[k].x >> 16;
-                const bool sp = lo >= s.n_tiles || e != g || qq < kTile || lo == s.n_tiles - 1;
-                mask = sp ? mask | (1u << k) : mask & ~(1u << k);
-            }
-            __syncthreads();  // s_fix is rewritten by the next round
-            if (lo >= t0 + kLinkChunk) break;  // the chunk is used up: the next one starts at lo
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
         }
+        if (lane == 63) s_sum[wv] = x;
+        __syncthreads();
+        uint32_t off = 0, chunk_total = 0;
+        for (uint32_t k = 0; k < kLinkWaves; ++k) {
+            if (k < wv) off += s_sum[k];
+            chunk_total += s_sum[k];
+        }
+        uint32_t b = base + off + x - cnt;
+#pragma unroll
+        for (uint32_t k = 0; k < kLinkPer; ++k) {
+            const uint32_t j = j0 + k, c = sm[k].y & 0xFFFu;
+            if (j < J) {
+                s.tile_entry[j] = make_uint2(b, c);
+                account(j, b, c, sm[k].y >> 16);
+                b += c;
+            }
+        }
+        base += chunk_total;
+        if (J == ~0u) {  // no special tile in the chunk (it ended before the span's last tile)
+            e = s_q[kLinkThreads - 1] - kTile;
+            t0 += kLinkChunk;
+            __syncthreads();
+            continue;
+        }
+        const uint32_t jin = J == t0 ? e : (s.sum[J - 1].x >> 16) - kTile;  // J's real entry
+        const uint2 sj = s.sum[J];
+        __syncthreads();  // s_q / s_min / s_sum are rewritten below and by the next chunk
+        if ((sj.x & 0xFFFFu) == jin) {  // uniform. The guess was right: the walk stops in J, or J is the last tile
+            if (tid == 0) {
+                s_fix[0] = sj.y & 0xFFFu;
+                s_fix[1] = sj.x >> 16;
+                s_fix[2] = (sj.y >> 12) & 0xFu;
+                s_fix[3] = sj.y >> 16;
+            }
+        } else {  // a decoy led the guess astray: walk J again from its real entry
+            relink_tile(s, J, jin, tb, s_min, s_fix);
+        }
+        __syncthreads();
+        const uint32_t c = s_fix[0], q = s_fix[1];
+        if (tid == 0) {
+            s.tile_entry[J] = make_uint2(base, c);
+            account(J, base, c, s_fix[3]);
+        }
+        base += c;
+        if (q < kTile || J == nt - 1) {  // stopped in J, or left the span (EMPTY)
+            why = q < kTile ? s_fix[2] : HALO_RING_STOP_EMPTY;
+            last = J;
+            break;
+        }
+        t0 = J + 1;
+        e = q - kTile;
+        __syncthreads();
     }
     // the longest record taken: every whole tile's, and the cut tile's records before max_frames
 #pragma unroll

@@ -224,8 +224,8 @@ def test_ring_timeout_retires_the_request(dev, golden, oracle_lib):
 
 
 def test_drains_while_a_persistent_ring_is_polled(dev, oracle_lib):
-    """unregistering host memory, attaching and detaching another ring, and syncing a route
-    table are device drains. With another thread polling a HALO_RING_PERSISTENT ring non-stop, each
+    """unregistering host memory, attaching and detaching another ring, syncing a route
+    table and halo_rx_device_synchronize are device drains. With another thread polling a HALO_RING_PERSISTENT ring non-stop, each
     must finish promptly (the drain stops the resident consumer and keeps polls on launches while it
     waits) and every poll must stay correct."""
     from halo_amd import _lib, synth
@@ -278,6 +278,11 @@ def test_drains_while_a_persistent_ring_is_polled(dev, oracle_lib):
             t.sync()  # the second sync drains the device before reusing a generation
             durations.setdefault("route_sync", []).append(time.perf_counter() - t0)
             t.close()
+            # the exported drain: a caller's device synchronisation that does not wait
+            # for the resident consumer another thread keeps busy
+            t0 = time.perf_counter()
+            _lib.device_synchronize(0)
+            durations.setdefault("device_synchronize", []).append(time.perf_counter() - t0)
         time.sleep(0.1)
     finally:
         stop.set()
