@@ -1148,8 +1148,13 @@ def roofline(alg_bytes_per_launch, kernel_ms, traffic=None, frame_bytes=None):
     """`frame_bytes` (the frames' own bytes per launch, SURVEY §8d's primary R): also report the
     R-only fraction beside the (R + M + W) one."""
     achieved = alg_bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    session = None
+    if isinstance(traffic, dict):  # load_traffic: the bytes and the profiling session they come from
+        traffic, session = traffic["bytes"], traffic["session"]
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+    if session:
+        r["traffic_session"] = session
     if frame_bytes:
         r["frac_frames_only"] = round(frame_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if MEASURED_READ_GBS:
@@ -1159,12 +1164,15 @@ def roofline(alg_bytes_per_launch, kernel_ms, traffic=None, frame_bytes=None):
 
 
 def load_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if any, with the
+    profiling session they come from: {"bytes": B, "session": "r5t"} or None."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
         return None
     try:
-        return json.load(open(p)).get(workload, {}).get("hbm_bytes_per_launch")
+        d = json.load(open(p))
+        b = d.get(workload, {}).get("hbm_bytes_per_launch")
+        return None if b is None else {"bytes": b, "session": d.get("sessions", {}).get(workload)}
     except Exception:
         return None
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 import csv
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -141,7 +142,7 @@ def main():
     for r in kt:
         d = int(r["Dispatch_Id"])
         if d in amap:
-            short = r["Kernel_Name"].split("(")[0].split("::")[-1] if "(anonymous" not in r["Kernel_Name"].split("(")[0] else r["Kernel_Name"].split("::")[2].split("(")[0]
+            short = re.search(r"ring_\w+?_kernel", r["Kernel_Name"]).group(0)
             ring_kernels[amap[d]][short].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     for step in ("kfetch", "kwrite", "ksq", "krd", "kwrq"):
         rows = _rows(os.path.join(sess, step, "run_counter_collection.csv"))
