@@ -349,25 +349,31 @@ typedef struct {
     const halo_rx_netif_t* netif;
     halo_rx_result_t* out;
     uint64_t first, last;
+    uint32_t reps;
     uint32_t hist[HALO_RX_STATUS_COUNT];
 } ora_job_t;
 
 static void* ora_job(void* arg) {
     ora_job_t* j = (ora_job_t*)arg;
     memset(j->hist, 0, sizeof j->hist);
-    for (uint64_t i = j->first; i < j->last; ++i) {
-        const uint8_t* f = j->offsets_dw ? j->bytes + ((uint64_t)j->offsets_dw[i] << 2) : j->bytes + i * j->stride;
-        const uint32_t L = j->lens ? j->lens[i] : j->len;
-        ora_rx_frame(f, L, j->flags, j->netif, &j->out[i]);
-        j->hist[j->out[i].status]++;
+    for (uint32_t r = 0; r < j->reps; ++r) {
+        for (uint64_t i = j->first; i < j->last; ++i) {
+            const uint8_t* f = j->offsets_dw ? j->bytes + ((uint64_t)j->offsets_dw[i] << 2) : j->bytes + i * j->stride;
+            const uint32_t L = j->lens ? j->lens[i] : j->len;
+            ora_rx_frame(f, L, j->flags, j->netif, &j->out[i]);
+            if (r == 0) j->hist[j->out[i].status]++;
+        }
     }
     return NULL;
 }
 
-/* threads <= 1: run on the calling thread (the reference's one goroutine per NetIf). */
-ORA_API int ora_rx_batch(const uint8_t* bytes, const uint32_t* offsets_dw, const uint16_t* lens, uint64_t stride,
-                         uint32_t len, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
-                         halo_rx_result_t* out, uint32_t* hist, int threads) {
+/* threads <= 1: run on the calling thread (the reference's one goroutine per NetIf). `reps`: every
+ * thread parses its shard that many times (the same records each time) — for timing many passes
+ * with one thread start each, so the thread starts do not dominate a many-core measurement. */
+ORA_API int ora_rx_batch_reps(const uint8_t* bytes, const uint32_t* offsets_dw, const uint16_t* lens, uint64_t stride,
+                              uint32_t len, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
+                              halo_rx_result_t* out, uint32_t* hist, int threads, uint32_t reps) {
+    if (reps < 1) reps = 1;
     if (threads < 1) threads = 1;
     if (threads > 1024) threads = 1024;
     ora_job_t* jobs = (ora_job_t*)calloc((size_t)threads, sizeof(ora_job_t));
@@ -379,6 +385,7 @@ ORA_API int ora_rx_batch(const uint8_t* bytes, const uint32_t* offsets_dw, const
         j->flags = flags; j->netif = netif; j->out = out;
         j->first = (uint64_t)n * t / threads;
         j->last = (uint64_t)n * (t + 1) / threads;
+        j->reps = reps;
     }
     int rc = 0;
     int started = 0;
@@ -394,6 +401,12 @@ ORA_API int ora_rx_batch(const uint8_t* bytes, const uint32_t* offsets_dw, const
     free(jobs);
     free(tid);
     return rc;
+}
+
+ORA_API int ora_rx_batch(const uint8_t* bytes, const uint32_t* offsets_dw, const uint16_t* lens, uint64_t stride,
+                         uint32_t len, uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
+                         halo_rx_result_t* out, uint32_t* hist, int threads) {
+    return ora_rx_batch_reps(bytes, offsets_dw, lens, stride, len, n, flags, netif, out, hist, threads, 1);
 }
 
 ORA_API void ora_engine_batch(const uint8_t* bytes, const uint32_t* offsets_dw, const uint16_t* lens,

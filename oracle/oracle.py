@@ -73,6 +73,8 @@ def lib() -> ctypes.CDLL:
         L.ora_engine_rx.argtypes = [vp, u32, u32, ctypes.POINTER(NetIf)]
         L.ora_rx_batch.restype = ctypes.c_int
         L.ora_rx_batch.argtypes = [vp, vp, vp, u64, u32, u32, u32, ctypes.POINTER(NetIf), vp, vp, ctypes.c_int]
+        L.ora_rx_batch_reps.restype = ctypes.c_int
+        L.ora_rx_batch_reps.argtypes = [vp, vp, vp, u64, u32, u32, u32, ctypes.POINTER(NetIf), vp, vp, ctypes.c_int, u32]
         L.ora_engine_lo.restype = ctypes.c_int
         L.ora_engine_lo.argtypes = [vp, u32, u32, ctypes.POINTER(NetIf)]
         L.ora_engine_batch.restype = None
@@ -158,16 +160,17 @@ def engine_lo(packet: bytes, netif: NetIf, flags: int = 1) -> int:
 
 
 def rx_batch(data: np.ndarray, lens: np.ndarray, netif: NetIf, flags: int = 1, offsets_dw=None, stride: int = 0,
-             length: int = 0, threads: int = 1):
-    """Returns (records, status histogram)."""
+             length: int = 0, threads: int = 1, reps: int = 1):
+    """Returns (records, status histogram). `reps`: every thread parses its shard that many times
+    (timing: one thread start per measurement)."""
     n = int(lens.shape[0]) if lens is not None else int(data.shape[0] // stride)
     out = np.zeros(n, dtype=RESULT_DTYPE)
     hist = np.zeros(STATUS_COUNT, dtype=np.uint32)
     data = np.ascontiguousarray(data, dtype=np.uint8)
     lens_c = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
     offs_c = None if offsets_dw is None else np.ascontiguousarray(offsets_dw, dtype=np.uint32)
-    rc = lib().ora_rx_batch(_p(data), _p(offs_c), _p(lens_c), stride, length, n, flags, netif, _p(out), _p(hist),
-                            threads)
+    rc = lib().ora_rx_batch_reps(_p(data), _p(offs_c), _p(lens_c), stride, length, n, flags, netif, _p(out),
+                                 _p(hist), threads, reps)
     assert rc == 0
     return out, hist
 
