@@ -538,7 +538,12 @@ __device__ __forceinline__ unsigned long long* launch_tree(uint32_t* set_u32, un
     for (uint32_t j = 0; j < kHistTrees; ++j) {
         const uint32_t k = (k0 + j) & (kHistTrees - 1u);
         unsigned long long key = j ? set[k] : key0;
-        if (key == 0) key = atomicCAS(set + k, 0ull, q);  // 0: claimed now; q: claimed by another block
+        if (key == 0) {  // claim it (device scope: a native compare-and-swap, no retry loop)
+            unsigned long long expect = 0;
+            __hip_atomic_compare_exchange_strong(set + k, &expect, q, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            key = expect;  // 0: claimed now; q: claimed by another block of this queue
+        }
         if (key == 0 || key == q) return set + kHistKeyWords + (uint64_t)k * kHistWords;
     }
     return nullptr;  // every key taken by another queue, or poisoned (hist_trees: no barrier bits)
@@ -559,6 +564,9 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
         if (hist.s[t]) atomicAdd(&p.hist_out[t], hist.s[t]);
         return;
     }
+    // (Carrying the arrivals in word 0 alone and adding only the statuses a block saw — one atomic
+    // per clean block instead of 14 — ran 0.6 us slower per 1M-frame launch, r5u: the cost is the
+    // chain of dependent round trips the last block pays at the tail, not the number of atomics.)
     constexpr unsigned long long kOne = 1ull << 40, kCount = kOne - 1;
     unsigned long long* l1 = tree + s * kHistStride + t;
     unsigned long long now = atomicAdd(l1, kOne | hist.s[t]) + (kOne | hist.s[t]);
