@@ -564,9 +564,11 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
         if (hist.s[t]) atomicAdd(&p.hist_out[t], hist.s[t]);
         return;
     }
-    // (Carrying the arrivals in word 0 alone and adding only the statuses a block saw — one atomic
-    // per clean block instead of 14 — ran 0.6 us slower per 1M-frame launch, r5u: the cost is the
-    // chain of dependent round trips the last block pays at the tail, not the number of atomics.)
+    // The tree costs a fixed ~2.5 us per launch, not a per-block cost (1M frames: +2.7 us, 4M: +2.4,
+    // 16M: +1.4; counting, the LDS adds and the barrier alone: +0.4): the last block's two dependent
+    // round trips. Arrivals in one word with only the statuses a block saw (one atomic per clean
+    // block) ran 0.6 us slower; one level of 64 / 256 / 1024 slots ran +0.3 / +1.3 / +9 us (the
+    // completers' adds queue on one counter at ~10 ns each). DESIGN.md §14.5.
     constexpr unsigned long long kOne = 1ull << 40, kCount = kOne - 1;
     unsigned long long* l1 = tree + s * kHistStride + t;
     unsigned long long now = atomicAdd(l1, kOne | hist.s[t]) + (kOne | hist.s[t]);

@@ -19,17 +19,19 @@ def main():
         other.halo_rx_init(0)
     _lib.check("init", _lib.lib.halo_rx_init(0))
     dev = torch.device("cuda:0")
-    lay = synth.layout(1 << 20, length=64)
+    import os
+    n = int(os.environ.get("HIST_FRAMES", 1 << 20))
+    lay = synth.layout(n, length=64)
     fr = synth.frames_device(lay, NetIf.make(), device=dev)
-    out = torch.empty((1 << 20, 32), dtype=torch.uint8, device=dev)
-    hist = torch.zeros(14, dtype=torch.int32, device=dev)
+    out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    hist = torch.zeros(16, dtype=torch.int32, device=dev)
     def parse(h):
         if other is None:
             protocol.parse_frames_batch(fr["bytes"], fr["offsets_dw"], fr["lens"], netif=NetIf.make(),
                                         max_len_hint=64, out=out, hist=h)
             return
         rc = other.halo_rx_parse_batch_device(
-            _lib.ptr(fr["bytes"]), _lib.ptr(fr["offsets_dw"]), _lib.ptr(fr["lens"]), 1 << 20, 1, NetIf.make(), 64,
+            _lib.ptr(fr["bytes"]), _lib.ptr(fr["offsets_dw"]), _lib.ptr(fr["lens"]), n, 1, NetIf.make(), 64,
             _lib.ptr(out), _lib.ptr(h), torch.cuda.current_stream().cuda_stream)
         assert rc == 0, rc
 
@@ -44,7 +46,11 @@ def main():
         torch.cuda.synchronize()
         print(f"hist={'on ' if h is not None else 'off'} {e0.elapsed_time(e1) / reps * 1000:.2f} us/launch", flush=True)
     total = int(hist.sum().item())
-    assert total == 2 * (reps + 20) * (1 << 20), total
+    import os
+    if os.environ.get("HIST_NOCHECK"):
+        print("total", total)
+    else:
+        assert total == 2 * (reps + 20) * n, total
     print("hist exact", np.asarray(hist.cpu())[:2])
 
 
