@@ -65,6 +65,8 @@ struct Scan {
     uint32_t max_frames;
     uint64_t half;          // RingBuffer.size / 2
     uint32_t half32;        // min(half, 2^32 - 1)
+    uint32_t lim;           // min(half32, cap): the longest length a record may have
+    uint32_t lim_dw;        // its dwords, (lim + 7) / 4
     uint2* tile_map;        // [n_tiles][W]: (entry into the next tile | kMapStop, records taken)
     uint2* sb_map;          // [n_sb][W]
     uint2* ss_map;          // [n_ss][W]
@@ -281,7 +283,8 @@ __global__ void __launch_bounds__(kThreads) ring_expand_kernel(const uint2* pare
 // Tile tables. nxt[q]: the position of the record after the one whose length
 // field is tile position q (bits 0-12; >= kTile: the next tile's position + kTile) with that
 // length's low two bits (bits 13-14: with the record's dwords they give the length back), or
-// kLdsStop | ReadPacket's reason when q fails its checks. list: the positions >= lo that pass.
+// kLdsStop when q fails ReadPacket's checks (the reason is worked out again, for the one position
+// a walk stops at, by stop_why). list: the positions >= lo that pass.
 constexpr uint32_t kListMax = kTile / 2;  // records of >= 2 dwords: at most this many per tile
 constexpr uint32_t kNone = 0xFFFFu;      // tile summary: no position of the tile passes the checks
 constexpr uint32_t kPosMask = 0x1FFFu;   // kTile + W - 1 < 2^13
@@ -293,6 +296,13 @@ static_assert(kTile + (kMaxCapacity + 7) / 4 <= kPosMask + 1, "nxt positions fit
 __device__ __forceinline__ uint32_t nxt_len(uint32_t q, uint32_t v) {
     const uint32_t dw = (v & kPosMask) - q, r = (v >> 13) & 3u;
     return ((dw - 1u - (r != 0u)) << 2) | r;
+}
+
+// Why ReadPacket stops at span dword a (a position whose nxt is kLdsStop).
+__device__ __forceinline__ uint32_t stop_why(const Scan& s, uint32_t a) {
+    uint32_t why = HALO_RING_STOP_EMPTY;
+    if (a < s.n_dw) record_dwords(s, a, s.span[a], why);
+    return why;
 }
 
 // One tile's tables, shared by the workgroup that walks it (12 KB: eight 4-wave workgroups per CU;
@@ -308,40 +318,58 @@ struct TileTab {
 // workgroup of W waves; returns how many pass (list holds the first kListMax). Lane l of wave w
 // takes the 16-byte chunks w * kTile / W + 256 u + 4 l: the tile's bytes are read once, with every
 // load of a lane in flight together.
+//
+// The walk is VALU-bound here (round 5: 612 VALU a wave, 38 a position), so the common tile takes a
+// shorter test: when the tile ends at least one longest record (lim = min(size / 2, capacity)) before
+// the span does, a position passes exactly when 1 <= len <= lim — no record can run past the span
+// from it, and EMPTY / PARTIAL cannot apply — which is one compare whose lane mask is also the
+// position's ballot. The record's dwords are (len + 7) >> 2 (= ceil((4 + len) / 4)).
 template <int W>
-__device__ __forceinline__ uint32_t tile_tabulate(const Scan& s, uint32_t t, TileTab& tb, uint32_t lo) {
-    constexpr uint32_t Q = kTile / (W * 256);  // 16-byte chunks per lane
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    const uint32_t tbase = t * kTile, wbase = w * (kTile / W);
-    uint4 v[Q];
-    if (tbase + kTile <= s.n_dw) {  // uniform
+constexpr uint32_t kTabQ = kTile / (W * 256);  // 16-byte chunks per lane
+
+template <int W>
+__device__ __forceinline__ void tile_load(const Scan& s, uint32_t t, uint4 (&v)[kTabQ<W>]) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t at = t * kTile + w * (kTile / W) + 4 * lane;
+    if (t * kTile + kTile <= s.n_dw) {  // uniform
 #pragma unroll
-        for (uint32_t u = 0; u < Q; ++u) {
-            const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + tbase + wbase + 256 * u + 4 * lane);
+        for (uint32_t u = 0; u < kTabQ<W>; ++u) {
+            const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + at + 256 * u);
             v[u] = make_uint4(x.x, x.y, x.z, x.w);
         }
     } else {
 #pragma unroll
-        for (uint32_t u = 0; u < Q; ++u) v[u] = span_quad(s, tbase + wbase + 256 * u + 4 * lane);
+        for (uint32_t u = 0; u < kTabQ<W>; ++u) v[u] = span_quad(s, at + 256 * u);
     }
-    uint32_t mine[Q];  // bit j: position q + j holds a record and is at or past lo
+}
+
+template <int W, bool INNER>
+__device__ __forceinline__ uint32_t tabulate_as(const Scan& s, uint32_t t, TileTab& tb, uint32_t lo,
+                                                const uint4 (&v)[kTabQ<W>]) {
+    constexpr uint32_t Q = kTabQ<W>;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t tbase = t * kTile, wbase = w * (kTile / W);
+    bool m[Q][4];  // position q + j holds a record and is at or past lo
     uint32_t cnt = 0;
 #pragma unroll
     for (uint32_t u = 0; u < Q; ++u) {
         const uint32_t q = wbase + 256 * u + 4 * lane;
         const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
         uint32_t nx[4];
-        mine[u] = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            uint32_t why;
-            const uint32_t step = record_dwords(s, tbase + q + j, d[j], why);
-            nx[j] = step ? (q + j + step) | ((d[j] & 3u) << 13) : (kLdsStop | why);
-            mine[u] |= (step && q + j >= lo) ? 1u << j : 0u;
+            bool pass;
+            if constexpr (INNER) {
+                pass = d[j] - 1u < s.lim;
+            } else {
+                uint32_t why;
+                pass = record_dwords(s, tbase + q + j, d[j], why) != 0;
+            }
+            nx[j] = pass ? ((q + j + ((d[j] + 7u) >> 2)) | ((d[j] & 3u) << 13)) : kLdsStop;
+            m[u][j] = pass && q + j >= lo;
+            cnt += (uint32_t)__popcll(__ballot(m[u][j]));
         }
         *reinterpret_cast<uint2*>(&tb.nxt[q]) = make_uint2(nx[0] | (nx[1] << 16), nx[2] | (nx[3] << 16));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cnt += (uint32_t)__popcll(__ballot((mine[u] >> j) & 1u));
     }
     if (lane == 0) tb.part[w] = cnt;
     __syncthreads();
@@ -354,23 +382,37 @@ __device__ __forceinline__ uint32_t tile_tabulate(const Scan& s, uint32_t t, Til
     // ordered compaction (wave, then chunk, then lane, then j)
 #pragma unroll
     for (uint32_t u = 0; u < Q; ++u) {
-        uint32_t before = 0, total = 0;
+        uint32_t slot = k, total = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint64_t b = __ballot((mine[u] >> j) & 1u);
-            before += lane_rank(b);
+        for (int j = 0; j < 4; ++j) {  // + the candidates of the lanes before this one
+            const uint64_t b = __ballot(m[u][j]);
+            slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, slot));
             total += (uint32_t)__popcll(b);
         }
         const uint32_t q = wbase + 256 * u + 4 * lane;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t slot = k + before + (uint32_t)__builtin_popcount(mine[u] & ((1u << j) - 1u));
-            if (((mine[u] >> j) & 1u) && slot < kListMax) tb.list[slot] = (uint16_t)(q + j);
+            if (m[u][j] && slot < kListMax) tb.list[slot] = (uint16_t)(q + j);
+            slot += m[u][j] ? 1u : 0u;
         }
         k += total;
     }
     __syncthreads();
     return n_act;
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t tile_tabulate(const Scan& s, uint32_t t, TileTab& tb, uint32_t lo,
+                                                  const uint4 (&v)[kTabQ<W>]) {
+    if ((uint64_t)t * kTile + kTile + s.lim_dw <= s.n_dw) return tabulate_as<W, true>(s, t, tb, lo, v);  // uniform
+    return tabulate_as<W, false>(s, t, tb, lo, v);
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t tile_tabulate(const Scan& s, uint32_t t, TileTab& tb, uint32_t lo) {
+    uint4 v[kTabQ<W>];
+    tile_load<W>(s, t, v);
+    return tile_tabulate<W>(s, t, tb, lo, v);
 }
 
 // The first "break" at list index >= i0: the first listed candidate whose link does not reach the
@@ -463,7 +505,7 @@ __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
         const uint32_t v = q < kTile ? tb.nxt[q] : 0u;
         if (base + c == n && c) s.info->end_bytes = 4ull * (tbase + q);
         // where the walk ends inside this tile: say why, unless max_frames cut it (MAX, set)
-        if (q < kTile && n == *s.total && (v & kLdsStop)) s.info->stop = v & 0xFFu;
+        if (q < kTile && n == *s.total && (v & kLdsStop)) s.info->stop = stop_why(s, tbase + q);
     }
     uint32_t max_len = 0;
     for (uint32_t j = tid; j < c; j += kThreads) {
@@ -509,11 +551,11 @@ __device__ __forceinline__ uint32_t keep_records(const Scan& s, uint32_t t, cons
     return mx;  // the wave's
 }
 
-__global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
-    __shared__ TileTab tb;
-    __shared__ uint32_t s_mx[kTileWaves];
-    const uint32_t t = blockIdx.x, tid = threadIdx.x;
-    const uint32_t n_act = tile_tabulate<kTileWaves>(s, t, tb, 0);
+// One tile of A: its tables, its guess, its walk, its records and summary.
+__device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& tb, uint32_t* s_mx,
+                                           const uint4 (&v)[kTabQ<kTileWaves>]) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n_act = tile_tabulate<kTileWaves>(s, t, tb, 0, v);
     // The guess: the first listed candidate whose chain of links does not stop inside the tile. The
     // dword before a record is often a decoy — a frame's last bytes and zero padding make a small
     // "length" (1.3 % of IMIX tiles, tools: a 570 B frame's last dword) — whose link lands nowhere;
@@ -539,9 +581,20 @@ __global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
     if (tid == 0) {
         uint32_t m = 0;
         for (uint32_t x = 0; x < kTileWaves; ++x) m = max(m, s_mx[x]);
-        const uint32_t why = wk.q < kTile ? tb.nxt[wk.q] & 0xFFu : 0u;
+        const uint32_t why = wk.q < kTile ? stop_why(s, t * kTile + wk.q) : 0u;
         s.sum[t] = make_uint2(g | (wk.q << 16), wk.c | (why << 12) | (m << 16));
     }
+}
+
+__global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
+    __shared__ TileTab tb;
+    __shared__ uint32_t s_mx[kTileWaves];
+    // (one tile per workgroup: workgroups that took tiles t, t + 2048, ... and loaded the next
+    // one's bytes while working on the current one ran slower, 24.9 against 19.0 us for 1M 64 B
+    // records, profiles/r06/r6c: the tile's work, not its load, is what a CU waits on)
+    uint4 v[kTabQ<kTileWaves>];
+    tile_load<kTileWaves>(s, blockIdx.x, v);
+    guess_tile(s, blockIdx.x, tb, s_mx, v);
 }
 
 constexpr uint32_t kLinkThreads = 1024, kLinkWaves = kLinkThreads / 64, kLinkPer = 16;  // 256 MB spans a chunk
@@ -562,7 +615,7 @@ __device__ __forceinline__ void relink_tile(const Scan& s, uint32_t J, uint32_t 
         for (uint32_t k = 0; k < kLinkWaves; ++k) mm = max(mm, s_part[k]);
         s_fix[0] = wk.c;
         s_fix[1] = wk.q;
-        s_fix[2] = wk.q < kTile ? tb.nxt[wk.q] & 0xFFu : 0u;
+        s_fix[2] = wk.q < kTile ? stop_why(s, J * kTile + wk.q) : 0u;
         s_fix[3] = mm;
     }
 }
@@ -796,6 +849,8 @@ Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_
     s.max_frames = max_frames;  // 0: no frame may be taken
     s.half = ring_size / 2;
     s.half32 = (uint32_t)std::min<uint64_t>(s.half, 0xFFFFFFFFull);
+    s.lim = std::min(s.half32, cap);
+    s.lim_dw = (uint32_t)(((uint64_t)s.lim + 7) / 4);
     s.tile_map = reinterpret_cast<uint2*>(ws + g.tile_map_off);
     s.sb_map = reinterpret_cast<uint2*>(ws + g.sb_map_off);
     s.ss_map = reinterpret_cast<uint2*>(ws + g.ss_map_off);
