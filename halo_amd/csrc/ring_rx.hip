@@ -591,7 +591,7 @@ __global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
     __shared__ uint32_t s_mx[kTileWaves];
     // (one tile per workgroup: workgroups that took tiles t, t + 2048, ... and loaded the next
     // one's bytes while working on the current one ran slower, 24.9 against 19.0 us for 1M 64 B
-    // records, profiles/r06/r6c: the tile's work, not its load, is what a CU waits on)
+    // records, profiles/r05/r5zc: the tile's work, not its load, is what a CU waits on)
     uint4 v[kTabQ<kTileWaves>];
     tile_load<kTileWaves>(s, blockIdx.x, v);
     guess_tile(s, blockIdx.x, tb, s_mx, v);
