@@ -626,6 +626,7 @@ __global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
     __shared__ uint32_t s_q[kLinkThreads];  // each thread's last tile's exit (its successor's entry)
     __shared__ uint32_t s_fix[4];           // the special tile's records, exit, why, longest record
     __shared__ uint32_t s_cut[2];           // the tile (and records before it) max_frames cuts inside
+    __shared__ uint32_t s_sj[3];            // the special tile's summary and the exit of the one before
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     const uint32_t mf = s.max_frames, nt = s.n_tiles;
     uint32_t t0 = 0, e = 0, base = 0;  // the next tile to link, its entry, records before it (uniform)
@@ -663,15 +664,21 @@ __global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
         }
         uint32_t prev_q = 0;
         if (j0 > t0 && j0 <= nt) prev_q = s.sum[j0 - 1].x >> 16;
-        uint32_t first = ~0u;
+        uint32_t first = ~0u, fx = 0, fy = 0, fpe = 0;  // this thread's first special tile: summary, exit before
 #pragma unroll
         for (uint32_t k = 0; k < kLinkPer; ++k) {
             const uint32_t j = j0 + k, g = sm[k].x & 0xFFFFu, q = sm[k].x >> 16;
             const uint32_t in = j == t0 ? e : prev_q - kTile;  // wraps (no match) when prev_q < kTile
             const bool special = j >= nt || in != g || q < kTile || j == nt - 1;
-            if (special && first == ~0u) first = j;
+            if (special && first == ~0u) {
+                first = j;
+                fx = sm[k].x;
+                fy = sm[k].y;
+                fpe = prev_q;
+            }
             prev_q = q;
         }
+        const uint32_t my_first = first;
         s_q[tid] = prev_q;
         // block: the first special tile J (every chunk that reaches the span's last tile has one)
 #pragma unroll
@@ -714,9 +721,16 @@ __global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
             __syncthreads();
             continue;
         }
-        const uint32_t jin = J == t0 ? e : (s.sum[J - 1].x >> 16) - kTile;  // J's real entry
-        const uint2 sj = s.sum[J];
-        __syncthreads();  // s_q / s_min / s_sum are rewritten below and by the next chunk
+        // J's summary and the exit of the tile before it, from the thread that found J (no reload)
+        if (my_first == J) {
+            s_sj[0] = fx;
+            s_sj[1] = fy;
+            s_sj[2] = fpe;
+        }
+        __syncthreads();
+        const uint32_t jin = J == t0 ? e : s_sj[2] - kTile;  // J's real entry
+        const uint2 sj = make_uint2(s_sj[0], s_sj[1]);
+        __syncthreads();  // s_q / s_min / s_sum / s_sj are rewritten below and by the next chunk
         if ((sj.x & 0xFFFFu) == jin) {  // uniform. The guess was right: the walk stops in J, or J is the last tile
             if (tid == 0) {
                 s_fix[0] = sj.y & 0xFFFu;
