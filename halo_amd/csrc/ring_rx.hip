@@ -552,10 +552,11 @@ __device__ __forceinline__ uint32_t keep_records(const Scan& s, uint32_t t, cons
 }
 
 // One tile of A: its tables, its guess, its walk, its records and summary.
+template <int W>
 __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& tb, uint32_t* s_mx,
-                                           const uint4 (&v)[kTabQ<kTileWaves>]) {
+                                           const uint4 (&v)[kTabQ<W>]) {
     const uint32_t tid = threadIdx.x;
-    const uint32_t n_act = tile_tabulate<kTileWaves>(s, t, tb, 0, v);
+    const uint32_t n_act = tile_tabulate<W>(s, t, tb, 0, v);
     // The guess: the first listed candidate whose chain of links does not stop inside the tile. The
     // dword before a record is often a decoy — a frame's last bytes and zero padding make a small
     // "length" (1.3 % of IMIX tiles, tools: a 570 B frame's last dword) — whose link lands nowhere;
@@ -563,7 +564,7 @@ __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& t
     uint32_t i0 = 0, F0 = ~0u;  // the chosen chain: its first listed index and its first break
     if (t > 0 && n_act <= kListMax) {
         for (uint32_t k = 0, tries = 0; k < n_act && tries < kGuessTries; ++tries) {  // uniform
-            const uint32_t F = first_break<kTileWaves>(tb, n_act, k), q = tb.nxt[tb.list[F]] & kPosMask;
+            const uint32_t F = first_break<W>(tb, n_act, k), q = tb.nxt[tb.list[F]] & kPosMask;
             if (!(q < kTile && (tb.nxt[q] & kLdsStop))) {
                 i0 = k;
                 F0 = F;
@@ -574,27 +575,32 @@ __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& t
     }
     const uint32_t g = t == 0 ? 0u : n_act ? tb.list[i0] : kNone;
     TileWalk wk{0, kNone};
-    if (g != kNone) wk = tile_walk<kTileWaves>(tb, n_act, i0, g, kListMax, F0);  // uniform (tile 0: i0 = 0)
+    if (g != kNone) wk = tile_walk<W>(tb, n_act, i0, g, kListMax, F0);  // uniform (tile 0: i0 = 0)
     const uint32_t mx = keep_records(s, t, tb, i0, wk.c);
     if ((tid & 63u) == 0) s_mx[tid >> 6] = mx;
     __syncthreads();
     if (tid == 0) {
         uint32_t m = 0;
-        for (uint32_t x = 0; x < kTileWaves; ++x) m = max(m, s_mx[x]);
+        for (uint32_t x = 0; x < (uint32_t)W; ++x) m = max(m, s_mx[x]);
         const uint32_t why = wk.q < kTile ? stop_why(s, t * kTile + wk.q) : 0u;
         s.sum[t] = make_uint2(g | (wk.q << 16), wk.c | (why << 12) | (m << 16));
     }
 }
 
-__global__ void __launch_bounds__(kThreads) ring_guess_kernel(const Scan s) {
+#ifndef HALO_RING_GUESS_WAVES
+#define HALO_RING_GUESS_WAVES 4  // waves per tile in A
+#endif
+constexpr uint32_t kGuessWaves = HALO_RING_GUESS_WAVES;
+
+__global__ void __launch_bounds__(kGuessWaves * 64) ring_guess_kernel(const Scan s) {
     __shared__ TileTab tb;
-    __shared__ uint32_t s_mx[kTileWaves];
+    __shared__ uint32_t s_mx[kGuessWaves];
     // (one tile per workgroup: workgroups that took tiles t, t + 2048, ... and loaded the next
     // one's bytes while working on the current one ran slower, 24.9 against 19.0 us for 1M 64 B
     // records, profiles/r05/r5zc: the tile's work, not its load, is what a CU waits on)
-    uint4 v[kTabQ<kTileWaves>];
-    tile_load<kTileWaves>(s, blockIdx.x, v);
-    guess_tile(s, blockIdx.x, tb, s_mx, v);
+    uint4 v[kTabQ<kGuessWaves>];
+    tile_load<kGuessWaves>(s, blockIdx.x, v);
+    guess_tile<kGuessWaves>(s, blockIdx.x, tb, s_mx, v);
 }
 
 constexpr uint32_t kLinkThreads = 1024, kLinkWaves = kLinkThreads / 64, kLinkPer = 16;  // 256 MB spans a chunk
@@ -886,7 +892,7 @@ Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_
 int launch_walk(const Scan& s, hipStream_t st) {
     const dim3 blk(kThreads);
     if (!HALO_RING_MAPS) {
-        hipLaunchKernelGGL(ring_guess_kernel, dim3(s.n_tiles), blk, 0, st, s);
+        hipLaunchKernelGGL(ring_guess_kernel, dim3(s.n_tiles), dim3(kGuessWaves * 64), 0, st, s);
         hipLaunchKernelGGL(ring_link_kernel, dim3(1), dim3(kLinkThreads), 0, st, s);
         hipLaunchKernelGGL(ring_copy_kernel, dim3((s.n_tiles + kTileWaves - 1) / kTileWaves), blk, 0, st, s);
         return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
