@@ -154,3 +154,27 @@ def test_guess_and_link_walk_equals_readpacket(oracle_lib, name, gen, kw, cap, m
             # needs none: DESIGN.md §14.2)
             tiles = (u // 4 + T - 1) // T
             assert repaired <= max(2, tiles // 10), (repaired, tiles)
+
+
+@pytest.mark.parametrize("ring_size,cap", [(1 << 12, 1514), (1 << 20, 1514), (1 << 26, 9014), (1 << 14, 16376)])
+def test_inner_tile_check_is_readpacket(ring_size, cap):
+    """ring_rx.hip tabulate_as<INNER>: in a tile that ends at least one longest record (lim =
+    min(size / 2, capacity), (lim + 7) / 4 dwords) before the span does, a position passes
+    ReadPacket's four checks exactly when 1 <= len <= lim, and its record is (len + 7) >> 2 dwords
+    — the shortcut the guess kernel takes instead of record_dwords."""
+    rng = np.random.default_rng(ring_size ^ cap)
+    half32 = min(ring_size // 2, 2**32 - 1)
+    lim = min(half32, cap)
+    lim_dw = (lim + 7) // 4
+    n_dw = 50 * T
+    for t in (0, 3, 47):
+        if t * T + T + lim_dw > n_dw:
+            continue
+        a = t * T + rng.integers(0, T, 20000)
+        ln = np.concatenate([rng.integers(0, 2 * lim + 8, 19000), rng.integers(0, 2**32, 1000, dtype=np.uint64)])
+        ln = ln.astype(np.int64)
+        dw = (ln >> 2) + 1 + ((ln & 3) != 0)
+        full = (a < n_dw) & (ln != 0) & (ln <= half32) & (n_dw - a >= dw) & (ln <= cap)
+        short = ((ln - 1) & 0xFFFFFFFF) < lim
+        assert np.array_equal(full, short)
+        assert np.array_equal(dw[full], (ln[full] + 7) >> 2)
