@@ -1398,6 +1398,9 @@ rx_stream_kernel(const RxParams p) {
 #ifndef HALO_RX_LANE_MAX_BLOCKS
 #define HALO_RX_LANE_MAX_BLOCKS HALO_RX_MAX_BLOCKS
 #endif
+#ifndef HALO_RX_HIST_HALVE_MAX  // lane-kernel grids up to this many blocks are halved when a histogram is kept
+#define HALO_RX_HIST_HALVE_MAX 16384u
+#endif
 constexpr int kVariantMix = -1, kVariantStream = 2, kVariantStreamMixed = 3;
 
 uint32_t grid_for(uint64_t n, uint32_t frames_per_wave, uint64_t max_blocks = HALO_RX_MAX_BLOCKS,
@@ -1414,7 +1417,12 @@ hipError_t launch_variant(const RxParams& p, int variant, hipStream_t s) {
     switch (variant) {
         case 1: {
             constexpr uint32_t wpb = HALO_RX_LANE_BLOCK / 64;
-            hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid_for(p.n, 64, HALO_RX_LANE_MAX_BLOCKS * 4 / wpb, wpb)),
+            uint32_t grid = grid_for(p.n, 64, HALO_RX_LANE_MAX_BLOCKS * 4 / wpb, wpb);
+            // with a status histogram, batches up to 1M frames take half the waves, two frame groups
+            // each: half the arrivals in the histogram tree, whose tail is a fixed cost per launch
+            // (1M x 64 B: +2.1 instead of +2.7 us, 8192 blocks; 4096 gave no gain, profiles/r05/r5zm)
+            if (p.hist && grid <= HALO_RX_HIST_HALVE_MAX) grid = (grid + 1) / 2;
+            hipLaunchKernelGGL((rx_lane_kernel<LAYOUT, FUSE>), dim3(grid),
                                dim3(HALO_RX_LANE_BLOCK), HALO_RX_LANE_LDS_PAD, s, p);
             break;
         }
