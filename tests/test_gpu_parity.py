@@ -351,7 +351,8 @@ def test_histogram_tree_across_grid_sizes_and_launches(dev, variant):
     from halo_amd import protocol, synth
     from halo_amd._lib import NetIf
 
-    for n, length in [(7, 64), (64 * 1024 + 1, 64), (40000, 200), (1 << 21, 64)]:
+    # (1M frames = 16384 lane blocks: the largest grid halved with a histogram; one group more is not)
+    for n, length in [(7, 64), (64 * 1024 + 1, 64), (40000, 200), (1 << 20, 64), ((1 << 20) + 64, 64), (1 << 21, 64)]:
         lay = synth.layout(n, length=length, mutate_shift=3)
         fr = synth.frames_device(lay, NetIf.make(), device=dev)
         hist = torch.zeros(14, dtype=torch.int32, device=dev)
