@@ -536,8 +536,9 @@ __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
 // Three launches, each tile read once (the map path it replaces: seven launches and a serial chain
 // of map lookups between them, 0.19 ms for 1M 64 B records, profiles/r05/r5f).
 struct RingCtl {
-    uint32_t total;      // records the walk takes before it stops (max_frames ignored)
     uint32_t last_tile;  // the tile the walk ends in
+    uint32_t n;          // records taken (min(total, max_frames)): C reads (last_tile, n) in one load
+    uint32_t total;      // records the walk takes before it stops (max_frames ignored)
 };
 
 // A tile's walk into its workspace slot (position | length << 16) and its longest record.
@@ -787,6 +788,7 @@ __global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
         const uint32_t n = min(base, mf);
         s.ctl->total = base;
         s.ctl->last_tile = last;
+        s.ctl->n = min(base, mf);
         halo_rx_ring_scan_t info;
         info.n_frames = n;
         info.stop = n < base ? HALO_RING_STOP_MAX : why;
@@ -800,9 +802,12 @@ __global__ void __launch_bounds__(kLinkThreads) ring_link_kernel(const Scan s) {
 __global__ void __launch_bounds__(kThreads) ring_copy_kernel(const Scan s) {
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t t = blockIdx.x * kTileWaves + w;
-    if (t > s.ctl->last_tile) return;  // wave-uniform: tiles past the walk's end hold nothing
-    const uint32_t n = s.info->n_frames;
-    const uint2 te = s.tile_entry[t];
+    // the three reads in one round trip (the tile's entry read before the walk's end is known)
+    const uint64_t tw = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(s.tile_entry + t));  // whole-workgroup padded
+    const uint2 te = make_uint2((uint32_t)tw, (uint32_t)(tw >> 32));
+    const uint2 ln = *reinterpret_cast<const uint2*>(s.ctl);  // (last_tile, n)
+    const uint32_t last = ln.x, n = ln.y;
+    if (t > last) return;  // wave-uniform: tiles past the walk's end hold nothing
     const uint32_t base = te.x;
     if (base >= n) return;
     const uint32_t cnt = min(te.y, n - base), tbase = t * kTile;
@@ -852,7 +857,7 @@ Geom geometry(uint64_t used, uint32_t cap) {
     g.sb_entry_off = o;
     o += (uint64_t)g.n_sb * sizeof(uint2);
     g.tile_entry_off = o;
-    o += (uint64_t)g.n_tiles * sizeof(uint2);
+    o += (uint64_t)(g.n_tiles + kTileWaves - 1) / kTileWaves * kTileWaves * sizeof(uint2);  // C reads whole workgroups
     g.total_off = o;
     o += 256;
     g.bytes = o;
@@ -881,8 +886,8 @@ Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_
     s.ss_entry = reinterpret_cast<uint2*>(ws + g.ss_entry_off);
     s.sb_entry = reinterpret_cast<uint2*>(ws + g.sb_entry_off);
     s.tile_entry = reinterpret_cast<uint2*>(ws + g.tile_entry_off);
-    s.total = reinterpret_cast<uint32_t*>(ws + g.total_off);
     s.ctl = reinterpret_cast<RingCtl*>(ws + g.total_off);
+    s.total = &s.ctl->total;
     s.sum = reinterpret_cast<uint2*>(ws + g.sum_off);
     s.tmp = reinterpret_cast<uint32_t*>(ws + g.tmp_off);
     s.info = d_info;
