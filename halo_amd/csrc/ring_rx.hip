@@ -529,7 +529,7 @@ __global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
 //    the workspace, with a summary: (guess, where the walk leaves or stops, records, why, longest).
 // B. One workgroup links the summaries: tile t's guess is right when the walk through tile t - 1
 //    (itself verified) enters tile t there. By induction from tile 0 every guess that matches is
-//    the real entry, so a chunk of 16384 tiles is settled by one comparison per tile and a prefix
+//    the real entry, so a chunk of 8192 tiles is settled by one comparison per tile and a prefix
 //    sum; a tile whose guess is wrong (a decoy in the record that straddles its start) is walked
 //    again by the workgroup from its real entry, and the linking goes on after it.
 // C. Every tile copies its records to (dword offset, length) at its place in the batch.
@@ -608,7 +608,10 @@ __global__ void __launch_bounds__(kGuessWaves * 64) ring_guess_kernel(const Scan
     guess_tile<kGuessWaves>(s, blockIdx.x, tb, s_mx, v);
 }
 
-constexpr uint32_t kLinkThreads = 1024, kLinkWaves = kLinkThreads / 64, kLinkPer = 16;  // 256 MB spans a chunk
+#ifndef HALO_RING_LINK_THREADS
+#define HALO_RING_LINK_THREADS 512  // 1024: 8.7 us, 256: 10.6, 512: 8.0 for 1M 64 B records (profiles/r05/r5zt)
+#endif
+constexpr uint32_t kLinkThreads = HALO_RING_LINK_THREADS, kLinkWaves = kLinkThreads / 64, kLinkPer = 16;  // 512: a chunk spans 128 MB
 constexpr uint32_t kLinkChunk = kLinkThreads * kLinkPer;
 
 // B's second walk of tile J from its real entry `jin` (the guess was wrong): its records to the
