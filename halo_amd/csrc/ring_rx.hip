@@ -556,12 +556,24 @@ __device__ __forceinline__ uint32_t keep_records(const Scan& s, uint32_t t, cons
     return mx;  // the wave's
 }
 
+#ifdef HALO_GUESS_TRACE  // tools only: phase timestamps (100 MHz) of every tile into the frame offsets
+#define GTRACE(k) do { if (threadIdx.x == 0) reinterpret_cast<uint64_t*>(s.off_dw)[8ull * t + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define GTRACE(k) ((void)0)
+#endif
+
 // One tile of A: its tables, its guess, its walk, its records and summary.
 template <int W>
 __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& tb, uint32_t* s_mx,
                                            const uint4 (&v)[kTabQ<W>]) {
     const uint32_t tid = threadIdx.x;
+#ifdef HALO_GUESS_TRACE
+    if (tid == 0) __builtin_amdgcn_s_waitcnt(0);  // (the tile's bytes are in)
+    { const uint32_t sink = v[0].x; if (sink == 0xDEADBEEFu && tid == 1) reinterpret_cast<uint32_t*>(s.off_dw)[0] = sink; }
+#endif
+    GTRACE(1);
     const uint32_t n_act = tile_tabulate<W>(s, t, tb, 0, v);
+    GTRACE(2);
     // The guess: the first listed candidate whose chain of links does not stop inside the tile. The
     // dword before a record is often a decoy — a frame's last bytes and zero padding make a small
     // "length" (1.3 % of IMIX tiles, tools: a 570 B frame's last dword) — whose link lands nowhere;
@@ -578,9 +590,11 @@ __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& t
             k = F + 1;
         }
     }
+    GTRACE(3);
     const uint32_t g = t == 0 ? 0u : n_act ? tb.list[i0] : kNone;
     TileWalk wk{0, kNone};
     if (g != kNone) wk = tile_walk<W>(tb, n_act, i0, g, kListMax, F0);  // uniform (tile 0: i0 = 0)
+    GTRACE(4);
     const uint32_t mx = keep_records(s, t, tb, i0, wk.c);
     if ((tid & 63u) == 0) s_mx[tid >> 6] = mx;
     __syncthreads();
@@ -590,6 +604,7 @@ __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& t
         const uint32_t why = wk.q < kTile ? stop_why(s, t * kTile + wk.q) : 0u;
         s.sum[t] = make_uint2(g | (wk.q << 16), wk.c | (why << 12) | (m << 16));
     }
+    GTRACE(5);
 }
 
 #ifndef HALO_RING_GUESS_WAVES
@@ -604,6 +619,9 @@ __global__ void __launch_bounds__(kGuessWaves * 64) ring_guess_kernel(const Scan
     // one's bytes while working on the current one ran slower, 24.9 against 19.0 us for 1M 64 B
     // records, profiles/r05/r5zc: the tile's work, not its load, is what a CU waits on)
     uint4 v[kTabQ<kGuessWaves>];
+#ifdef HALO_GUESS_TRACE
+    { const uint32_t t = blockIdx.x; GTRACE(0); }
+#endif
     tile_load<kGuessWaves>(s, blockIdx.x, v);
     guess_tile<kGuessWaves>(s, blockIdx.x, tb, s_mx, v);
 }
@@ -905,6 +923,9 @@ int launch_walk(const Scan& s, hipStream_t st) {
     const dim3 blk(kThreads);
     if (!HALO_RING_MAPS) {
         hipLaunchKernelGGL(ring_guess_kernel, dim3(s.n_tiles), dim3(kGuessWaves * 64), 0, st, s);
+#ifdef HALO_GUESS_TRACE
+        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;  // A alone: its trace is in d_off
+#endif
         hipLaunchKernelGGL(ring_link_kernel, dim3(1), dim3(kLinkThreads), 0, st, s);
         hipLaunchKernelGGL(ring_copy_kernel, dim3((s.n_tiles + kTileWaves - 1) / kTileWaves), blk, 0, st, s);
         return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
