@@ -355,6 +355,7 @@ void fuzz_planning(int iters) {
                 if (!cnt) break;  // a single frame larger than the staging chunk
                 ++g_packed;
                 CHECK(used <= chunk_bytes);
+                CHECK(used == halo::pack_need(plen.data() + next, cnt, cap));  // the pre-check's sum is the packer's
                 for (uint32_t j = 0; j < cnt; ++j)
                     if (plen[next + j] <= cap)
                         CHECK(memcmp(staging + 4ull * h_off[j], bytes + offs[next + j], plen[next + j]) == 0);
