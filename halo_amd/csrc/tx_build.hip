@@ -527,7 +527,7 @@ __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t s
 #define HALO_TXB_SMALL 1
 #endif
 #ifndef HALO_TXB_DESC_PREFETCH
-#define HALO_TXB_DESC_PREFETCH 0
+#define HALO_TXB_DESC_PREFETCH 1  // 64 B: 24.9 / 24.7 us against 25.5 / 25.0 without (profiles/r05/r5zx)
 #endif
 #ifndef HALO_TXB_DESC_LDS  // G = 1: the tile's descriptors read coalesced, through LDS
 #define HALO_TXB_DESC_LDS 0  // measured slower: 64 B 30.2 / 30.5 us against 29.1 / 29.3 (profiles/r04/r4p)
