@@ -570,6 +570,24 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     // block) ran 0.6 us slower; one level of 64 / 256 / 1024 slots ran +0.3 / +1.3 / +9 us (the
     // completers' adds queue on one counter at ~10 ns each). DESIGN.md §14.5.
     constexpr unsigned long long kOne = 1ull << 40, kCount = kOne - 1;
+#ifndef HALO_HIST_RUNS
+#define HALO_HIST_RUNS 16  // 0: off. 1M x 64 B: +1.8-2.0 us against +2.1-2.4 for the two-level tree;
+#endif                     // runs of 8: +5.6, of 32: +1.8-2.0 (profiles/r05/r5zz2)
+    if (HALO_HIST_RUNS && g <= kHistSlots * (uint32_t)(HALO_HIST_RUNS ? HALO_HIST_RUNS : 1)) {  // uniform
+        // Grids up to 16384 blocks: slot = a run of 16 consecutive blocks. Workgroups are dispatched
+        // in order, so the runs complete one after another through the launch instead of all at its
+        // end, and each completer adds straight into the caller's counters (one level: the adds
+        // arrive spread out, not queued on one counter at the tail).
+        constexpr uint32_t R = HALO_HIST_RUNS ? HALO_HIST_RUNS : 1;
+        const uint32_t r = blockIdx.x / R;
+        unsigned long long* w = tree + r * kHistStride + t;
+        const unsigned long long add = kOne | hist.s[t];
+        const unsigned long long now1 = atomicAdd(w, add) + add;
+        if ((now1 >> 40) != (g - r * R < R ? g - r * R : R)) return;
+        atomicExch(w, 0ull);
+        if (now1 & kCount) atomicAdd(&p.hist_out[t], (uint32_t)(now1 & kCount));
+        return;
+    }
     unsigned long long* l1 = tree + s * kHistStride + t;
     unsigned long long now = atomicAdd(l1, kOne | hist.s[t]) + (kOne | hist.s[t]);
     if ((now >> 40) != g / kHistSlots + (g % kHistSlots > s)) return;
