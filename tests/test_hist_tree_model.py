@@ -1,4 +1,5 @@
-"""CPU: the status histogram's two-level tree (rx_parse.hip flush_hist), restated in Python.
+"""CPU: the status histogram's trees (rx_parse.hip flush_hist), restated in Python: the two-level tree
+(grids above 16384 blocks) and, at the end of the file, the one level of 16-block runs.
 
 Every block adds (1 << 40 | count) to status word k of level-1 slot b % 1024; the add that brings
 the slot's arrivals to its block count (g // 1024 + (g % 1024 > s)) moves the slot's total to
@@ -54,3 +55,37 @@ def test_tree_counts_exact_and_words_reset(g):
         assert out[0] == counts.sum(), (g, launch)
         assert done == min(g, SLOTS)  # every used level-1 slot completed exactly once
         assert all(v == 0 for v in l1.values()) and all(v == 0 for v in l2.values())
+
+
+RUN = 16  # HALO_HIST_RUNS
+
+
+def run_runs(counts: np.ndarray, order: np.ndarray, words: dict, out: np.ndarray) -> int:
+    """flush_hist for grids up to SLOTS * RUN blocks: block b adds (1 << 40 | count) to word b // RUN;
+    the add that brings a run's arrivals to its size (min(RUN, g - RUN * r)) zeroes the word and adds
+    the run's total to the caller's counter."""
+    g = len(counts)
+    done = 0
+    for b in order:
+        r = b // RUN
+        now = words.get(r, 0) + (ONE | int(counts[b]))
+        words[r] = now
+        if now >> 40 != min(RUN, g - RUN * r):
+            continue
+        done += 1
+        words[r] = 0
+        out[0] += now & MASK
+    return done
+
+
+@pytest.mark.parametrize("g", [1, 15, 16, 17, 1023, 8192, 8193, 16383, 16384])
+def test_runs_counts_exact_and_words_reset(g):
+    rng = np.random.default_rng(g + 7)
+    words = {}
+    for launch in range(3):
+        counts = rng.integers(0, 64, g)
+        out = np.zeros(1, np.int64)
+        done = run_runs(counts, rng.permutation(g), words, out)
+        assert out[0] == counts.sum(), (g, launch)
+        assert done == (g + RUN - 1) // RUN  # every run completed exactly once
+        assert max(words) < SLOTS and all(v == 0 for v in words.values())
