@@ -564,11 +564,12 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
         if (hist.s[t]) atomicAdd(&p.hist_out[t], hist.s[t]);
         return;
     }
-    // The tree costs a fixed ~2.5 us per launch, not a per-block cost (1M frames: +2.7 us, 4M: +2.4,
-    // 16M: +1.4; counting, the LDS adds and the barrier alone: +0.4): the last block's two dependent
-    // round trips. Arrivals in one word with only the statuses a block saw (one atomic per clean
-    // block) ran 0.6 us slower; one level of 64 / 256 / 1024 slots ran +0.3 / +1.3 / +9 us (the
-    // completers' adds queue on one counter at ~10 ns each). DESIGN.md §14.5.
+    // What it costs is a fixed tail per launch, not a per-block price (two-level tree: 1M frames
+    // +2.7 us, 4M +2.4, 16M +1.4; counting, the LDS adds and the barrier alone +0.4): the last
+    // block's chain of dependent round trips. Arrivals in one word with only the statuses a block saw
+    // ran 0.6 us slower; one level of 64 / 256 / 1024 slots strided over the grid ran +0.3 / +1.3 / +9
+    // us (their completers all finish at the end and queue on one counter, ~10 ns an add). Runs of
+    // consecutive blocks complete through the launch instead. DESIGN.md §14.5.
     constexpr unsigned long long kOne = 1ull << 40, kCount = kOne - 1;
 #ifndef HALO_HIST_RUNS
 #define HALO_HIST_RUNS 16  // 0: off. 1M x 64 B: +1.8-2.0 us against +2.1-2.4 for the two-level tree;
