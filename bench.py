@@ -1411,7 +1411,7 @@ def main():
         sec["config2_status_histogram"] = {
             "mpps": round(n * args.steps / wh / 1e6, 1), "kernel_ms": round(kh, 5), "roofline": roofline(alg, kh),
             "vs_headline": round(kern_ms / kh, 4), "hist_frames": hsum, "hist_ok": int(hist[0].item()),
-            "what": "the headline step with d_status_hist (block-aggregated in LDS, then a fence-free two-level tree of per-status (arrivals, count) words into the caller's counters)"}
+            "what": "the headline step with d_status_hist (block-aggregated in LDS, then fence-free self-completing (arrivals, count) words: one level of 16-block runs for grids up to 16384 blocks, a two-level tree above; the lane grid halved up to 1M frames)"}
         assert hsum == n * (args.steps + args.warmup) and int(hist[0].item()) == hsum
         # the batch stream handed over 8 batches per launch (halo_rx_parse_batches_device): the ramp
         # and tail of a 1M-frame launch paid once per 8M frames
