@@ -56,6 +56,8 @@ def parse_args():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-secondary", action="store_true")
+    p.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                   help="the full record (prose, probe tables, curves); stdout carries the compact line")
     return p.parse_args()
 
 
@@ -1283,6 +1285,102 @@ def cpu_baseline(fr, seconds: float):
                                    "note": "the box's CPU share for one GPU (OMP_NUM_THREADS)"}}
 
 
+LINE_LIMIT = 7680  # bytes: the final stdout line stays under 8 KB, what the driver parses
+# per-entry numbers the stdout line keeps; everything else (prose, probe tables, per-size curves'
+# percentiles) goes to the detail file only
+_KEEP_NUM = ("mpps", "mstrings_per_s", "mlookups_per_s", "mrecords_per_s", "gbit_s", "kernel_ms", "ms_per_batch",
+             "us_per_batch", "ok", "speedup_vs_separate", "vs_headline", "vs_headline_per_batch", "failing_frac",
+             "crossover_frames", "cpu_port_ns_per_frame", "value", "unit", "ms_per_step")
+_KEEP_ROOF = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_session", "frac_frames_only",
+              "peak_measured_read", "frac_of_measured", "size_matched_probe_ms", "frac_of_size_matched",
+              "frac_of_gather_probe", "frac_of_load_pattern_probe", "frac_of_layout_matched")
+_SAMPLE_MAX = 200
+
+
+def _compact_roofline(r: dict) -> dict:
+    return {k: r[k] for k in _KEEP_ROOF if k in r}
+
+
+def _compact_cpu(c: dict) -> dict:
+    out = {k: c[k] for k in ("value", "unit", "cores", "kind") if k in c}
+    if "sample" in c:
+        out["sample"] = str(c["sample"])[:_SAMPLE_MAX]
+    for k in ("multi_thread", "multi_thread_share"):
+        if isinstance(c.get(k), dict):
+            out[k] = {kk: c[k][kk] for kk in ("value", "threads", "cpus_in_affinity") if kk in c[k]}
+    return out
+
+
+def _compact_entry(e):
+    """Numbers only: the whitelisted scalars of an entry, its roofline's fractions, its CPU baseline's
+    value, and the same for every nested entry (compact records, launch-per-poll, per-size curves)."""
+    if not isinstance(e, dict):
+        return e if isinstance(e, (int, float, bool)) else None
+    if e and all(k.isdigit() and isinstance(v, dict) for k, v in e.items()):  # a per-size curve: medians only
+        return {k: v.get("us_median") for k, v in e.items()}
+    out = {}
+    for k, v in e.items():
+        if k == "roofline" and isinstance(v, dict):
+            out[k] = {kk: v[kk] for kk in ("frac", "frac_of_size_matched", "frac_of_gather_probe",
+                                             "frac_of_load_pattern_probe", "frac_of_layout_matched",
+                                             "traffic_session") if kk in v}
+        elif k == "cpu_baseline" and isinstance(v, dict):
+            out[k] = {kk: v[kk] for kk in ("value", "unit", "cores") if kk in v}
+        elif isinstance(v, dict):
+            c = _compact_entry(v)
+            if c:
+                out[k] = c
+        elif k in _KEEP_NUM and isinstance(v, (int, float, bool, str)) and not (isinstance(v, str) and len(v) > 16):
+            out[k] = v
+    return out
+
+
+def compact_line(line: dict, limit: int = LINE_LIMIT) -> dict:
+    """The stdout JSON line the driver parses: the headline keys, `roofline`, `cpu_baseline`,
+    `config4_128M_one_gpu` and, per secondary, its numbers only. Prose fields (what / note / sample
+    beyond 200 chars / path / mix) and probe tables stay in the detail file. If the result would still
+    exceed `limit` bytes, secondaries are dropped largest first (named in `secondary_dropped`)."""
+    out = {}
+    for k, v in line.items():
+        if k == "roofline":
+            out[k] = _compact_roofline(v)
+        elif k == "cpu_baseline":
+            out[k] = None if v is None else _compact_cpu(v)
+        elif k == "per_rank":
+            out[k] = [{"rank": r.get("rank"), "pci_bus_id": r.get("pci_bus_id"), "kernel_ms": r.get("kernel_ms"),
+                       "valid": (r.get("validation") or {}).get("valid")} for r in v]
+        elif k == "config4_128M_one_gpu" and isinstance(v, dict):
+            c = {kk: v[kk] for kk in ("frames", "steps", "value", "unit", "gbit_s", "ms_per_step", "kernel_ms",
+                                      "alg_bytes_per_launch") if kk in v}
+            c["roofline"] = _compact_roofline(v.get("roofline", {}))
+            out[k] = c
+        elif k == "secondary" and isinstance(v, dict):
+            out[k] = {name: _compact_entry(e) for name, e in v.items()}
+        elif k in ("note", "whole_shard_launch") and isinstance(v, dict):
+            out[k] = _compact_entry(v)
+        else:
+            out[k] = v
+    while len(json.dumps(out)) > limit and out.get("secondary"):
+        name = max(out["secondary"], key=lambda n: len(json.dumps(out["secondary"][n])))
+        del out["secondary"][name]
+        out.setdefault("secondary_dropped", []).append(name)
+    return out
+
+
+def emit_line(line: dict, detail_path: str) -> str:
+    """Write the full record to `detail_path` (a JSON file) and print the compact line on stdout."""
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(detail_path)), exist_ok=True)
+        with open(detail_path, "w") as f:
+            json.dump(line, f, indent=1)
+        log(f"[bench] full record: {detail_path}")
+    except OSError as e:
+        log(f"[bench] could not write {detail_path}: {e}")
+    s = json.dumps(compact_line(line))
+    print(s, flush=True)
+    return s
+
+
 def main():
     args = parse_args()
     plan = rank_plan(args.gpus, os.environ)
@@ -1373,7 +1471,7 @@ def main():
                             "not a scaling point")
         d.close()
         if d.rank == 0:
-            print(json.dumps(line), flush=True)
+            emit_line(line, args.detail)
         sys.exit(0 if line["validated"] else 3)
     del shard
     line["roofline"]["note"] = ("achieved = (frame bytes + 6 B metadata + 32 B record) per launch / average "
@@ -1522,7 +1620,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(bs[0], args.cpu_seconds)
     d.close()
     if d.rank == 0:
-        print(json.dumps(line), flush=True)
+        emit_line(line, args.detail)
     if not line["validated"]:
         sys.exit(3)
 
