@@ -298,6 +298,10 @@ def bench_lib():
         L.halo_bench_rx_flow_steps.argtypes = [i32, vp, vp, vp, u32, u32, vp, u32, vp, u32, u32, vp, u32, vp] + tail
         L.halo_bench_stream_rw.restype = ctypes.c_int
         L.halo_bench_stream_rw.argtypes = [vp, vp, i32, u64, u64, vp] + tail
+        L.halo_bench_stream_rw_v.restype = ctypes.c_int
+        L.halo_bench_stream_rw_v.argtypes = [vp, vp, i32, u64, u64, vp, i32] + tail
+        L.halo_bench_stream_rw_name.restype = ctypes.c_char_p
+        L.halo_bench_stream_rw_name.argtypes = [i32]
         L.halo_bench_ring_scan_steps.restype = ctypes.c_int
         L.halo_bench_ring_scan_steps.argtypes = [i32, vp, u64, u64, u32, vp, vp, vp, vp, u64] + tail
         L.halo_bench_pci_bus_id.restype = ctypes.c_int
@@ -1115,11 +1119,15 @@ def measure_read_peak(dev, d: Dist, gib: int = 4):
     return MEASURED_READ_GBS
 
 
+LAST_PROBE_SHAPES = {}  # the last size_matched_probe: ms per shape
+
+
 def size_matched_probe(dev, read_bytes: int, write_bytes: int, d: Dist, nbuf: int = 8, steps: int = 50):
-    """Speed-of-light for a kernel's byte shape on this box: one kernel that streams `read_bytes`
-    in (16 KB tiles, 16-byte loads) and writes `write_bytes` out (coalesced 16-byte stores) over
-    `nbuf` rotating buffers, doing no other work (tools/bench_loop.hip stream_rw_kernel). Returns
-    the average launch duration in ms."""
+    """Speed-of-light for a kernel's byte shape on this box: kernels that stream `read_bytes` in
+    (tiles of 16-byte loads) and write `write_bytes` out (coalesced 16-byte stores) over `nbuf`
+    rotating buffers, doing no other work (tools/bench_loop.hip stream_rw_kernel). Every shape of
+    the family (16 / 32 / 64 KB tiles, plain and non-temporal) is timed; returns the fastest one's
+    average launch duration in ms (VERDICT r5 #3: one shape alone was not a ceiling at 16M frames)."""
     import ctypes
 
     import torch
@@ -1129,11 +1137,17 @@ def size_matched_probe(dev, read_bytes: int, write_bytes: int, d: Dist, nbuf: in
     dsts = [torch.empty(w16, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     sink = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
     arr = lambda xs: (ctypes.c_void_p * len(xs))(*[x.data_ptr() for x in xs])  # noqa: E731
-    _, k = time_native(bench_lib().halo_bench_stream_rw, arr(srcs), arr(dsts), nbuf, r16, w16, sink.data_ptr(),
-                       steps=steps, warmup=5, d=d)
+    L = bench_lib()
+    LAST_PROBE_SHAPES.clear()
+    v = 0
+    while L.halo_bench_stream_rw_name(v) is not None:
+        _, k = time_native(L.halo_bench_stream_rw_v, arr(srcs), arr(dsts), nbuf, r16, w16, sink.data_ptr(), v,
+                           steps=steps, warmup=5, d=d)
+        LAST_PROBE_SHAPES[L.halo_bench_stream_rw_name(v).decode()] = round(k, 5)
+        v += 1
     del srcs, dsts, sink
     torch.cuda.empty_cache()
-    return k
+    return min(LAST_PROBE_SHAPES.values())
 
 
 def dev_of(t):
@@ -1143,6 +1157,9 @@ def dev_of(t):
 def with_probe(r: dict, probe_ms: float, kernel_ms: float) -> dict:
     r["size_matched_probe_ms"] = round(probe_ms, 5)
     r["frac_of_size_matched"] = round(probe_ms / kernel_ms, 4)
+    if LAST_PROBE_SHAPES:
+        r["size_matched_shape"] = min(LAST_PROBE_SHAPES, key=LAST_PROBE_SHAPES.get)
+        r["size_matched_shapes_ms"] = dict(LAST_PROBE_SHAPES)
     return r
 
 
@@ -1233,8 +1250,12 @@ def e2e_host(dev, netif, steps: int):
     return res
 
 
-def cpu_baseline(fr, seconds: float):
-    """The C oracle (scalar restatement of the Go path) on the host, 1 thread, then all cores."""
+def cpu_baseline(fr, seconds: float, rotate: int):
+    """The C oracle (scalar restatement of the Go path) on the host over the SAME workload the GPU
+    line rotates through: the rank's whole shard (`rotate` batches, 16M x 64 B = 1.07 GB of frames +
+    512 MB of records at the defaults), so no pass is served from the CPU caches.
+    One thread (the reference's one goroutine per NetIf), the box's CPU share for one GPU
+    (OMP_NUM_THREADS) and every CPU in the affinity mask, index-sharded over the threads."""
     import numpy as np
 
     from oracle import oracle
@@ -1242,29 +1263,23 @@ def cpu_baseline(fr, seconds: float):
     oracle.build()
     lay = fr["layout"]
     host = fr["bytes"].cpu().numpy()
+    n = lay["n"]
+    out = np.zeros(n, dtype=oracle.RESULT_DTYPE)  # touched once, reused by every pass
     netif = oracle.NetIf.make()
     res = {}
-    # one thread (the reference's one goroutine per NetIf), the host's CPU share for this process
-    # (the GPU box exports OMP_NUM_THREADS = its per-GPU share) and every CPU in the affinity mask
-    # (§8d "all cores"), capped only so that each thread gets >= 4096 frames
     affinity = len(os.sched_getaffinity(0))
     share = max(1, min(affinity, int(os.environ.get("OMP_NUM_THREADS") or affinity)))
-    every = max(1, min(affinity, lay["n"] // 4096, 1024))
+    every = max(1, min(affinity, n // 4096, 1024))
     for threads in sorted({1, share, every}):
-        oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads)  # warm
-        # every thread parses its shard `reps` times per call, so one thread start serves many passes
-        # (at 256 threads, a start per pass cost more than the pass: 92 vs 191 Mpps on 16, r5s)
-        passes, reps, t0 = 0, 1, time.perf_counter()
+        oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads, out=out)  # warm
+        passes, t0 = 0, time.perf_counter()
         while True:
-            c0 = time.perf_counter()
-            oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads, reps=reps)
-            passes += reps
+            oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads, out=out)
+            passes += 1
             el = time.perf_counter() - t0
             if el >= seconds / 2 or (threads > 1 and el >= 2.0):
                 break
-            if threads > 1 and time.perf_counter() - c0 < 0.25:
-                reps *= 2
-        res[threads] = (passes * lay["n"] / el / 1e6, passes, el)
+        res[threads] = (passes * n / el / 1e6, passes, el)
     one, mt, sh = res[1], res[every], res[share]
     model = "unknown"
     try:
@@ -1274,13 +1289,13 @@ def cpu_baseline(fr, seconds: float):
                 break
     except OSError:
         pass
+    shard = f"{n >> 20}M x {int(lay['lens'][0])}B UDP frames ({rotate} batches, the GPU line's rotation)"
     return {"value": round(one[0], 3), "unit": "Mpps", "cores": 1, "kind": "port",
-            "sample": f"{lay['n']} x {int(lay['lens'][0])}B UDP frames (batch 0 of the workload), "
-                      f"{one[1]} passes in {one[2]:.1f}s, oracle/halo_rx_oracle.c -O2, one thread "
-                      f"(the reference's one goroutine per NetIf); cpu={model}",
+            "sample": f"{shard}, {one[1]} passes in {one[2]:.1f}s, oracle/halo_rx_oracle.c -O2, one thread; "
+                      f"cpu={model}",
             "multi_thread": {"value": round(mt[0], 3), "threads": every, "passes": mt[1],
                              "cpus_in_affinity": affinity, "cpu_model": model,
-                             "note": "index-sharded over threads = len(sched_getaffinity) (>= 4096 frames each)"},
+                             "note": "the same shard index-sharded over threads = len(sched_getaffinity)"},
             "multi_thread_share": {"value": round(sh[0], 3), "threads": share, "passes": sh[1],
                                    "note": "the box's CPU share for one GPU (OMP_NUM_THREADS)"}}
 
@@ -1614,10 +1629,11 @@ def main():
         torch.cuda.empty_cache()
         line["secondary"] = sec
     if d.world == 1 and not args.no_cpu:  # rank 0 at N=1 only
-        bs = make_batches(dev, netif, n=n, rotate=1, rank=0)
+        _, cshard = shard_batches(dev, netif, rank=0, n=n, rotate=args.rotate)
         torch.cuda.synchronize()
-        log("[cpu baseline] timing the oracle on the host")
-        line["cpu_baseline"] = cpu_baseline(bs[0], args.cpu_seconds)
+        log("[cpu baseline] timing the oracle on the host over the rotated shard")
+        line["cpu_baseline"] = cpu_baseline(cshard, args.cpu_seconds, args.rotate)
+        del cshard
     d.close()
     if d.rank == 0:
         emit_line(line, args.detail)

@@ -201,7 +201,8 @@ func (x *Ctx) SetResident(maxFrames int, maxBytes uint64) error {
 // those kernels too, which end only 20 ms after their last request.
 func DeviceSynchronize(device int) error { return halo(C.halo_rx_device_synchronize(C.int(device))) }
 
-// Release frees the device-wide state of the library on `device` (halo_rx_release).
+// Release drains `device` and hands back its status-histogram tree keys (halo_rx_release); the
+// trees, rings, contexts and captured graphs stay valid.
 func Release(device int) error { return halo(C.halo_rx_release(C.int(device))) }
 
 // Close frees the context.

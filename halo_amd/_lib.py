@@ -222,6 +222,7 @@ _u8p = ctypes.c_void_p
 _PROTOS = {
     "halo_rx_version": (ctypes.c_char_p, []),
     "halo_rx_init": (ctypes.c_int, [ctypes.c_int]),
+    "halo_rx_debug_hist_keys": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_uint32]),
     "halo_rx_device_synchronize": (ctypes.c_int, [ctypes.c_int]),
     "halo_rx_release": (ctypes.c_int, [ctypes.c_int]),
     "halo_rx_strerror": (ctypes.c_char_p, [ctypes.c_int]),

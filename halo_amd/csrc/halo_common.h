@@ -77,13 +77,22 @@ int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 // streams of other devices need no host-side key at all.
 constexpr uint32_t kHistSlots = 1024, kHistFan = 32, kHistStride = 16;
 constexpr uint32_t kHistWords = (kHistSlots + kHistSlots / kHistFan) * kHistStride;  // 64-bit words
-constexpr uint32_t kHistTrees = 16, kHistKeyWords = 16;  // keys first (one 128 B line), then trees
+// 64 trees (round 6; 16 before): more queues than a process normally has (GPU_MAX_HW_QUEUES = 4
+// per device, plus one per CU-masked stream). A launch whose queue finds no free key takes the
+// fallback, 9x slower at 1M frames.
+constexpr uint32_t kHistTrees = 64, kHistKeyWords = 64;  // keys first (four 128 B lines), then trees
 constexpr uint64_t kHistSetBytes = 8ull * (kHistKeyWords + (uint64_t)kHistTrees * kHistWords);
 // The tree set of `device`, allocated and zeroed at first use (halo_rx_init does it ahead of any
-// capture); nullptr when that fails, or when it is first needed inside a stream capture.
+// capture); nullptr when that fails, or when it is first needed inside a stream capture. Once made,
+// a set lives as long as the process: graphs captured with its address stay valid.
 uint32_t* hist_trees(int device, hipStream_t capture_probe);
 int stream_device(hipStream_t s);  // the device a launch on `s` runs on (-1: unknown)
-void hist_trees_release(int device);  // frees the set (the caller has drained the device)
+// Frees every key of the device's set (poisoned keys stay poisoned): queues that no longer exist
+// give their trees back. The caller has drained the device, and no launch may run alongside.
+int hist_trees_reset_keys(int device);
+// Test hook behind halo_rx_debug_hist_keys: op 0 counts the claimed keys; 1 poisons every key; 2
+// occupies all keys but `arg` with ids no queue has; 3 = hist_trees_reset_keys.
+int hist_keys_debug(int device, int op, uint32_t arg);
 
 // The resident small-poll consumer of a ring attached with HALO_RING_PERSISTENT (ring_rx.hip
 // drives it, rx_parse.hip runs it): kSvcGroups workgroups that wait on this control block, in

@@ -147,7 +147,11 @@ extern "C" HALO_API int halo_rx_init(int device) {
     if (hipSetDevice(device) != hipSuccess) return HALO_E_NODEV;
     const int rc = halo::check_device();
     if (rc) return rc;
-    return halo::hist_trees(device, nullptr) ? HALO_OK : HALO_E_NOMEM;
+    // the trees are only needed by histogram-on calls: a failure here (e.g. a global-mode capture on
+    // another stream refusing the allocation) is left for such a call to report
+    (void)halo::hist_trees(device, nullptr);
+    (void)hipGetLastError();
+    return HALO_OK;
 }
 
 extern "C" HALO_API int halo_rx_device_synchronize(int device) {
@@ -159,11 +163,25 @@ extern "C" HALO_API int halo_rx_device_synchronize(int device) {
 extern "C" HALO_API int halo_rx_release(int device) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return HALO_E_NODEV;
-    halo::ParkResidents park(device);  // hipFree waits for every kernel on the device
+    halo::ParkResidents park(device);
     const int rc = halo::drain_device(device);
     if (rc) return rc;
-    halo::hist_trees_release(device);
-    return HALO_OK;
+    // the tree set itself stays (a captured graph holds its address); its keys are handed back, so
+    // the queues of streams destroyed since can no longer exhaust them
+    return halo::hist_trees_reset_keys(device);
+}
+
+extern "C" HALO_API int halo_rx_debug_hist_keys(int device, int op, uint32_t arg) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return HALO_E_NODEV;
+    if (op < 0 || op > 3) return HALO_E_INVAL;
+    if (op != 0) {  // writes: nothing of this library's may be running on the device
+        halo::ParkResidents park(device);
+        const int rc = halo::drain_device(device);
+        if (rc) return rc;
+        return halo::hist_keys_debug(device, op, arg);
+    }
+    return halo::hist_keys_debug(device, op, arg);
 }
 
 // ---- host-memory batch path ---------------------------------------------------------------
@@ -292,7 +310,7 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
     if (chunk_bytes < 65536) return HALO_E_INVAL;
     auto* c = new (std::nothrow) halo_rx_host_ctx;
     if (!c) return HALO_E_NOMEM;
-    halo::ParkResidents park(device);  // pinned allocations (and a failed create's frees)
+    halo::ParkUsed park(device);  // pinned allocations (and a failed create's frees: hipHostFree waits on every device)
     c->device = device;
     c->chunk_frames = chunk_frames;
     // zero-copy chunks with GPU-converted metadata stage nothing on the host, so they can be
@@ -330,7 +348,7 @@ extern "C" HALO_API int halo_rx_host_ctx_create(int device, uint32_t chunk_frame
 extern "C" HALO_API int halo_rx_host_ctx_destroy(halo_rx_host_ctx_t* ctx) {
     if (!ctx) return HALO_E_INVAL;
     (void)hipSetDevice(ctx->device);
-    halo::ParkResidents park(ctx->device);  // hipFree / hipHostFree wait for every kernel on the device
+    halo::ParkUsed park(ctx->device);  // hipFree waits for the device's kernels, hipHostFree for every device's
     for (auto& s : ctx->slot)
         if (s.stream) (void)hipStreamSynchronize(s.stream);
     free_ctx(ctx);
@@ -577,7 +595,7 @@ extern "C" HALO_API int halo_rx_host_ctx_set_resident(halo_rx_host_ctx_t* ctx, u
     if (!ctx) return HALO_E_INVAL;
     if (max_frames > halo::kSvcMaxFrames || max_bytes > (64ull << 20)) return HALO_E_INVAL;
     if (hipSetDevice(ctx->device) != hipSuccess) return HALO_E_NODEV;
-    halo::ParkResidents park(ctx->device);  // frees and pinned allocations below
+    halo::ParkUsed park(ctx->device);  // frees and pinned allocations below (hipHostFree: every device)
     free_resident(ctx->res);
     if (max_frames == 0) return HALO_OK;
     // default: room for max_frames full-MTU frames, so a PacketHandle batch of 1514 B frames is served

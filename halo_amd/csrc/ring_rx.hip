@@ -25,9 +25,9 @@
 // cheaper here than workgroups waiting on each other's device-scope messages: one-launch walks
 // (a linker workgroup; a decoupled look-back) and B + C in one launch were built, bit-exact, and
 // measured slower.
-// HALO_RING_MAPS=1 builds the previous resolution instead (tile maps of every entry position by
-// pointer jumping, composed into superblocks, chained by one workgroup, expanded back down, then
-// emitted): 0.19 ms against 0.033 for 1M 64 B records, kept for comparison.
+// The previous resolution (tile maps of every entry position by pointer jumping, composed into
+// superblocks, chained, expanded back down, then emitted: 0.19 ms against 0.033 for 1M 64 B
+// records) is recorded in DESIGN.md §10.4 / §14.2 and was removed from the library.
 // Every step applies ReadPacket's checks in ReadPacket's order, so the frames taken, the stop and
 // the new tail are those of repeated ReadPacket calls (tests/test_gpu_ring.py, against the oracle,
 // which tests/test_ring_oracle.py checks against the reference's own cgo/ring_buffer.h).
@@ -47,10 +47,7 @@ namespace {
 
 constexpr uint32_t kTile = 4096;                 // span dwords per tile (16 KB)
 constexpr uint32_t kThreads = 256;
-constexpr uint32_t kJumpRounds = 12;             // a walk inside a tile takes <= kTile/2 = 2^11 records
-constexpr uint32_t kLdsStop = 0x8000u;           // jump-table target: the walk stops inside the tile
-constexpr uint32_t kMapStop = 0xFFFFFFFFu;       // tile / superblock map entry: the walk stops
-constexpr uint32_t kMapLds = 8192;               // map entries (uint2) staged in LDS: 64 KB
+constexpr uint32_t kLdsStop = 0x8000u;           // nxt entry: the walk stops at this position
 constexpr uint32_t kMaxCapacity = 4 * kTile - 8; // the longest record must fit a tile's entry window
 constexpr uint64_t kMaxSpan = (16ull << 30) - (64ull << 10);  // dword offsets stay below 2^32
 constexpr uint64_t kPieceBytes = 16ull << 20;    // DMA piece (1024 tiles) whose maps start on arrival
@@ -62,25 +59,15 @@ struct Scan {
     uint32_t n_dw;          // used / 4
     uint32_t n_tiles;
     uint32_t cap;           // receive buffer capacity: len(data) of ReadPacket
-    uint32_t W;             // entry window: dwords of the longest acceptable record
-    uint32_t S;             // tiles per superblock
-    uint32_t n_sb;          // superblocks: S tiles each
-    uint32_t n_ss;          // super-superblocks: S superblocks each
     uint32_t max_frames;
     uint64_t half;          // RingBuffer.size / 2
     uint32_t half32;        // min(half, 2^32 - 1)
     uint32_t lim;           // min(half32, cap): the longest length a record may have
     uint32_t lim_dw;        // its dwords, (lim + 7) / 4
-    uint2* tile_map;        // [n_tiles][W]: (entry into the next tile | kMapStop, records taken)
-    uint2* sb_map;          // [n_sb][W]
-    uint2* ss_map;          // [n_ss][W]
-    uint2* ss_entry;        // [n_ss]: (entry | kMapStop, records before it)
-    uint2* sb_entry;        // [n_sb]: (entry | kMapStop, records before the superblock)
-    uint2* tile_entry;      // [n_tiles]: (entry | kMapStop, records before the tile)
-    uint32_t* total;        // records the walk takes before it stops (max_frames ignored)
-    struct RingCtl* ctl;    // (guess path) total and the tile the walk ends in; total aliases it
-    uint2* sum;             // (guess path) [n_tiles]: (guess | exit << 16, records | why << 12 | longest << 16)
-    uint32_t* tmp;          // (guess path) [n_tiles][kTile / 2]: a tile's records, position | length << 16
+    uint2* tile_entry;      // [n_tiles]: (records before the tile, records the tile takes), from B
+    struct RingCtl* ctl;    // total and the tile the walk ends in
+    uint2* sum;             // [n_tiles]: (guess | exit << 16, records | why << 12 | longest << 16)
+    uint32_t* tmp;          // [n_tiles][kTile / 2]: a tile's records, position | length << 16
     halo_rx_ring_scan_t* info;
     uint32_t* off_dw;       // frame i's bytes start at span dword off_dw[i]
     uint16_t* lens;
@@ -110,178 +97,6 @@ __device__ __forceinline__ uint4 span_quad(const Scan& s, uint32_t a) {
     }
     return make_uint4(a < s.n_dw ? s.span[a] : 0u, a + 1 < s.n_dw ? s.span[a + 1] : 0u,
                       a + 2 < s.n_dw ? s.span[a + 2] : 0u, a + 3 < s.n_dw ? s.span[a + 3] : 0u);
-}
-
-// Span dwords of tile t into LDS: every thread's four 16-byte loads in flight at once (the branch on
-// the span's end is uniform over the block, so the loads are not serialised behind it).
-__device__ __forceinline__ void load_tile(const Scan& s, uint32_t t, uint32_t* dw) {
-    constexpr int kPer = kTile / (4 * kThreads);
-    const uint32_t base = t * kTile;
-    uint4 v[kPer];
-    if (base + kTile <= s.n_dw) {
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) {
-            const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(s.span + base + 4 * (threadIdx.x + u * kThreads));
-            v[u] = make_uint4(x.x, x.y, x.z, x.w);
-        }
-    } else {
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) v[u] = span_quad(s, base + 4 * (threadIdx.x + u * kThreads));
-    }
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) *reinterpret_cast<uint4*>(dw + 4 * (threadIdx.x + u * kThreads)) = v[u];
-}
-
-// Stage `count` map entries src[0..count) into LDS with 8 loads in flight per thread.
-__device__ __forceinline__ void stage_maps(const uint2* src, uint32_t count, uint2* m) {
-    for (uint32_t k0 = 0; k0 < count; k0 += 8 * kThreads) {
-        uint2 r[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t k = k0 + u * kThreads + threadIdx.x;
-            if (k < count) r[u] = src[k];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t k = k0 + u * kThreads + threadIdx.x;
-            if (k < count) m[k] = r[u];
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t lane_rank(uint64_t b) {
-    return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-}
-
-// 1. Tile maps for tiles [tile0, tile0 + gridDim.x). Jump-table entry: bits 0-15 target position
-// (< kTile: inside the tile; kTile..2*kTile-1: the next tile's position + kTile; kLdsStop: the
-// walk stops), bits 16-31 records taken on the way. Only positions whose first step stays inside
-// the tile can change, and in ring data nearly every position that is not a record start fails
-// ReadPacket's checks at once (a random dword is rarely a length <= capacity), so the rounds run
-// over a compacted list of those positions and stop as soon as a round changes nothing.
-__global__ void __launch_bounds__(kThreads) ring_tile_map_kernel(const Scan s, uint32_t tile0) {
-    __shared__ __align__(16) uint32_t jt[2][kTile];
-    __shared__ uint16_t act[kTile];
-    __shared__ uint32_t n_act;
-    const uint32_t t = tile0 + blockIdx.x;
-    const uint32_t lane = threadIdx.x & 63u;
-    if (threadIdx.x == 0) n_act = 0;
-    load_tile(s, t, jt[1]);
-    __syncthreads();
-    const uint32_t base = t * kTile;
-    for (uint32_t q = threadIdx.x; q < kTile; q += kThreads) {  // uniform trip count
-        uint32_t why;
-        const uint32_t step = record_dwords(s, base + q, jt[1][q], why);
-        const uint32_t v = step ? ((q + step) | (1u << 16)) : kLdsStop;
-        const bool active = step && q + step < kTile;
-        const uint64_t b = __ballot(active);
-        uint32_t slot = 0;
-        if (lane == 0) slot = atomicAdd(&n_act, (uint32_t)__popcll(b));
-        slot = (uint32_t)__shfl((int)slot, 0, 64);
-        if (active) act[slot + lane_rank(b)] = (uint16_t)q;
-        jt[0][q] = v;
-        jt[1][q] = v;  // this thread's own raw dword is consumed: both buffers start equal
-    }
-    __syncthreads();
-    const uint32_t na = n_act;
-    uint32_t cur = 0;
-    for (uint32_t r = 0; r < kJumpRounds; ++r) {
-        int changed = 0;
-        for (uint32_t i = threadIdx.x; i < na; i += kThreads) {
-            const uint32_t q = act[i];
-            const uint32_t v = jt[cur][q];
-            const uint32_t tg = v & 0xFFFFu;
-            uint32_t nv = v;
-            if (tg < kTile) {
-                const uint32_t w = jt[cur][tg];
-                nv = (w & 0xFFFFu) | ((v & 0xFFFF0000u) + (w & 0xFFFF0000u));
-                changed = 1;
-            }
-            jt[cur ^ 1][q] = nv;
-        }
-        cur ^= 1;
-        if (!__syncthreads_or(changed)) break;
-    }
-    uint2* out = s.tile_map + (uint64_t)t * s.W;
-    for (uint32_t e = threadIdx.x; e < s.W; e += kThreads) {
-        const uint32_t v = jt[cur][e];
-        const uint32_t tg = v & 0xFFFFu;
-        out[e] = make_uint2((tg & kLdsStop) ? kMapStop : tg - kTile, v >> 16);
-    }
-}
-
-// 2. Compose groups of S consecutive maps (tiles -> superblocks -> super-superblocks): block b
-// composes src maps [b*S, b*S + S).
-__global__ void __launch_bounds__(kThreads) ring_compose_kernel(const uint2* src, uint32_t n_src, uint2* dst,
-                                                                uint32_t W, uint32_t S) {
-    __shared__ uint2 m[kMapLds];
-    const uint32_t g0 = blockIdx.x * S;
-    const uint32_t nt = min(S, n_src - g0);
-    stage_maps(src + (uint64_t)g0 * W, nt * W, m);
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < W; e += kThreads) {
-        uint32_t cur = e, taken = 0;
-        for (uint32_t k = 0; k < nt && cur != kMapStop; ++k) {
-            const uint2 v = m[k * W + cur];
-            taken += v.y;
-            cur = v.x;
-        }
-        dst[(uint64_t)blockIdx.x * W + e] = make_uint2(cur, taken);
-    }
-}
-
-// 3. Chain the top-level maps from the span's start (one workgroup; maps staged in LDS in chunks).
-__global__ void __launch_bounds__(kThreads) ring_chain_kernel(const Scan s) {
-    __shared__ uint2 m[kMapLds];
-    const uint32_t per = kMapLds / s.W;
-    uint32_t entry = 0, taken = 0;  // thread 0's walk
-    for (uint32_t c0 = 0; c0 < s.n_ss; c0 += per) {
-        const uint32_t nc = min(per, s.n_ss - c0);
-        __syncthreads();
-        stage_maps(s.ss_map + (uint64_t)c0 * s.W, nc * s.W, m);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (uint32_t k = 0; k < nc; ++k) {
-                s.ss_entry[c0 + k] = make_uint2(entry, taken);
-                if (entry != kMapStop) {
-                    const uint2 v = m[k * s.W + entry];
-                    taken += v.y;
-                    entry = v.x;
-                }
-            }
-        }
-    }
-    if (threadIdx.x == 0) {
-        const uint32_t n = min(taken, s.max_frames);
-        *s.total = taken;
-        halo_rx_ring_scan_t info;
-        info.n_frames = n;
-        info.stop = n < taken ? HALO_RING_STOP_MAX : HALO_RING_STOP_EMPTY;  // a tile refines EMPTY
-        info.end_bytes = 0;
-        info.max_len = 0;
-        info.pad = 0;
-        *s.info = info;
-    }
-}
-
-// 4. Entries one level down: thread p follows the maps of parent p's (up to S) children from the
-// parent's entry, writing each child's entry and the records before it.
-__global__ void __launch_bounds__(kThreads) ring_expand_kernel(const uint2* parent_entry, uint32_t n_parent,
-                                                               const uint2* child_map, uint32_t n_child,
-                                                               uint2* child_entry, uint32_t W, uint32_t S) {
-    const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
-    if (p >= n_parent) return;
-    const uint2 e = parent_entry[p];
-    uint32_t entry = e.x, base = e.y;
-    const uint32_t c1 = min((p + 1) * S, n_child);
-    for (uint32_t k = p * S; k < c1; ++k) {
-        child_entry[k] = make_uint2(entry, base);
-        if (entry != kMapStop) {
-            const uint2 v = child_map[(uint64_t)k * W + entry];
-            base += v.y;
-            entry = v.x;
-        }
-    }
 }
 
 // Tile tables. nxt[q]: the position of the record after the one whose length
@@ -492,36 +307,7 @@ __device__ __forceinline__ TileWalk tile_walk(TileTab& tb, uint32_t n_act, uint3
 
 __device__ __forceinline__ uint32_t len_dwords(uint32_t len) { return (len >> 2) + 1u + ((len & 3u) != 0u); }
 
-// (maps path) 5. Emit: one workgroup per tile, from its entry (ring_expand_kernel): the walk
-// through the tile and the records' (offset, length) pairs.
 constexpr uint32_t kTileWaves = kThreads / 64;
-__global__ void __launch_bounds__(kThreads) ring_emit_kernel(const Scan s) {
-    __shared__ TileTab tb;
-    const uint32_t t = blockIdx.x, tid = threadIdx.x;
-    const uint32_t n = s.info->n_frames;
-    const uint2 te = s.tile_entry[t];
-    const uint32_t entry = te.x, base = te.y;
-    if (entry == kMapStop || base > n) return;  // uniform
-    const uint32_t n_act = tile_tabulate<kTileWaves>(s, t, tb, entry);
-    const TileWalk wk = tile_walk<kTileWaves>(tb, n_act, 0, entry, min(n - base, kListMax));
-    const uint32_t c = wk.c, q = wk.q, tbase = t * kTile;
-    if (tid == 0) {
-        const uint32_t v = q < kTile ? tb.nxt[q] : 0u;
-        if (base + c == n && c) s.info->end_bytes = 4ull * (tbase + q);
-        // where the walk ends inside this tile: say why, unless max_frames cut it (MAX, set)
-        if (q < kTile && n == *s.total && (v & kLdsStop)) s.info->stop = stop_why(s, tbase + q);
-    }
-    uint32_t max_len = 0;
-    for (uint32_t j = tid; j < c; j += kThreads) {
-        const uint32_t e = tb.list[j], len = nxt_len(e, tb.nxt[e]);
-        s.off_dw[base + j] = tbase + e + 1;
-        s.lens[base + j] = (uint16_t)len;
-        max_len = max(max_len, len);
-    }
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) max_len = max(max_len, (uint32_t)__shfl_xor((int)max_len, m, 64));
-    if ((tid & 63u) == 0 && max_len) atomicMax(&s.info->max_len, max_len);
-}
 
 // ---- the record walk by guess and verify (the default) ------------------------------------------
 // A. Every tile guesses its entry — the first position that passes ReadPacket's checks (tile 0:
@@ -556,24 +342,12 @@ __device__ __forceinline__ uint32_t keep_records(const Scan& s, uint32_t t, cons
     return mx;  // the wave's
 }
 
-#ifdef HALO_GUESS_TRACE  // tools only: phase timestamps (100 MHz) of every tile into the frame offsets
-#define GTRACE(k) do { if (threadIdx.x == 0) reinterpret_cast<uint64_t*>(s.off_dw)[8ull * t + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define GTRACE(k) ((void)0)
-#endif
-
 // One tile of A: its tables, its guess, its walk, its records and summary.
 template <int W>
 __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& tb, uint32_t* s_mx,
                                            const uint4 (&v)[kTabQ<W>]) {
     const uint32_t tid = threadIdx.x;
-#ifdef HALO_GUESS_TRACE
-    if (tid == 0) __builtin_amdgcn_s_waitcnt(0);  // (the tile's bytes are in)
-    { const uint32_t sink = v[0].x; if (sink == 0xDEADBEEFu && tid == 1) reinterpret_cast<uint32_t*>(s.off_dw)[0] = sink; }
-#endif
-    GTRACE(1);
     const uint32_t n_act = tile_tabulate<W>(s, t, tb, 0, v);
-    GTRACE(2);
     // The guess: the first listed candidate whose chain of links does not stop inside the tile. The
     // dword before a record is often a decoy — a frame's last bytes and zero padding make a small
     // "length" (1.3 % of IMIX tiles, tools: a 570 B frame's last dword) — whose link lands nowhere;
@@ -590,11 +364,9 @@ __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& t
             k = F + 1;
         }
     }
-    GTRACE(3);
     const uint32_t g = t == 0 ? 0u : n_act ? tb.list[i0] : kNone;
     TileWalk wk{0, kNone};
     if (g != kNone) wk = tile_walk<W>(tb, n_act, i0, g, kListMax, F0);  // uniform (tile 0: i0 = 0)
-    GTRACE(4);
     const uint32_t mx = keep_records(s, t, tb, i0, wk.c);
     if ((tid & 63u) == 0) s_mx[tid >> 6] = mx;
     __syncthreads();
@@ -604,7 +376,6 @@ __device__ __forceinline__ void guess_tile(const Scan& s, uint32_t t, TileTab& t
         const uint32_t why = wk.q < kTile ? stop_why(s, t * kTile + wk.q) : 0u;
         s.sum[t] = make_uint2(g | (wk.q << 16), wk.c | (why << 12) | (m << 16));
     }
-    GTRACE(5);
 }
 
 #ifndef HALO_RING_GUESS_WAVES
@@ -619,9 +390,6 @@ __global__ void __launch_bounds__(kGuessWaves * 64) ring_guess_kernel(const Scan
     // one's bytes while working on the current one ran slower, 24.9 against 19.0 us for 1M 64 B
     // records, profiles/r05/r5zc: the tile's work, not its load, is what a CU waits on)
     uint4 v[kTabQ<kGuessWaves>];
-#ifdef HALO_GUESS_TRACE
-    { const uint32_t t = blockIdx.x; GTRACE(0); }
-#endif
     tile_load<kGuessWaves>(s, blockIdx.x, v);
     guess_tile<kGuessWaves>(s, blockIdx.x, tb, s_mx, v);
 }
@@ -841,42 +609,21 @@ __global__ void __launch_bounds__(kThreads) ring_copy_kernel(const Scan s) {
     }
 }
 
-#ifndef HALO_RING_MAPS
-#define HALO_RING_MAPS 0  // 1: the tile-map walk (pointer jumping, compose, chain, expand, emit)
-#endif
-
 struct Geom {
-    uint32_t n_dw, n_tiles, W, S, n_sb, n_ss;
-    uint64_t tile_map_off, sb_map_off, ss_map_off, ss_entry_off, sb_entry_off, tile_entry_off, total_off, bytes;
-    uint64_t sum_off, tmp_off;
+    uint32_t n_dw, n_tiles;
+    uint64_t sum_off, tmp_off, tile_entry_off, total_off, bytes;
 };
 
 Geom geometry(uint64_t used, uint32_t cap) {
     Geom g{};
     g.n_dw = (uint32_t)(used >> 2);
     g.n_tiles = std::max<uint32_t>(1, (g.n_dw + kTile - 1) / kTile);
-    g.W = (cap + 7) / 4;  // ceil((4 + cap) / 4)
-    g.S = std::max<uint32_t>(1, kMapLds / g.W);
-    g.n_sb = (g.n_tiles + g.S - 1) / g.S;
-    g.n_ss = (g.n_sb + g.S - 1) / g.S;
+    (void)cap;
     uint64_t o = 0;
-    if (HALO_RING_MAPS) {
-        g.tile_map_off = o;
-        o += (uint64_t)g.n_tiles * g.W * sizeof(uint2);
-        g.sb_map_off = o;
-        o += (uint64_t)g.n_sb * g.W * sizeof(uint2);
-        g.ss_map_off = o;
-        o += (uint64_t)g.n_ss * g.W * sizeof(uint2);
-    } else {
-        g.sum_off = o;
-        o += (uint64_t)g.n_tiles * sizeof(uint2);
-        g.tmp_off = o;
-        o += (uint64_t)g.n_tiles * kListMax * sizeof(uint32_t);
-    }
-    g.ss_entry_off = o;
-    o += (uint64_t)g.n_ss * sizeof(uint2);
-    g.sb_entry_off = o;
-    o += (uint64_t)g.n_sb * sizeof(uint2);
+    g.sum_off = o;
+    o += (uint64_t)g.n_tiles * sizeof(uint2);
+    g.tmp_off = o;
+    o += (uint64_t)g.n_tiles * kListMax * sizeof(uint32_t);
     g.tile_entry_off = o;
     o += (uint64_t)(g.n_tiles + kTileWaves - 1) / kTileWaves * kTileWaves * sizeof(uint2);  // C reads whole workgroups
     g.total_off = o;
@@ -892,23 +639,13 @@ Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_
     s.n_dw = g.n_dw;
     s.n_tiles = g.n_tiles;
     s.cap = cap;
-    s.W = g.W;
-    s.S = g.S;
-    s.n_sb = g.n_sb;
-    s.n_ss = g.n_ss;
     s.max_frames = max_frames;  // 0: no frame may be taken
     s.half = ring_size / 2;
     s.half32 = (uint32_t)std::min<uint64_t>(s.half, 0xFFFFFFFFull);
     s.lim = std::min(s.half32, cap);
     s.lim_dw = (uint32_t)(((uint64_t)s.lim + 7) / 4);
-    s.tile_map = reinterpret_cast<uint2*>(ws + g.tile_map_off);
-    s.sb_map = reinterpret_cast<uint2*>(ws + g.sb_map_off);
-    s.ss_map = reinterpret_cast<uint2*>(ws + g.ss_map_off);
-    s.ss_entry = reinterpret_cast<uint2*>(ws + g.ss_entry_off);
-    s.sb_entry = reinterpret_cast<uint2*>(ws + g.sb_entry_off);
     s.tile_entry = reinterpret_cast<uint2*>(ws + g.tile_entry_off);
     s.ctl = reinterpret_cast<RingCtl*>(ws + g.total_off);
-    s.total = &s.ctl->total;
     s.sum = reinterpret_cast<uint2*>(ws + g.sum_off);
     s.tmp = reinterpret_cast<uint32_t*>(ws + g.tmp_off);
     s.info = d_info;
@@ -917,28 +654,11 @@ Scan make_scan(const Geom& g, const uint8_t* d_span, uint64_t ring_size, uint32_
     return s;
 }
 
-// The record walk of a span: tile maps, composed and chained (HALO_RING_MAPS), or the guess /
-// link / copy kernels.
+// The record walk of a span: the guess / link / copy kernels.
 int launch_walk(const Scan& s, hipStream_t st) {
-    const dim3 blk(kThreads);
-    if (!HALO_RING_MAPS) {
-        hipLaunchKernelGGL(ring_guess_kernel, dim3(s.n_tiles), dim3(kGuessWaves * 64), 0, st, s);
-#ifdef HALO_GUESS_TRACE
-        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;  // A alone: its trace is in d_off
-#endif
-        hipLaunchKernelGGL(ring_link_kernel, dim3(1), dim3(kLinkThreads), 0, st, s);
-        hipLaunchKernelGGL(ring_copy_kernel, dim3((s.n_tiles + kTileWaves - 1) / kTileWaves), blk, 0, st, s);
-        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
-    }
-    hipLaunchKernelGGL(ring_tile_map_kernel, dim3(s.n_tiles), blk, 0, st, s, 0u);
-    hipLaunchKernelGGL(ring_compose_kernel, dim3(s.n_sb), blk, 0, st, s.tile_map, s.n_tiles, s.sb_map, s.W, s.S);
-    hipLaunchKernelGGL(ring_compose_kernel, dim3(s.n_ss), blk, 0, st, s.sb_map, s.n_sb, s.ss_map, s.W, s.S);
-    hipLaunchKernelGGL(ring_chain_kernel, dim3(1), blk, 0, st, s);
-    hipLaunchKernelGGL(ring_expand_kernel, dim3((s.n_ss + kThreads - 1) / kThreads), blk, 0, st, s.ss_entry, s.n_ss,
-                       s.sb_map, s.n_sb, s.sb_entry, s.W, s.S);
-    hipLaunchKernelGGL(ring_expand_kernel, dim3((s.n_sb + kThreads - 1) / kThreads), blk, 0, st, s.sb_entry, s.n_sb,
-                       s.tile_map, s.n_tiles, s.tile_entry, s.W, s.S);
-    hipLaunchKernelGGL(ring_emit_kernel, dim3(s.n_tiles), dim3(kThreads), 0, st, s);
+    hipLaunchKernelGGL(ring_guess_kernel, dim3(s.n_tiles), dim3(kGuessWaves * 64), 0, st, s);
+    hipLaunchKernelGGL(ring_link_kernel, dim3(1), dim3(kLinkThreads), 0, st, s);
+    hipLaunchKernelGGL(ring_copy_kernel, dim3((s.n_tiles + kTileWaves - 1) / kTileWaves), dim3(kThreads), 0, st, s);
     return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
 }
 
@@ -990,7 +710,7 @@ namespace {
 // Returns false when the ring memory could not be unregistered (the caller must not free it then:
 // the pages stay mapped for the device).
 bool free_ring(halo_rx_ring* r) {
-    halo::ParkResidents park(r->device);  // hipFree / hipHostFree wait for every kernel on the device
+    halo::ParkUsed park(r->device);  // hipFree waits for the device's kernels, hipHostFree for every device's
     halo::resident_destroy(r->svc);      // stops the consumer and waits for its kernel to end
     for (hipEvent_t e : r->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1032,7 +752,7 @@ void* device_view(const void* p, uint64_t bytes) {
 int alloc_small(halo_rx_ring* r, uint64_t bytes) {
     const uint32_t frames = (uint32_t)std::min<uint64_t>(bytes / 8, r->max_frames);
     if (frames > r->small_frames) {
-        halo::ParkResidents park(r->device);
+        halo::ParkUsed park(r->device);  // hipHostFree waits for kernels on every device
         if (r->h_soff) (void)hipHostFree(r->h_soff);
         if (r->h_slen) (void)hipHostFree(r->h_slen);
         if (r->h_sres) (void)hipHostFree(r->h_sres);
@@ -1044,12 +764,19 @@ int alloc_small(halo_rx_ring* r, uint64_t bytes) {
         r->d_soff = nullptr;
         r->d_slen = nullptr;
         if (r->svc) halo::resident_set_arrays(r->svc, r->d_data, nullptr, nullptr);  // freed above
+        // on failure the small path is switched off (small = 0): every later poll takes the pipelined
+        // path instead of walking with no arrays and returning nothing
+        r->small = 0;
         if (hipHostMalloc((void**)&r->h_soff, 4ull * frames, hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc((void**)&r->h_slen, 2ull * frames, hipHostMallocDefault) != hipSuccess)
             return HALO_E_NOMEM;
         r->d_soff = static_cast<uint32_t*>(device_view(r->h_soff, 4ull * frames));
         r->d_slen = static_cast<uint16_t*>(device_view(r->h_slen, 2ull * frames));
-        if (!r->d_soff || !r->d_slen) return HALO_E_NOMEM;
+        if (!r->d_soff || !r->d_slen) {
+            r->d_soff = nullptr;
+            r->d_slen = nullptr;
+            return HALO_E_NOMEM;
+        }
         r->small_frames = frames;
         if (r->svc) halo::resident_set_arrays(r->svc, r->d_data, r->d_soff, r->d_slen);
     }
@@ -1182,7 +909,7 @@ extern "C" HALO_API int halo_rx_ring_attach(int device, void* ring_mem, int64_t 
     if (max_bytes < 8) return HALO_E_INVAL;
     if (max_frames == 0 || max_frames > max_bytes / 8) max_frames = (uint32_t)std::min<uint64_t>(max_bytes / 8, 0xFFFFFFFFull);
     if ((rc = halo_rx_init(device))) return rc;
-    halo::ParkResidents park(device);  // allocations, registration (and a failed attach's frees)
+    halo::ParkUsed park(device);  // allocations, registration (and a failed attach's frees: hipHostFree waits on every device)
     auto* r = new (std::nothrow) halo_rx_ring;
     if (!r) return HALO_E_NOMEM;
     r->device = device;

@@ -522,9 +522,16 @@ __device__ __forceinline__ void process_frame(const RxParams& p, uint64_t i, boo
 #ifndef HALO_HIST_HDR
 #define HALO_HIST_HDR 0  // measurement knob: 1 = every block re-reads its dispatch packet's barrier bit
 #endif
-// key0: the word at the queue's first probe slot as the block read it when it started (Hist::key).
-// A key never changes once set, so a stale copy can only read 0, and then the CAS (performed at
-// memory) returns the real key.
+// key0: the word at the queue's first probe slot as block thread 0 read it when the block started
+// (Hist::key). A key never changes once set, so a stale copy can only read 0, and then the CAS
+// (performed at memory) returns the real key.
+// Called by the 64 lanes of wave 0 (every kernel that counts has blocks of whole waves, >= 64
+// threads). Lane j reads probe slot k0 + j (kHistTrees == 64: every slot in one round trip); the
+// first slot in probe order holding this queue's key is the tree; otherwise the slots read as free
+// are claimed in probe order by lane 0, one CAS each, until one is this queue's. A queue that finds
+// every key held by others (or poisoned) returns nullptr after that one round trip (16 serial probes
+// before round 6).
+static_assert(kHistTrees == 64, "one probe slot per lane of a wave");
 __device__ __forceinline__ unsigned long long* launch_tree(uint32_t* set_u32, unsigned long long key0) {
 #if HALO_HIST_HDR
     // 100 us per 1M-frame launch: the packet lives in host memory (bench_hist, profiles/r05)
@@ -533,18 +540,26 @@ __device__ __forceinline__ unsigned long long* launch_tree(uint32_t* set_u32, un
 #endif
     unsigned long long* set = reinterpret_cast<unsigned long long*>(set_u32);
     const unsigned long long q = launch_queue();
-    const uint32_t k0 = tree_slot0(q);
-    if (key0 == q) return set + kHistKeyWords + (uint64_t)k0 * kHistWords;
-    for (uint32_t j = 0; j < kHistTrees; ++j) {
-        const uint32_t k = (k0 + j) & (kHistTrees - 1u);
-        unsigned long long key = j ? set[k] : key0;
-        if (key == 0) {  // claim it (device scope: a native compare-and-swap, no retry loop)
-            unsigned long long expect = 0;
-            __hip_atomic_compare_exchange_strong(set + k, &expect, q, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+    const uint32_t k0 = tree_slot0(q), lane = threadIdx.x & 63u;
+    const unsigned long long k0key =
+        ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(key0 >> 32), 0, 64) << 32) |
+        (uint32_t)__shfl((int)(uint32_t)key0, 0, 64);
+    if (k0key == q) return set + kHistKeyWords + (uint64_t)k0 * kHistWords;  // uniform
+    const unsigned long long key = set[(k0 + lane) & (kHistTrees - 1u)];
+    const uint64_t mine = __ballot(key == q);
+    if (mine) return set + kHistKeyWords + (uint64_t)((k0 + (uint32_t)__builtin_ctzll(mine)) & (kHistTrees - 1u)) * kHistWords;
+    uint64_t free_slots = __ballot(key == 0);
+    while (free_slots) {  // uniform
+        const uint32_t k = (k0 + (uint32_t)__builtin_ctzll(free_slots)) & (kHistTrees - 1u);
+        unsigned long long got = 0;
+        if (lane == 0) {  // claim it (device scope: a native compare-and-swap, no retry loop)
+            __hip_atomic_compare_exchange_strong(set + k, &got, q, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
-            key = expect;  // 0: claimed now; q: claimed by another block of this queue
         }
-        if (key == 0 || key == q) return set + kHistKeyWords + (uint64_t)k * kHistWords;
+        got = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(got >> 32), 0, 64) << 32) |
+              (uint32_t)__shfl((int)(uint32_t)got, 0, 64);
+        if (got == 0 || got == q) return set + kHistKeyWords + (uint64_t)k * kHistWords;  // claimed now / by a sibling block
+        free_slots &= free_slots - 1;  // another queue's key (our read was stale): the next free slot
     }
     return nullptr;  // every key taken by another queue, or poisoned (hist_trees: no barrier bits)
 }
@@ -557,9 +572,10 @@ __device__ __forceinline__ void flush_hist(const RxParams& p, Hist& hist) {
     for (int m = 1; m < 64; m <<= 1) ok += __shfl_xor(ok, m, 64);
     if ((threadIdx.x & 63u) == 0 && ok) atomicAdd(&hist.s[HALO_RX_OK], ok);
     __syncthreads();
+    if (t >= 64) return;
+    unsigned long long* tree = launch_tree(p.hist, hist.key);  // wave 0: one probe round trip for the block
     if (t >= HALO_RX_STATUS_COUNT) return;
     const uint32_t s = blockIdx.x & (kHistSlots - 1u), g = gridDim.x;
-    unsigned long long* tree = launch_tree(p.hist, hist.key);  // wave 0 only: one request for its lanes
     if (!tree) {  // no tree this launch can own alone: straight into the caller's counters
         if (hist.s[t]) atomicAdd(&p.hist_out[t], hist.s[t]);
         return;
@@ -1563,7 +1579,8 @@ int stream_device(hipStream_t s) {
 
 namespace {
 std::mutex g_trees_mu;
-uint32_t* g_trees[64];
+uint32_t* g_trees[64];      // a device's set: made once, never freed (graphs hold its address)
+bool g_no_barriers[64];     // the probe found a dispatch without the barrier bit: keys stay poisoned
 
 // Writes its own AQL packet header (the barrier bit is bit 8) to *out.
 __global__ void dispatch_header_probe(unsigned long long* out) {
@@ -1613,15 +1630,54 @@ uint32_t* hist_trees(int device, hipStream_t capture_probe) {
         m = nullptr;
     }
     if (cur != device) (void)hipSetDevice(cur);
+    g_no_barriers[device] = ok && !barriers;
     p = static_cast<uint32_t*>(m);
     return p;
 }
 
-void hist_trees_release(int device) {
-    if (device < 0 || device >= 64) return;
+namespace {
+// Writes the key words of `device`'s set (g_trees_mu held): all 0 (free), all ~0 (poisoned), or
+// ids no queue has for all but the first `free_keys` slots.
+int write_keys(int device, int fill, uint32_t free_keys) {
+    uint32_t* set = g_trees[device];
+    if (!set) return HALO_E_NOMEM;
+    unsigned long long k[kHistKeyWords];
+    for (uint32_t j = 0; j < kHistKeyWords; ++j)
+        k[j] = fill == 0 ? 0ull : fill == 1 ? ~0ull : (j < free_keys ? 0ull : 0x40ull * (j + 1));  // not a queue address
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return HALO_E_NODEV;
+    if (cur != device && hipSetDevice(device) != hipSuccess) return HALO_E_NODEV;
+    const bool ok = hipMemcpy(set, k, sizeof k, hipMemcpyHostToDevice) == hipSuccess;
+    if (cur != device) (void)hipSetDevice(cur);
+    return ok ? HALO_OK : HALO_E_HIP;
+}
+}  // namespace
+
+int hist_trees_reset_keys(int device) {
+    if (device < 0 || device >= 64) return HALO_E_NODEV;
     std::lock_guard<std::mutex> g(g_trees_mu);
-    if (g_trees[device]) (void)hipFree(g_trees[device]);
-    g_trees[device] = nullptr;
+    if (!g_trees[device]) return HALO_OK;
+    return write_keys(device, g_no_barriers[device] ? 1 : 0, 0);
+}
+
+int hist_keys_debug(int device, int op, uint32_t arg) {
+    if (device < 0 || device >= 64) return HALO_E_NODEV;
+    if (op == 3) return hist_trees_reset_keys(device);
+    if (!hist_trees(device, nullptr)) return HALO_E_NOMEM;
+    std::lock_guard<std::mutex> g(g_trees_mu);
+    if (op == 1) return write_keys(device, 1, 0);
+    if (op == 2) return arg > kHistTrees ? HALO_E_INVAL : write_keys(device, 2, arg);
+    if (op != 0) return HALO_E_INVAL;
+    unsigned long long k[kHistKeyWords];
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return HALO_E_NODEV;
+    if (cur != device && hipSetDevice(device) != hipSuccess) return HALO_E_NODEV;
+    const bool ok = hipMemcpy(k, g_trees[device], sizeof k, hipMemcpyDeviceToHost) == hipSuccess;
+    if (cur != device) (void)hipSetDevice(cur);
+    if (!ok) return HALO_E_HIP;
+    int claimed = 0;
+    for (uint32_t j = 0; j < kHistTrees; ++j) claimed += k[j] != 0 && k[j] != ~0ull;
+    return claimed;
 }
 }  // namespace halo
 

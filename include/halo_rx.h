@@ -199,18 +199,32 @@ typedef void* halo_stream_t; /* a hipStream_t (NULL = the device's null stream) 
 /* ---- device / library -------------------------------------------------------------- */
 HALO_API const char* halo_rx_version(void);
 /* Selects `device` for the calling thread, checks that it is a gfx950 part and makes the device's
- * status-histogram trees (2.2 MB, zeroed): call it before capturing histogram-on parses in a
- * hipGraph, since a capture cannot allocate. Idempotent. */
+ * status-histogram trees (8.7 MB, zeroed, kept for the life of the process): call it before
+ * capturing histogram-on parses in a hipGraph, since a capture cannot allocate (such a call
+ * returns HALO_E_NOMEM when the trees were never made). A failure to make the trees does not fail
+ * this call: the next histogram-on call outside a capture tries again. Idempotent. */
 HALO_API int halo_rx_init(int device);
 /* Waits for all work on `device` the way hipDeviceSynchronize does, after stopping this library's
  * resident consumers on it (rings attached with HALO_RING_PERSISTENT, host contexts with
  * halo_rx_host_ctx_set_resident). A caller's own hipDeviceSynchronize / torch.cuda.synchronize()
  * waits for those kernels too, and they end only 20 ms after their last request (never, while
- * another thread keeps them busy); this call does not. The consumers restart on their next request. */
+ * another thread keeps them busy); this call does not. The consumers restart on their next request.
+ * Like hipDeviceSynchronize on ROCm 7, it does NOT wait for the per-thread stream
+ * (hipStreamPerThread) of a host thread that has already exited: synchronise that stream on its
+ * own thread before the thread ends. */
 HALO_API int halo_rx_device_synchronize(int device);
-/* Frees the device-wide state halo_rx_init made (after halo_rx_device_synchronize). Rings, contexts
- * and route tables stay valid; the next histogram-on call makes the trees again. */
+/* Drains `device` (as halo_rx_device_synchronize) and hands back every status-histogram tree key,
+ * so that the HSA queues of streams destroyed since no longer hold trees (64 keys per device; a
+ * queue that finds none left counts straight into the caller's counters, exact but ~9x slower at
+ * 1M frames). The trees themselves stay: graphs captured with histogram-on parses remain valid and
+ * count exactly when replayed after this call. Rings, contexts and route tables stay valid. Must
+ * not run while another thread launches parses on `device`. */
 HALO_API int halo_rx_release(int device);
+/* TESTING ONLY — the histogram tree keys of `device`. op 0: returns how many keys HSA queues have
+ * claimed (>= 0); op 1: poisons every key (every histogram-on launch takes the fallback); op 2:
+ * occupies all keys but `arg` (<= 64) with ids no queue has; op 3: frees every key as
+ * halo_rx_release does. Ops 1-3 drain the device first and must not run alongside parses. */
+HALO_API int halo_rx_debug_hist_keys(int device, int op, uint32_t arg);
 HALO_API const char* halo_rx_strerror(int code);
 HALO_API const char* halo_rx_status_name(int status);
 

@@ -160,11 +160,14 @@ def engine_lo(packet: bytes, netif: NetIf, flags: int = 1) -> int:
 
 
 def rx_batch(data: np.ndarray, lens: np.ndarray, netif: NetIf, flags: int = 1, offsets_dw=None, stride: int = 0,
-             length: int = 0, threads: int = 1, reps: int = 1):
+             length: int = 0, threads: int = 1, reps: int = 1, out=None):
     """Returns (records, status histogram). `reps`: every thread parses its shard that many times
-    (timing: one thread start per measurement)."""
+    (timing: one thread start per measurement). `out`: a RESULT_DTYPE array of n records to reuse
+    (timing: no fresh allocation per call)."""
     n = int(lens.shape[0]) if lens is not None else int(data.shape[0] // stride)
-    out = np.zeros(n, dtype=RESULT_DTYPE)
+    if out is None:
+        out = np.zeros(n, dtype=RESULT_DTYPE)
+    assert out.dtype == RESULT_DTYPE and out.shape[0] >= n and out.flags.c_contiguous
     hist = np.zeros(STATUS_COUNT, dtype=np.uint32)
     data = np.ascontiguousarray(data, dtype=np.uint8)
     lens_c = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)

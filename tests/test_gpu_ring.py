@@ -149,10 +149,11 @@ def test_poll_stops_like_readpacket(dev, golden, oracle_lib, small_poll):
         cons.close()
 
 
-def _records_span(rng, lens, corrupt_at=None, corrupt_val=0, garbage=0.0):
+def _records_span(rng, lens, corrupt_at=None, corrupt_val=0, garbage=0.0, garbage_bytes=None):
     """A ring span in stream order holding records of `lens` (+ random bytes). `garbage`: the
     fraction of payload dwords replaced by values that pass ReadPacket's length checks (1..1514),
-    so walks started off the record chain look valid for a while (record decoys)."""
+    so walks started off the record chain look valid for a while (record decoys); only within the
+    byte range `garbage_bytes` = (lo, hi) when given."""
     lens = np.asarray(lens, np.int64)
     sizes = (4 + lens + 3) & ~3
     starts = np.zeros(len(lens), np.int64)
@@ -161,8 +162,10 @@ def _records_span(rng, lens, corrupt_at=None, corrupt_val=0, garbage=0.0):
     span = rng.integers(0, 256, used + 16, dtype=np.uint8)
     words = span[:used].view(np.uint32)
     if garbage:
-        decoy = rng.random(words.size) < garbage
-        words[decoy] = rng.integers(1, 1515, int(decoy.sum()), dtype=np.uint32)
+        lo, hi = (0, used) if garbage_bytes is None else garbage_bytes
+        win = words[lo // 4:hi // 4]
+        decoy = rng.random(win.size) < garbage
+        win[decoy] = rng.integers(1, 1515, int(decoy.sum()), dtype=np.uint32)
     words[starts // 4] = lens.astype(np.uint32)
     if corrupt_at is not None:
         words[starts[corrupt_at] // 4] = corrupt_val
@@ -229,6 +232,51 @@ def test_scan_device_matches_walk(dev, oracle_lib, name, gen, cap, max_frames, c
         assert (int(inf["stop"]), int(inf["end_bytes"]), int(inf["max_len"])) == (w_stop, w_end, w_ml), (name, trim)
         assert np.array_equal(d_off[:n].cpu().numpy().view(np.uint32), w_off), name
         assert np.array_equal(d_len[:n].cpu().numpy().view(np.uint16), w_len), name
+
+
+LINK_CHUNK_BYTES = 512 * 16 * 16384  # ring_link_kernel: kLinkThreads x kLinkPer tiles of 16 KB = 128 MiB
+
+
+@pytest.mark.parametrize("decoys,max_frames", [(False, 0), (True, 0), (True, 2_000_000)],
+                         ids=["plain", "decoys_after_boundary", "decoys_max_frames"])
+def test_scan_device_beyond_one_link_chunk(dev, oracle_lib, decoys, max_frames):
+    """the link kernel passes a whole 8192-tile chunk (128 MiB) with no special tile on its
+    summaries alone and enters the next chunk from the last thread's exit — only on spans > 128 MiB.
+    2.4M x 64 B records (163 MB); with decoys, every payload dword of the first 64 KB after the chunk
+    boundary is a plausible length, so the guesses of the tiles there are wrong and the second chunk
+    starts with a second walk from the entry the first chunk handed over. Against the oracle's walk."""
+    import torch
+
+    from halo_amd import _lib
+
+    O = oracle_lib
+    rng = np.random.default_rng(0x4C494E4B + decoys)
+    lens = [64] * 2_400_000
+    span, used = _records_span(rng, lens, garbage=1.0 if decoys else 0.0,
+                               garbage_bytes=(LINK_CHUNK_BYTES, LINK_CHUNK_BYTES + (64 << 10)))
+    assert used > LINK_CHUNK_BYTES + (1 << 20)
+    ring_size = 1 << 28
+    mf = max_frames or 0xFFFFFFFF
+    w_off, w_len, w_stop, w_end, w_ml = O.ring_scan(span, used, ring_size, 1514, mf)
+    assert len(w_off) == (max_frames or len(lens))
+    d_span = torch.from_numpy(span).to(dev)
+    n_max = used // 8
+    d_off = torch.zeros(n_max, dtype=torch.int32, device=dev)
+    d_len = torch.zeros(n_max, dtype=torch.int16, device=dev)
+    info = torch.zeros(24, dtype=torch.uint8, device=dev)
+    ws_bytes = _lib.lib.halo_rx_ring_scan_workspace(used, 1514)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    rc = _lib.lib.halo_rx_ring_scan_device(d_span.data_ptr(), used, ring_size, 1514, max_frames, d_off.data_ptr(),
+                                           d_len.data_ptr(), info.data_ptr(), ws.data_ptr(), ws_bytes,
+                                           torch.cuda.current_stream().cuda_stream)
+    _lib.check("halo_rx_ring_scan_device", rc)
+    torch.cuda.synchronize()
+    inf = info.cpu().numpy().view(_lib.RING_SCAN_DTYPE)[0]
+    n = int(inf["n_frames"])
+    assert n == len(w_off)
+    assert (int(inf["stop"]), int(inf["end_bytes"]), int(inf["max_len"])) == (w_stop, w_end, w_ml)
+    assert np.array_equal(d_off[:n].cpu().numpy().view(np.uint32), w_off)
+    assert np.array_equal(d_len[:n].cpu().numpy().view(np.uint16), w_len)
 
 
 @pytest.mark.parametrize("persistent", [False, True], ids=["launch", "persistent"])

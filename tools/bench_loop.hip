@@ -223,26 +223,43 @@ __global__ void __launch_bounds__(BLOCK) read_tile_kernel(const uint4* __restric
     if (acc == 0x9E3779B9u) sink[blockIdx.x & 4095u] = acc;  // practically never: keeps the loads live
 }
 
-// Size-matched speed-of-light probe: block t reads 16 KB tile t of `src` (four 16-byte loads per
-// thread in flight) and writes its share of `dst` with coalesced 16-byte stores — the rx kernel's
-// bytes (frames + metadata in, records out) with perfect access patterns and no work.
+// Size-matched speed-of-light probe: block t reads tile t of `src` (U 16-byte loads per thread in
+// flight: a 4U KB tile) and writes its share of `dst` with coalesced 16-byte stores — the rx kernel's
+// bytes (frames + metadata in, records out) with perfect access patterns and no work. A family of
+// shapes (tile size, non-temporal loads and stores) of which bench.py takes the fastest, so that the
+// probe is a ceiling at every size (the 16 KB plain shape alone ran slower than the
+// rx kernel at 16M frames).
+template <int U, bool NT>
 __global__ void __launch_bounds__(256) stream_rw_kernel(const uint4* __restrict__ src, uint64_t r16,
                                                         uint4* __restrict__ dst, uint64_t w16, uint64_t wt16,
                                                         uint32_t* __restrict__ sink) {
-    constexpr uint32_t kTile16 = 1024;  // 16 KB
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr uint32_t kTile16 = 256 * U;
     const uint64_t t = blockIdx.x;
     uint32_t acc = 0;
-    uint4 v[4];
+    uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
         const uint64_t k = t * kTile16 + u * 256 + threadIdx.x;
-        v[u] = k < r16 ? src[k] : make_uint4(0, 0, 0, 0);
+        if (NT && k < r16) {
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + k);
+            v[u] = make_uint4(x.x, x.y, x.z, x.w);
+        } else {
+            v[u] = k < r16 ? src[k] : make_uint4(0, 0, 0, 0);
+        }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     const uint64_t w0 = t * wt16, w1 = w0 + wt16 < w16 ? w0 + wt16 : w16;
-    for (uint64_t k = w0 + threadIdx.x; k < w1; k += 256) dst[k] = make_uint4((uint32_t)k, (uint32_t)t, 0, 0);
-    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;  // practically never: keeps the loads live
+    for (uint64_t k = w0 + threadIdx.x; k < w1; k += 256) {
+        if (NT) {
+            const u32x4 x = {(uint32_t)k, (uint32_t)t, 0u, 0u};
+            __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(dst) + k);
+        } else {
+            dst[k] = make_uint4((uint32_t)k, (uint32_t)t, 0, 0);
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[blockIdx.x & 0xFFFFFu] = acc;  // practically never: keeps the loads live
 }
 }  // namespace
 
@@ -304,24 +321,57 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_read_probe(cons
 }
 
 // The size-matched probe over `nbuf` rotating (src, dst) pairs, like the rx steps rotate batches.
+// `variant` picks the shape (halo_bench_stream_rw_name): HALO_E_RANGE past the last one.
+namespace {
+struct RwProbe {
+    const char* name;
+    uint32_t u;  // 16-byte loads per thread: the tile is 4u KB
+    void (*kernel)(const uint4*, uint64_t, uint4*, uint64_t, uint64_t, uint32_t*);
+};
+const RwProbe kRwProbes[] = {
+    {"tile16k", 4, stream_rw_kernel<4, false>},     {"tile16k_nt", 4, stream_rw_kernel<4, true>},
+    {"tile32k_nt", 8, stream_rw_kernel<8, true>},   {"tile64k_nt", 16, stream_rw_kernel<16, true>},
+    {"tile32k", 8, stream_rw_kernel<8, false>},
+};
+constexpr int kNumRwProbes = sizeof kRwProbes / sizeof kRwProbes[0];
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) const char* halo_bench_stream_rw_name(int variant) {
+    return variant >= 0 && variant < kNumRwProbes ? kRwProbes[variant].name : nullptr;
+}
+
+extern "C" __attribute__((visibility("default"))) int halo_bench_stream_rw_v(const void* const* srcs,
+                                                                              void* const* dsts, int nbuf,
+                                                                              uint64_t read_bytes, uint64_t write_bytes,
+                                                                              uint32_t* sink, int variant, int warmup,
+                                                                              int steps, void* stream, float* region_ms,
+                                                                              double* wall_s) {
+    if (variant < 0 || variant >= kNumRwProbes) return HALO_E_RANGE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const RwProbe& pr = kRwProbes[variant];
+    const uint64_t r16 = read_bytes / 16, w16 = write_bytes / 16;
+    const uint64_t tile16 = 256ull * pr.u;
+    const uint64_t tiles = (r16 + tile16 - 1) / tile16;
+    if (!tiles || nbuf <= 0 || tiles > 0xFFFFFFFFull) return HALO_E_INVAL;
+    const uint64_t wt16 = (w16 + tiles - 1) / tiles;
+    auto launch = [&](int step) {
+        const int b = step % nbuf;
+        hipLaunchKernelGGL(pr.kernel, dim3((uint32_t)tiles), dim3(256), 0, s, static_cast<const uint4*>(srcs[b]), r16,
+                           static_cast<uint4*>(dsts[b]), w16, wt16, sink);
+        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
+    };
+    return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
+}
+
+// The first shape (16 KB tiles, plain loads and stores): round 5's probe.
 extern "C" __attribute__((visibility("default"))) int halo_bench_stream_rw(const void* const* srcs,
                                                                             void* const* dsts, int nbuf,
                                                                             uint64_t read_bytes, uint64_t write_bytes,
                                                                             uint32_t* sink, int warmup, int steps,
                                                                             void* stream, float* region_ms,
                                                                             double* wall_s) {
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    const uint64_t r16 = read_bytes / 16, w16 = write_bytes / 16;
-    const uint64_t tiles = (r16 + 1023) / 1024;
-    if (!tiles || nbuf <= 0) return HALO_E_INVAL;
-    const uint64_t wt16 = (w16 + tiles - 1) / tiles;
-    auto launch = [&](int step) {
-        const int b = step % nbuf;
-        hipLaunchKernelGGL(stream_rw_kernel, dim3((uint32_t)tiles), dim3(256), 0, s, static_cast<const uint4*>(srcs[b]),
-                           r16, static_cast<uint4*>(dsts[b]), w16, wt16, sink);
-        return hipGetLastError() == hipSuccess ? HALO_OK : HALO_E_HIP;
-    };
-    return timed_loop(launch, warmup, steps, s, region_ms, wall_s);
+    return halo_bench_stream_rw_v(srcs, dsts, nbuf, read_bytes, write_bytes, sink, 0, warmup, steps, stream, region_ms,
+                                  wall_s);
 }
 
 // The transmit build's own layout with no build work (the tx_build line's layout-matched probe):

@@ -1,6 +1,9 @@
 """Phase timeline of the ring walk's guess kernel from a HALO_GUESS_TRACE build (tools only):
 per tile the start, bytes in, tables built, guess chosen, walk done, records kept, in us.
-usage: python tools/exp/guess_trace.py <libhalo_rx_gtrace.so> [frames] [length]"""
+The trace hooks were taken out of the product source in round 6; build the traced library from
+the last revision that had them:
+    tools/exp/build_rev.sh 9391269 gtrace -DHALO_GUESS_TRACE=1
+usage: python tools/exp/guess_trace.py tools/exp/libhalo_rx_gtrace.so [frames] [length]"""
 import ctypes
 import sys
 
