@@ -1250,12 +1250,38 @@ def e2e_host(dev, netif, steps: int):
     return res
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the process's cgroup allows (cgroup v2 cpu.max "quota period"), or None
+    when unlimited or unknown: on the GPU box the affinity mask lists every CPU of the machine while
+    the quota is the box's share for one GPU."""
+    try:
+        cg = "/sys/fs/cgroup"
+        for ln in open("/proc/self/cgroup"):
+            parts = ln.strip().split(":", 2)
+            if len(parts) == 3 and parts[0] == "0":
+                cand = os.path.join(cg, parts[2].lstrip("/"), "cpu.max")
+                if os.path.exists(cand):
+                    cg = os.path.dirname(cand)
+                break
+        if os.path.exists(os.path.join(cg, "cpu.max")):
+            q, per = open(os.path.join(cg, "cpu.max")).read().split()[:2]
+            return None if q == "max" else round(int(q) / int(per), 2)
+        v1 = os.path.join(cg, "cpu")  # cgroup v1: cfs quota / period
+        q = int(open(os.path.join(v1, "cpu.cfs_quota_us")).read())
+        per = int(open(os.path.join(v1, "cpu.cfs_period_us")).read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(fr, seconds: float, rotate: int):
     """The C oracle (scalar restatement of the Go path) on the host over the SAME workload the GPU
     line rotates through: the rank's whole shard (`rotate` batches, 16M x 64 B = 1.07 GB of frames +
     512 MB of records at the defaults), so no pass is served from the CPU caches.
     One thread (the reference's one goroutine per NetIf), the box's CPU share for one GPU
     (OMP_NUM_THREADS) and every CPU in the affinity mask, index-sharded over the threads."""
+    import resource
+
     import numpy as np
 
     from oracle import oracle
@@ -1272,14 +1298,16 @@ def cpu_baseline(fr, seconds: float, rotate: int):
     every = max(1, min(affinity, n // 4096, 1024))
     for threads in sorted({1, share, every}):
         oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads, out=out)  # warm
-        passes, t0 = 0, time.perf_counter()
+        passes, t0, c0 = 0, time.perf_counter(), resource.getrusage(resource.RUSAGE_SELF)
         while True:
             oracle.rx_batch(host, lay["lens"], netif, 1, offsets_dw=lay["offsets_dw"], threads=threads, out=out)
             passes += 1
             el = time.perf_counter() - t0
             if el >= seconds / 2 or (threads > 1 and el >= 2.0):
                 break
-        res[threads] = (passes * n / el / 1e6, passes, el)
+        c1 = resource.getrusage(resource.RUSAGE_SELF)
+        busy = (c1.ru_utime - c0.ru_utime) + (c1.ru_stime - c0.ru_stime)  # CPU seconds of every thread
+        res[threads] = (passes * n / el / 1e6, passes, el, round(busy / el, 1))
     one, mt, sh = res[1], res[every], res[share]
     model = "unknown"
     try:
@@ -1289,14 +1317,17 @@ def cpu_baseline(fr, seconds: float, rotate: int):
                 break
     except OSError:
         pass
-    shard = f"{n >> 20}M x {int(lay['lens'][0])}B UDP frames ({rotate} batches, the GPU line's rotation)"
+    shard = f"{n / 2 ** 20:g}M x {int(lay['lens'][0])}B UDP frames ({rotate} batches, the GPU line's rotation)"
+    quota = cgroup_cpu_quota()
     return {"value": round(one[0], 3), "unit": "Mpps", "cores": 1, "kind": "port",
             "sample": f"{shard}, {one[1]} passes in {one[2]:.1f}s, oracle/halo_rx_oracle.c -O2, one thread; "
                       f"cpu={model}",
             "multi_thread": {"value": round(mt[0], 3), "threads": every, "passes": mt[1],
-                             "cpus_in_affinity": affinity, "cpu_model": model,
-                             "note": "the same shard index-sharded over threads = len(sched_getaffinity)"},
-            "multi_thread_share": {"value": round(sh[0], 3), "threads": share, "passes": sh[1],
+                             "cpus_in_affinity": affinity, "cpu_quota_cores": quota, "cores_busy": mt[3],
+                             "cpu_model": model,
+                             "note": "the same shard index-sharded over threads = len(sched_getaffinity); "
+                                     "the process's cgroup CPU quota (cpu_quota_cores) caps what they get"},
+            "multi_thread_share": {"value": round(sh[0], 3), "threads": share, "passes": sh[1], "cores_busy": sh[3],
                                    "note": "the box's CPU share for one GPU (OMP_NUM_THREADS)"}}
 
 
@@ -1322,7 +1353,7 @@ def _compact_cpu(c: dict) -> dict:
         out["sample"] = str(c["sample"])[:_SAMPLE_MAX]
     for k in ("multi_thread", "multi_thread_share"):
         if isinstance(c.get(k), dict):
-            out[k] = {kk: c[k][kk] for kk in ("value", "threads", "cpus_in_affinity") if kk in c[k]}
+            out[k] = {kk: c[k][kk] for kk in ("value", "threads", "cpus_in_affinity", "cpu_quota_cores", "cores_busy") if kk in c[k]}
     return out
 
 

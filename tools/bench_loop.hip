@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(BLOCK) read_tile_kernel(const uint4* __restric
 // shapes (tile size, non-temporal loads and stores) of which bench.py takes the fastest, so that the
 // probe is a ceiling at every size (the 16 KB plain shape alone ran slower than the
 // rx kernel at 16M frames).
-template <int U, bool NT>
+template <int U, bool NT, bool NT_ST = NT>
 __global__ void __launch_bounds__(256) stream_rw_kernel(const uint4* __restrict__ src, uint64_t r16,
                                                         uint4* __restrict__ dst, uint64_t w16, uint64_t wt16,
                                                         uint32_t* __restrict__ sink) {
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(256) stream_rw_kernel(const uint4* __restrict_
     for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     const uint64_t w0 = t * wt16, w1 = w0 + wt16 < w16 ? w0 + wt16 : w16;
     for (uint64_t k = w0 + threadIdx.x; k < w1; k += 256) {
-        if (NT) {
+        if (NT_ST) {
             const u32x4 x = {(uint32_t)k, (uint32_t)t, 0u, 0u};
             __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(dst) + k);
         } else {
@@ -332,6 +332,8 @@ const RwProbe kRwProbes[] = {
     {"tile16k", 4, stream_rw_kernel<4, false>},     {"tile16k_nt", 4, stream_rw_kernel<4, true>},
     {"tile32k_nt", 8, stream_rw_kernel<8, true>},   {"tile64k_nt", 16, stream_rw_kernel<16, true>},
     {"tile32k", 8, stream_rw_kernel<8, false>},
+    // which half of the non-temporal gain is whose: NT loads with plain stores, and the reverse
+    {"tile16k_ntld", 4, stream_rw_kernel<4, true, false>}, {"tile16k_ntst", 4, stream_rw_kernel<4, false, true>},
 };
 constexpr int kNumRwProbes = sizeof kRwProbes / sizeof kRwProbes[0];
 }  // namespace

@@ -98,6 +98,13 @@ for s in "$@"; do
            step krd 600 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krd" -o run -- python3 tools/prof_kernels.py $PK_ARGS
            step kwrq 600 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/kwrq" -o run -- python3 tools/prof_kernels.py $PK_ARGS
            step ksq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ksq" -o run -- python3 tools/prof_kernels.py $PK_ARGS ;;
+    txbc)  PK_ARGS="tx_build_udp_1M_64B tx_build_udp_256k_1514B probe_tx_build_64B probe_tx_build_1514B"
+           step txb_kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/txb_kt" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step txb_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/txb_sq1" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step txb_sq2 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d "$OUT/txb_sq2" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step txb_rd 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/txb_rd" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step txb_wr 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/txb_wr" -o run -- python3 tools/prof_kernels.py $PK_ARGS ;;
+    pshape) step probe_shapes 300 python tools/exp/probe_shapes.py ;;
     *) echo "unknown step $s" ;;
   esac
 done

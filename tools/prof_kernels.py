@@ -37,6 +37,10 @@ WORKLOADS = [
     # transmit construction (§8f row f2, Build*): bench.tx_build_secondary's two workloads
     ("tx_build_udp_1M_64B", dict(length=64), 1 << 20, 1, 20, 0, 1, 22),
     ("tx_build_udp_256k_1514B", dict(length=64), 1 << 18, 1, 10, 0, 1, 1472),
+    # the size-matched probes of the two tx_build lines (every stream_rw_kernel shape, 10 launches
+    # each): the same bytes in and out with no build work, for counters next to the build's
+    ("probe_tx_build_64B", dict(length=64), 1 << 20, 1, 10, 0, 1, 22),
+    ("probe_tx_build_1514B", dict(length=64), 1 << 18, 1, 10, 0, 1, 1472),
 ]
 
 
@@ -103,6 +107,15 @@ def main():
             torch.cuda.synchronize()
             print(f"{name}: {launches} launches of {n}", flush=True)
             del bs, out, pk
+            torch.cuda.empty_cache()
+            continue
+        if name.startswith("probe_tx_build"):
+            del bs, out
+            plen = hint
+            stride = 64 if plen <= 22 else 1516
+            d = bench.Dist()
+            k = bench.size_matched_probe(dev, n * (40 + plen), n * (stride + 3), d, nbuf=1, steps=launches)
+            print(f"{name}: {launches} launches per shape, {bench.LAST_PROBE_SHAPES} (best {k:.5f} ms)", flush=True)
             torch.cuda.empty_cache()
             continue
         if name.startswith("tx_build"):
