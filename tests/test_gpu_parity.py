@@ -768,3 +768,62 @@ def test_netif_packet_handle_batch(dev, golden, oracle_lib):
     assert (0xC0A86401, 12345, bytes(range(22))) in got_udp
     # TCP payload starts at segment byte headerLen = 5 (tcp.go:49,68 quirk): 15 header bytes first
     assert any(len(p) == 33 and p[15:] == b"hello tcp payload!" for _, p, _, _, _ in got_tcp)
+
+
+def _dense_repack(src: np.ndarray, src_offs_dw: np.ndarray, lens: np.ndarray, lead_dw: int):
+    """Frames src[4*src_offs_dw[i] : +lens[i]] packed back to back at 4-byte-aligned starts, the first
+    `lead_dw` dwords into the buffer (so a 64-frame window's span starts off a 16-byte boundary)."""
+    sizes = (lens.astype(np.int64) + 3) & ~3
+    offs = np.zeros(len(lens), dtype=np.int64)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    offs += 4 * lead_dw
+    out = np.full(int(offs[-1] + sizes[-1]) + 64, 0x5A, dtype=np.uint8)
+    for i in range(len(lens)):
+        s, L, o = int(src_offs_dw[i]) * 4, int(lens[i]), int(offs[i])  # Python ints (NEP 50: no u16 wrap)
+        out[o:o + L] = src[s:s + L]
+    return out, (offs // 4).astype(np.uint32)
+
+
+@pytest.mark.parametrize("case", ["64B_aligned", "64B_lead1", "64B_lead3", "ragged_1to64", "mixed_long",
+                                  "swapped", "partial_tail"])
+def test_lane_coalesced_windows(dev, oracle_lib, case):
+    """The lane kernel's coalesced round 0 (rx_parse.hip lane_window_coalesced): windows of 64 frames of
+    <= 64 B packed back to back are read as whole rows through LDS; any other window (a longer frame,
+    frames out of order, the batch's partial last window) per lane. Every layout bit-exact vs the
+    oracle, histogram = records, under the lane variant and the automatic one (hint 64)."""
+    from halo_amd import synth
+    from halo_amd._lib import NetIf
+
+    rng = np.random.default_rng(zlib_crc(case))
+    n = 64 * 700 + (17 if case == "partial_tail" else 0)
+    long_ = case == "mixed_long"
+    lay = synth.layout(n, length=128 if long_ else 64, mutate_shift=3, first_index=5_000_000)
+    fr = synth.frames_device(lay, NetIf.make(), device=dev)
+    src = fr["bytes"].cpu().numpy()
+    lens = lay["lens"].astype(np.int64).copy()
+    if case == "ragged_1to64":
+        lens = rng.integers(1, 65, n)
+    elif long_:  # 64 B frames, and in one window in five a frame of 65..128 B
+        lens[:] = 64
+        for w in range(0, n // 64, 5):
+            lens[64 * w + int(rng.integers(0, 64))] = int(rng.integers(65, 129))
+    lead = {"64B_lead1": 1, "64B_lead3": 3}.get(case, 0)
+    data, offs = _dense_repack(src, lay["offsets_dw"], lens.astype(np.uint16), lead)
+    if case == "swapped":  # frames in memory order, but two records of every other window swapped
+        for w in range(0, n // 64, 2):
+            a, b = 64 * w + 5, 64 * w + 40
+            offs[a], offs[b] = offs[b], offs[a]
+            lens[a], lens[b] = lens[b], lens[a]
+    lens16 = lens.astype(np.uint16)
+    want, whist = oracle_lib.rx_batch(data, lens16, oracle_lib.NetIf.make(), 1, offsets_dw=offs, threads=8)
+    for variant, hint in ((1, 0), (0, 64)):
+        got, hist = _parse_ragged(dev, data, offs, lens16, 1, hint=hint, variant=variant)
+        assert_records_equal(got, want, None, f"coalesced windows {case} variant={variant}")
+        assert np.array_equal(hist, whist.astype(np.int64))
+    assert whist[1:].sum() > 0
+
+
+def zlib_crc(s: str) -> int:
+    import zlib
+
+    return zlib.crc32(s.encode())
