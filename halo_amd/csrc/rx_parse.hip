@@ -44,13 +44,23 @@
 namespace halo {
 namespace {
 
-__device__ __forceinline__ void store16(uint4* dst, uint4 v) {
-#if HALO_RX_NT_STORES
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst));
-#else
-    *dst = v;
+// NT: a non-temporal store. The byte-stream kernel's records take it (HALO_RX_STREAM_NT_STORES):
+// IMIX 1.272 -> 1.244 / 1.240 ms on one box (profiles/r06/r6c/ab_nt.log); the lane kernel's do
+// not (1M x 64 B 21.5 -> 22.2 us in the same A/B; §15.4).
+#ifndef HALO_RX_STREAM_NT_STORES
+#define HALO_RX_STREAM_NT_STORES 1
 #endif
+#ifndef HALO_RX_NT_STORES  // every other record store (measurement knob)
+#define HALO_RX_NT_STORES 0
+#endif
+template <bool NT = (HALO_RX_NT_STORES != 0)>
+__device__ __forceinline__ void store16(uint4* dst, uint4 v) {
+    if constexpr (NT) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(dst));
+    } else {
+        *dst = v;
+    }
 }
 
 // Byte offset of the IPv4 header in the buffer: 14 in an Ethernet frame, 0 for a LoChan packet
@@ -662,89 +672,13 @@ __device__ __forceinline__ void group_kernel_body(const RxParams& p) {
 template <int LAYOUT, int FUSE>
 __device__ __forceinline__ void lane_window_finish(const RxParams& p, uint32_t base, uint32_t lane, FrameState<1>& st,
                                                    uint4* s_rec_w, Hist& hist);
-// Coalesced round 0 (HALO_RX_LANE_COALESCE): when a wave's 64 frames are all present, each at most
-// 64 bytes and packed back to back in index order (a ring's records, a NIC batch), the wave reads
-// their span [first frame, last frame's end) as whole rows: load u of lane l takes the 16 bytes at
-// span dword b + 256 u + 4 l (b: the first frame's start rounded down to 16 bytes), so each load
-// instruction reads 1 KB contiguous — full 128-byte lines — instead of 64 frames' chunk u at a 64-byte
-// stride; non-temporal (HALO_RX_LANE_COALESCE_NT), which only pays when a load instruction covers
-// whole lines (the per-lane NT loads cost 18 %, §4.4). The rows go to the wave's LDS window
-// (16 span dwords per 20-dword row: frame-aligned 64-byte frames then read back with conflict-free
-// ds_read_b128), and each lane takes its own frame's 16 dwords from there. Every loaded 16-byte
-// block holds a frame byte of the span (the read contract, §3). Other windows take the per-lane loads.
-#ifndef HALO_RX_LANE_COALESCE
-#define HALO_RX_LANE_COALESCE 1
-#endif
-#ifndef HALO_RX_LANE_COALESCE_NT
-#define HALO_RX_LANE_COALESCE_NT 1
-#endif
-constexpr uint32_t kWinRows = 5;  // 64 x 16 dwords + up to 3 of alignment
-constexpr uint32_t kWinPitch = 20;  // LDS dwords per 16 span dwords
-constexpr uint32_t kWinDw = (kWinRows * 256 + 16) / 16 * kWinPitch;  // + the dwords a short frame's 16 reads pass
-__device__ __forceinline__ uint32_t win_at(uint32_t a) { return (a >> 4) * kWinPitch + (a & 15u); }
-
-template <int LAYOUT>
-__device__ __forceinline__ bool lane_window_coalesced(const RxParams& p, uint32_t base, uint32_t lane,
-                                                      FrameState<1>& st, uint32_t* s_win_w) {
-    if (base + 64 > p.n) return false;  // uniform: a partial window
-    const uint32_t o = (uint32_t)((uint64_t)(st.frame - p.bytes) >> 2);  // the frame's span dword
-    const uint32_t fdw = (st.L + 3u) >> 2;
-    const uint32_t nxt = (uint32_t)__shfl_down((int)o, 1, 64);
-    const bool ok = fdw <= 16u && (lane == 63u || nxt == o + fdw);
-    if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;  // uniform
-    const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)o) & ~3u;
-    const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)(o + fdw), 63);
-    if (e - b > kWinRows * 256u) return false;  // uniform (never, given the checks above)
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4* src = reinterpret_cast<const u32x4*>(p.bytes) + (b >> 2);
-    // every lane loads every row (a block past the span re-reads the span's last block: no
-    // predicated loads, whose undefined lanes cost the compiler 80 VGPRs of copies)
-    const uint32_t span = e - b, last = (span - 1u) & ~3u;
-    u32x4 v[kWinRows];
-#pragma unroll
-    for (uint32_t u = 0; u < kWinRows; ++u) {
-        const uint32_t a = 256u * u + 4u * lane, ac = a < span ? a : last;
-#if HALO_RX_LANE_COALESCE_NT
-        v[u] = __builtin_nontemporal_load(src + (ac >> 2));
-#else
-        v[u] = src[ac >> 2];
-#endif
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kWinRows; ++u) {
-        const uint32_t a = 256u * u + 4u * lane;
-        if (a < span) *reinterpret_cast<u32x4*>(s_win_w + win_at(a)) = v[u];
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t rel = o - b;
-    if (__builtin_amdgcn_ballot_w64((rel & 15u) != 0u) == 0) {  // uniform: every frame starts a row
-        const uint32_t* f = s_win_w + (rel >> 4) * kWinPitch;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const u32x4 x = *reinterpret_cast<const u32x4*>(f + 4 * u);
-            st.buf[u][0] = x.x; st.buf[u][1] = x.y; st.buf[u][2] = x.z; st.buf[u][3] = x.w;
-        }
-    } else {
-#pragma unroll
-        for (int d = 0; d < 16; ++d) st.buf[d >> 2][d & 3] = s_win_w[win_at(rel + d)];
-    }
-#pragma unroll
-    for (int d = 0; d < 16; ++d)
-        if ((uint32_t)d >= st.ndw) st.buf[d >> 2][d & 3] = 0u;  // as load4: nothing past the frame
-    __builtin_amdgcn_wave_barrier();  // read before the records are staged over the window
-    return true;
-}
-
-template <int LAYOUT, int FUSE, bool COAL = false>
+template <int LAYOUT, int FUSE>
 __device__ __forceinline__ void lane_window(const RxParams& p, uint32_t base, uint32_t lane, uint4* s_rec_w,
-                                           Hist& hist, uint32_t* s_win_w = nullptr) {
+                                           Hist& hist) {
     const uint32_t i = base + lane;
     FrameState<1> st;
     frame_meta<LAYOUT>(p, i, i < p.n, st);
-    bool coal = false;
-    if constexpr (COAL && HALO_RX_LANE_COALESCE && (LAYOUT == 0 || LAYOUT == 3))
-        coal = lane_window_coalesced<LAYOUT>(p, base, lane, st, s_win_w);
-    if (!coal) frame_loads<1>(0, st);  // uniform
+    frame_loads<1>(0, st);
     lane_window_finish<LAYOUT, FUSE>(p, base, lane, st, s_rec_w, hist);
 }
 
@@ -771,10 +705,8 @@ __device__ __forceinline__ void lane_window(const RxParams& p, uint32_t base, ui
 // A/B knobs: dynamic LDS bytes per lane-kernel block (caps resident blocks per CU, i.e. the
 // frame bytes in flight), and XCD-contiguous block order (blocks b, b+8, ... share an XCD; with
 // the remap each XCD's blocks take one contiguous range of the batch).
-// per wave: the record staging (512 dwords) or, with the coalesced round 0, the window it aliases
-constexpr uint32_t kLaneLdsDw = HALO_RX_LANE_COALESCE ? (kWinDw > 512u ? kWinDw : 512u) : 512u;
-#ifndef HALO_RX_LANE_LDS_PAD  // the block's LDS stays 2 KB + 4608 B whatever the window takes
-#define HALO_RX_LANE_LDS_PAD (4u * ::halo::kLaneLdsDw * (HALO_RX_LANE_BLOCK / 64) > 6656u ? 0u : 6656u - 4u * ::halo::kLaneLdsDw * (HALO_RX_LANE_BLOCK / 64))
+#ifndef HALO_RX_LANE_LDS_PAD
+#define HALO_RX_LANE_LDS_PAD 4608
 #endif
 #ifndef HALO_RX_LANE_XCD
 #define HALO_RX_LANE_XCD 0
@@ -805,9 +737,7 @@ __attribute__((amdgpu_waves_per_eu(HALO_RX_LANE_WAVES)))
 #endif
 rx_lane_kernel(const RxParams p) {
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
-    // per wave: the coalesced round 0's window, then (the same bytes) its 64 records of 32 B
-    __shared__ __align__(16) uint32_t s_win[HALO_RX_LANE_BLOCK / 64][kLaneLdsDw];
-    static_assert(kLaneLdsDw % 4 == 0, "rows of uint4");
+    __shared__ uint4 s_rec[HALO_RX_LANE_BLOCK / 64][128];  // per wave: 64 records of 32 B
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
     Hist hist = hist_open(p, s_hist);
@@ -833,9 +763,9 @@ rx_lane_kernel(const RxParams p) {
         st.frame = nx.frame; st.L = nx.L; st.ndw = nx.ndw;
         frame_loads<1>(0, st);
         frame_meta<LAYOUT>(p, i + nwaves * 64, i + nwaves * 64 < p.n, nx);
-        lane_window_finish<LAYOUT, FUSE>(p, base, lane, st, reinterpret_cast<uint4*>(s_win[w]), hist);
+        lane_window_finish<LAYOUT, FUSE>(p, base, lane, st, s_rec[w], hist);
 #else
-        lane_window<LAYOUT, FUSE, true>(p, base, lane, reinterpret_cast<uint4*>(s_win[w]), hist, s_win[w]);
+        lane_window<LAYOUT, FUSE>(p, base, lane, s_rec[w], hist);
 #endif
     }
     flush_hist(p, hist);
@@ -863,7 +793,7 @@ struct MultiParams {
 template <int LAYOUT>
 __global__ void __launch_bounds__(HALO_RX_LANE_BLOCK) rx_lane_multi_kernel(const MultiParams mp) {
     __shared__ uint32_t s_hist[HALO_RX_STATUS_COUNT];
-    __shared__ __align__(16) uint32_t s_win[HALO_RX_LANE_BLOCK / 64][kLaneLdsDw];  // as rx_lane_kernel
+    __shared__ uint4 s_rec[HALO_RX_LANE_BLOCK / 64][128];
     if (threadIdx.x < HALO_RX_STATUS_COUNT) s_hist[threadIdx.x] = 0;
     __syncthreads();
     Hist hist = hist_open(mp.p, s_hist);
@@ -882,7 +812,7 @@ __global__ void __launch_bounds__(HALO_RX_LANE_BLOCK) rx_lane_multi_kernel(const
         p.out = mp.out[b];
         p.n = mp.n[b];
         const uint32_t base = (win - (b ? mp.win_end[b - 1] : 0u)) * 64u;
-        lane_window<LAYOUT, 0, true>(p, base, lane, reinterpret_cast<uint4*>(s_win[w]), hist, s_win[w]);
+        lane_window<LAYOUT, 0>(p, base, lane, s_rec[w], hist);
     }
     flush_hist(mp.p, hist);
 }
@@ -1489,12 +1419,13 @@ rx_stream_kernel(const RxParams p) {
         frame_store<1, FUSE, L3>(p, i, present, 0, h, v, c, hist, &stage[compact ? lane : 2 * lane]);
         wave_lds_sync();
         const uint32_t nrec = p.n - wbase < 64 ? p.n - wbase : 64;
+        constexpr bool kNt = HALO_RX_STREAM_NT_STORES != 0;
         if (compact) {
-            if (lane < nrec) store16(reinterpret_cast<uint4*>(p.out) + wbase + lane, stage[lane]);
+            if (lane < nrec) store16<kNt>(reinterpret_cast<uint4*>(p.out) + wbase + lane, stage[lane]);
         } else {
             uint4* out4 = reinterpret_cast<uint4*>(p.out) + 2ull * wbase;
-            if (lane < 2 * nrec) store16(out4 + lane, stage[lane]);
-            if (64 + lane < 2 * nrec) store16(out4 + 64 + lane, stage[64 + lane]);
+            if (lane < 2 * nrec) store16<kNt>(out4 + lane, stage[lane]);
+            if (64 + lane < 2 * nrec) store16<kNt>(out4 + 64 + lane, stage[64 + lane]);
         }
         wave_lds_sync();
     }

@@ -787,10 +787,11 @@ def _dense_repack(src: np.ndarray, src_offs_dw: np.ndarray, lens: np.ndarray, le
 @pytest.mark.parametrize("case", ["64B_aligned", "64B_lead1", "64B_lead3", "ragged_1to64", "mixed_long",
                                   "swapped", "partial_tail"])
 def test_lane_coalesced_windows(dev, oracle_lib, case):
-    """The lane kernel's coalesced round 0 (rx_parse.hip lane_window_coalesced): windows of 64 frames of
-    <= 64 B packed back to back are read as whole rows through LDS; any other window (a longer frame,
-    frames out of order, the batch's partial last window) per lane. Every layout bit-exact vs the
-    oracle, histogram = records, under the lane variant and the automatic one (hint 64)."""
+    """Lane-kernel windows of 64 frames of <= 64 B packed back to back (spans starting off a 16-byte
+    boundary, ragged 1..64 B lengths), windows with a longer frame, records out of memory order and
+    a partial last window: bit-exact vs the oracle, histogram = records, under the lane variant and
+    the automatic one (hint 64). Written for the coalesced round 0 tried in round 6 (DESIGN §15.4,
+    commit 0b3928e), kept as coverage of the per-lane path's layouts."""
     from halo_amd import synth
     from halo_amd._lib import NetIf
 
