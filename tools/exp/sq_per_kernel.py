@@ -28,7 +28,7 @@ def main():
     vgpr = {}
     for d in args:
         for row in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-            k = short(row["Kernel_Name"])
+            k = short(row["Kernel_Name"]) + f" grid={row['Grid_Size']}"
             per[k][row["Counter_Name"]] += float(row["Counter_Value"])
             disp[k].add((d, row["Dispatch_Id"]))
             vgpr[k] = (row["VGPR_Count"], row["Accum_VGPR_Count"], row["SGPR_Count"], row["LDS_Block_Size"],
@@ -36,7 +36,7 @@ def main():
     dur = defaultdict(list)
     if kt:
         for row in csv.DictReader(open(os.path.join(kt, "run_kernel_trace.csv"))):
-            dur[short(row["Kernel_Name"])].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
+            dur[short(row["Kernel_Name"]) + f" grid={row['Grid_Size_X']}"].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3)
     for k, c in per.items():
         if "probe" in k and "stream_rw" not in k:
             continue
