@@ -309,6 +309,8 @@ def bench_lib():
         L.halo_bench_ring_polls.restype = ctypes.c_int
         L.halo_bench_ring_polls.argtypes = [vp, vp, vp, vp, vp, u32, u32, vp, vp, i32, i32, vp,
                                             ctypes.POINTER(ctypes.c_uint32)]
+        L.halo_bench_steps_queues.restype = ctypes.c_int
+        L.halo_bench_steps_queues.argtypes = [i32, vp, vp, vp, u32, u32, vp, u32, vp, i32] + tail
         L.halo_bench_multi_steps.restype = ctypes.c_int
         L.halo_bench_multi_steps.argtypes = [i32, vp, vp, vp, u32, u32, u32, vp, u32, vp, vp] + tail
         L.halo_bench_host_calls.restype = ctypes.c_int
@@ -1060,6 +1062,32 @@ STATUS_NAMES = ("OK", "ETH_LEN", "ETH_TYPE", "IP_LEN", "IP_VER", "IP_FRAG", "IP_
                 "IP_TOTLEN_UNDERFLOW", "IP_TOTLEN_OVERRUN", "L4_LEN", "ICMP_TYPE", "ICMP_CODE", "L4_CKSUM")
 
 
+def queues_secondary(batches, netif, steps: int, warmup: int, d: Dist, headline_ms: float) -> dict:
+    """The headline step with 2 and 4 launches in flight (step k on stream k % q, each stream its own
+    record array): what a caller that keeps several batches queued, one per NIC queue, gets from the
+    same one-batch launches. The headline itself is one stream, one launch after the other."""
+    import ctypes
+
+    import torch
+
+    n = batches[0]["layout"]["n"]
+    nb = len(batches)
+    arr = lambda xs: (ctypes.c_void_p * len(xs))(*xs)  # noqa: E731
+    res = {}
+    for q in (2, 4):
+        outs = [torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=batches[0]["bytes"].device) for _ in range(q)]
+        w, k = time_native(bench_lib().halo_bench_steps_queues, nb, arr([b["bytes"].data_ptr() for b in batches]),
+                           arr([b["offsets_dw"].data_ptr() for b in batches]),
+                           arr([b["lens"].data_ptr() for b in batches]), n, 1, ctypes.addressof(netif), 64,
+                           arr([o.data_ptr() for o in outs]), q, steps=steps, warmup=warmup, d=d)
+        res[f"queues_{q}"] = {"mpps": round(n * steps / w / 1e6, 1), "ms_per_batch": round(k, 5),
+                              "vs_headline_per_batch": round(headline_ms / k, 4)}
+        del outs
+    res["what"] = ("config 2's one-batch launches with 2 / 4 in flight on as many streams (each its own record "
+                   "array); ms_per_batch = event region / steps")
+    return res
+
+
 def batch_stream_secondary(batches, netif, steps: int, warmup: int, d: Dist, headline_ms: float, k: int = 8) -> dict:
     """The headline's batch stream, k batches per launch (halo_rx_parse_batches_device): each
     batch keeps its own records (k record arrays), the batches rotate as in the headline."""
@@ -1560,6 +1588,7 @@ def main():
         # the batch stream handed over 8 batches per launch (halo_rx_parse_batches_device): the ramp
         # and tail of a 1M-frame launch paid once per 8M frames
         sec["config2_batch_stream"] = batch_stream_secondary(batches, netif, args.steps, args.warmup, d, kern_ms)
+        sec["config2_queues"] = queues_secondary(batches, netif, args.steps, args.warmup, d, kern_ms)
 
         # forward / transmit rewrite (§8f row f2) on the headline frames: DNAT + SNAT + DPDK fill
         import numpy as np

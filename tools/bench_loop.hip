@@ -80,6 +80,58 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_tx_steps(
 }
 
 // Generic timed loop over a launch callback (row f3 kernels: flow-key hashing, XXH3 batches).
+// The headline step on `nq` streams at once (step k on stream k % nq, writing outs[k % nq]): a
+// caller that keeps several batches in flight, as one NIC queue per stream would. The first stream is
+// the caller's; the others are created here, start after an event on it and are joined back into it
+// before the closing event, so one event pair on the caller's stream brackets every launch.
+extern "C" __attribute__((visibility("default"))) int halo_bench_steps_queues(
+    int nbatch, const uint8_t* const* bytes, const uint32_t* const* offsets_dw, const uint16_t* const* lens,
+    uint32_t n, uint32_t flags, const halo_rx_netif_t* netif, uint32_t hint, halo_rx_result_t* const* outs, int nq,
+    int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0 || nq <= 0 || nq > 8 || steps <= 0 || !region_ms || !wall_s) return HALO_E_INVAL;
+    hipStream_t s0 = static_cast<hipStream_t>(stream);
+    hipStream_t q[8] = {s0};
+    hipEvent_t join[8] = {};
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = HALO_OK;
+    for (int k = 1; k < nq && rc == HALO_OK; ++k)
+        if (hipStreamCreateWithFlags(&q[k], hipStreamNonBlocking) != hipSuccess) rc = HALO_E_HIP;
+    for (int k = 0; k < nq && rc == HALO_OK; ++k)
+        if (hipEventCreateWithFlags(&join[k], hipEventDisableTiming) != hipSuccess) rc = HALO_E_HIP;
+    if (rc == HALO_OK && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = HALO_E_HIP;
+    auto launch = [&](int k) -> int {
+        const int b = k % nbatch, j = k % nq;
+        return halo_rx_parse_batch_device(bytes[b], offsets_dw[b], lens[b], n, flags, netif, hint, outs[j], nullptr,
+                                          q[j]);
+    };
+    for (int k = 0; k < warmup && rc == HALO_OK; ++k) rc = launch(k);
+    if (rc == HALO_OK && hipDeviceSynchronize() != hipSuccess) rc = HALO_E_HIP;
+    if (rc == HALO_OK) {
+        const auto t0 = std::chrono::steady_clock::now();
+        (void)hipEventRecord(e0, s0);
+        for (int k = 1; k < nq; ++k) (void)hipStreamWaitEvent(q[k], e0, 0);
+        for (int k = 0; k < steps && rc == HALO_OK; ++k) rc = launch(k);
+        for (int k = 1; k < nq; ++k) {
+            (void)hipEventRecord(join[k], q[k]);
+            (void)hipStreamWaitEvent(s0, join[k], 0);
+        }
+        (void)hipEventRecord(e1, s0);
+        if (hipStreamSynchronize(s0) != hipSuccess && rc == HALO_OK) rc = HALO_E_HIP;
+        const auto t1 = std::chrono::steady_clock::now();
+        *wall_s = std::chrono::duration<double>(t1 - t0).count();
+        *region_ms = -1.0f;
+        (void)hipEventElapsedTime(region_ms, e0, e1);
+    }
+    (void)hipDeviceSynchronize();
+    for (int k = 1; k < nq; ++k)
+        if (q[k]) (void)hipStreamDestroy(q[k]);
+    for (int k = 0; k < nq; ++k)
+        if (join[k]) (void)hipEventDestroy(join[k]);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return rc;
+}
+
 template <typename F>
 static int timed_loop(F launch, int warmup, int steps, hipStream_t s, float* region_ms, double* wall_s) {
     if (steps <= 0 || !region_ms || !wall_s) return HALO_E_INVAL;

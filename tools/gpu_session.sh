@@ -105,6 +105,13 @@ for s in "$@"; do
            step txb_rd 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/txb_rd" -o run -- python3 tools/prof_kernels.py $PK_ARGS
            step txb_wr 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/txb_wr" -o run -- python3 tools/prof_kernels.py $PK_ARGS ;;
     pshape) step probe_shapes 300 python tools/exp/probe_shapes.py ;;
+    pmcall) PK_ARGS="${PKALL:-}"
+           step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step kfetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/kfetch" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step kwrite 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/kwrite" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step krd 600 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/krd" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step kwrq 600 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/kwrq" -o run -- python3 tools/prof_kernels.py $PK_ARGS
+           step ksq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/ksq" -o run -- python3 tools/prof_kernels.py $PK_ARGS ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -82,7 +82,7 @@ def main():
     only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     order = []
     for name, _kw, _n, _rot, launches, *_ in WORKLOADS:
-        if (only is None or name in only) and not name.startswith("ring_"):  # the ring walk: below
+        if (only is None or name in only) and not name.startswith(("ring_", "probe_")):  # the ring walk: below; probes: not ours
             order += [name] * launches
 
     def family(w):
