@@ -101,3 +101,29 @@ def test_limit_is_honoured(limit):
     # secondaries go first; the headline, roofline and CPU baseline are never dropped
     assert len(json.dumps(c)) <= limit or not c["secondary"]
     assert c["roofline"]["frac"] == full["roofline"]["frac"]
+
+
+def test_cpu_baseline_reports_threads_and_busy_cores():
+    """bench.cpu_baseline on a small shard (CPU only): one thread, the share and every CPU, each with
+    its busy-core measurement, and the cgroup quota field present (None where unlimited)."""
+    import numpy as np
+    import torch
+
+    from halo_amd import synth
+    from oracle import oracle as O
+
+    O.build()
+    lay = synth.layout(1 << 16, length=64)
+    data = O.synth_batch(lay["seed"], 0, lay["lens"], lay["kinds"], O.NetIf.make(), offsets_dw=lay["offsets_dw"])
+    res = bench.cpu_baseline({"bytes": torch.from_numpy(np.ascontiguousarray(data)), "layout": lay}, 0.4, 16)
+    assert res["unit"] == "Mpps" and res["cores"] == 1 and res["kind"] == "port" and res["value"] > 0
+    for k in ("multi_thread", "multi_thread_share"):
+        assert res[k]["value"] > 0 and res[k]["threads"] >= 1 and res[k]["cores_busy"] >= 0
+    assert "cpu_quota_cores" in res["multi_thread"]
+    assert "16 batches" in res["sample"]
+    assert len(json.dumps(bench.compact_line({"cpu_baseline": res})["cpu_baseline"])) < 700
+
+
+def test_cgroup_quota_parser(tmp_path, monkeypatch):
+    q = bench.cgroup_cpu_quota()
+    assert q is None or q > 0
