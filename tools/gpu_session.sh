@@ -105,6 +105,8 @@ for s in "$@"; do
            step txb_rd 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum --output-format csv -d "$OUT/txb_rd" -o run -- python3 tools/prof_kernels.py $PK_ARGS
            step txb_wr 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/txb_wr" -o run -- python3 tools/prof_kernels.py $PK_ARGS ;;
     pshape) step probe_shapes 300 python tools/exp/probe_shapes.py ;;
+    profhead) step profhead 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profhead" -o run -- python3 bench.py --no-secondary --no-cpu ;;
+    timix) step tune_imix 300 python tools/tune.py --spec imix:0,570B:0 && step tune_imix2 300 python tools/tune.py --spec imix:-2,570B:-2 ;;
     pmcall) PK_ARGS="${PKALL:-}"
            step kt 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 tools/prof_kernels.py $PK_ARGS
            step kfetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/kfetch" -o run -- python3 tools/prof_kernels.py $PK_ARGS
