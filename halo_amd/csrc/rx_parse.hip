@@ -708,9 +708,6 @@ __device__ __forceinline__ void lane_window(const RxParams& p, uint32_t base, ui
 #ifndef HALO_RX_LANE_LDS_PAD
 #define HALO_RX_LANE_LDS_PAD 4608
 #endif
-#ifndef HALO_RX_LANE_FRONTS  // measurement knob: windows dealt from this many far-apart ranges
-#define HALO_RX_LANE_FRONTS 1
-#endif
 #ifndef HALO_RX_LANE_XCD
 #define HALO_RX_LANE_XCD 0
 #endif
@@ -750,12 +747,6 @@ rx_lane_kernel(const RxParams p) {
     const uint32_t nb = gridDim.x, per = nb >> 3, rem = nb & 7u, xcd = blockIdx.x & 7u;
     const uint32_t lblock = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (blockIdx.x >> 3);
     const uint32_t wave = (lblock * blockDim.x + threadIdx.x) >> 6;
-#elif HALO_RX_LANE_FRONTS > 1
-    // F fronts: consecutive waves take windows from F equal, far-apart ranges of the batch
-    const uint32_t W = (gridDim.x * blockDim.x) >> 6, gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    constexpr uint32_t F = HALO_RX_LANE_FRONTS;
-    const uint32_t per = W / F, rem = W % F, f = gw % F, k = gw / F;
-    const uint32_t wave = f * per + (f < rem ? f : rem) + k;
 #else
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
 #endif
