@@ -192,8 +192,7 @@ struct halo_rx_host_ctx {
         halo::Resident* svc = nullptr;
         uint32_t max_frames = 0;
         uint64_t max_bytes = 0;
-        bool vram = false;           // h_bytes / h_off / h_len are device memory written through the BAR
-        uint8_t* h_bytes = nullptr;  // pinned (or VRAM); d_* are the device's addresses of the same memory
+        uint8_t* h_bytes = nullptr;  // pinned; d_* are the device's addresses of the same memory
         uint8_t* d_bytes = nullptr;
         uint32_t* h_off = nullptr;
         uint32_t* d_off = nullptr;
@@ -229,36 +228,14 @@ struct halo_rx_host_ctx {
     } slot[2];
 };
 
-#ifndef HALO_RESIDENT_VRAM
-#define HALO_RESIDENT_VRAM 1  // resident staging in VRAM when the device has a large BAR
-#endif
-
 namespace {
 void free_resident(halo_rx_host_ctx::Resident& r) {
     halo::resident_destroy(r.svc);  // stops the consumer and waits for its kernel to end
-    auto release = [&](void* p) {
-        if (!p) return;
-        if (r.vram) (void)hipFree(p);
-        else (void)hipHostFree(p);
-    };
-    release(r.h_bytes);
-    release(r.h_off);
-    release(r.h_len);
+    if (r.h_bytes) (void)hipHostFree(r.h_bytes);
+    if (r.h_off) (void)hipHostFree(r.h_off);
+    if (r.h_len) (void)hipHostFree(r.h_len);
     if (r.h_res) (void)hipHostFree(r.h_res);
     r = halo_rx_host_ctx::Resident{};
-}
-
-// Device memory the host writes directly through a large PCI BAR (uncached on the GPU side, so a
-// request's loads always see the bytes the host wrote for it): `*h` and `*d` are the same address.
-template <typename T>
-bool vram_mapped(T** h, T** d, uint64_t bytes) {
-    void* p = nullptr;
-    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    *h = *d = static_cast<T*>(p);
-    return true;
 }
 
 template <typename T>
@@ -402,9 +379,6 @@ int resident_batch(halo_rx_host_ctx* c, const uint8_t* bytes, const uint64_t* of
     if (halo::pack_need(lens, n, cap) > R.max_bytes) return 1;
     if (halo::pack_chunk(bytes, offsets, lens, n, 0, n, R.max_bytes, cap, R.h_bytes, R.h_off, R.h_len, &used) != n)
         return 1;
-    // VRAM staging: the writes went out through the BAR's write-combining buffers; drain them before
-    // the request line (host memory) is written, so the consumer cannot see the request first
-    if (R.vram) __builtin_ia32_sfence();
     uint32_t ulen = lens[0], ustride = 0;
     for (uint32_t i = 1; i < n && ulen; ++i) ulen = lens[i] == ulen ? ulen : 0u;
     if (ulen > cap || (flags & HALO_RX_L3_START)) ulen = 0;  // the strided layout has no L3 form
@@ -628,24 +602,9 @@ extern "C" HALO_API int halo_rx_host_ctx_set_resident(halo_rx_host_ctx_t* ctx, u
     if (max_bytes == 0) max_bytes = std::min<uint64_t>(1516ull * max_frames, 64ull << 20);
     max_bytes = (max_bytes + 3) & ~3ull;
     auto& R = ctx->res;
-    // The staging the consumer reads (frames, offsets, lengths): in the GPU's own memory when the host
-    // can write it through a large BAR (HALO_RESIDENT_VRAM), so the consumer's reads of a request are
-    // local instead of PCIe round trips; else pinned host memory. The records go to host memory.
-    int large_bar = 0;
-    if (HALO_RESIDENT_VRAM && hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, ctx->device) != hipSuccess) {
-        (void)hipGetLastError();
-        large_bar = 0;
-    }
-    if (HALO_RESIDENT_VRAM && large_bar == 1) {
-        R.vram = true;  // (free_resident frees these with hipFree)
-        if (!(vram_mapped(&R.h_bytes, &R.d_bytes, max_bytes + 64) && vram_mapped(&R.h_off, &R.d_off, 4ull * max_frames) &&
-              vram_mapped(&R.h_len, &R.d_len, 2ull * max_frames)))
-            free_resident(R);  // a partial set: start over in host memory (R.vram is false again)
-    }
-    bool ok = R.vram || (pinned_mapped(&R.h_bytes, &R.d_bytes, max_bytes + 64) &&  // + a dword tail any load may cover
-                         pinned_mapped(&R.h_off, &R.d_off, 4ull * max_frames) &&
-                         pinned_mapped(&R.h_len, &R.d_len, 2ull * max_frames));
-    ok = ok && pinned_mapped(&R.h_res, &R.d_res, sizeof(halo_rx_result_t) * (uint64_t)max_frames);
+    bool ok = pinned_mapped(&R.h_bytes, &R.d_bytes, max_bytes + 64) &&  // + a dword tail any load may cover
+              pinned_mapped(&R.h_off, &R.d_off, 4ull * max_frames) && pinned_mapped(&R.h_len, &R.d_len, 2ull * max_frames) &&
+              pinned_mapped(&R.h_res, &R.d_res, sizeof(halo_rx_result_t) * (uint64_t)max_frames);
     ok = ok && halo::resident_create(ctx->device, R.d_bytes, R.d_off, R.d_len, &R.svc) == HALO_OK;
     if (!ok) {
         free_resident(R);
