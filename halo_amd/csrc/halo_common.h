@@ -66,8 +66,8 @@ int check_device();  // 0 if the current device is gfx950, else HALO_E_*
 // kHistStride 64-bit words each (arrivals << 40 | count, one per status), zero between launches.
 // Trees belong to HSA queues, not to streams: a device's tree set holds kHistTrees trees and a key
 // word per tree, and a launch's blocks take the tree whose key is their queue (queue_ptr), claiming
-// a free key on the queue's first launch; keys are never released, so every block of every launch
-// on a queue agrees on its tree. Sharing a tree between launches of one queue is safe because
+// a free key on the queue's first launch; keys are released only by halo_rx_release, with the
+// device drained, so every block of every launch on a queue agrees on its tree. Sharing a tree between launches of one queue is safe because
 // every HIP dispatch carries the AQL barrier bit (profiles/r05/queue_probe.log: null, created and
 // per-thread streams, graph replays): a packet starts only after every earlier packet of its queue
 // has completed, so no two launches are ever inside one tree. hist_trees checks the bit once per
