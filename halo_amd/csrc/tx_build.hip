@@ -456,10 +456,15 @@ __device__ __forceinline__ uint32_t prefix_mask(int32_t n) {
 // a clamped value lands only in bytes the masks drop. Header bytes [0, hdr_end) from the lane's
 // header dwords, payload [hdr_end, pay_end), zero padding after; the L4 segment summed with one
 // v_dot2 per dword. The caller stages o[] in LDS and the wave stores its frames cooperatively.
+// UNI: every active lane of the wave has the same header end, payload end and layout (one protocol,
+// one payload length: the common batch), so the byte masks and the checksum field's position are
+// computed once, in scalar registers (HALO_TXB_SMALL_UNIFORM).
+template <bool UNI>
 __device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f, const uint32_t* hdr,
                                             const void* safe, uint32_t (&o)[16]) {
     const bool csum = (p.flags & HALO_RX_CSUM_ENABLE) != 0;
-    const uint32_t H = f.hdr_end, PE = f.hdr_end + f.plen;
+    const uint32_t H = UNI ? (uint32_t)__builtin_amdgcn_readfirstlane((int)f.hdr_end) : f.hdr_end;
+    const uint32_t PE = UNI ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(f.hdr_end + f.plen)) : f.hdr_end + f.plen;
     const uint64_t sv = f.pay - H;  // virtual address of frame byte 0 in payload space
     const uint32_t sh = (uint32_t)(sv & 3u);
     typedef const __attribute__((address_space(1))) uint32_t gu32_t;
@@ -485,7 +490,7 @@ __device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f
         o[k] = (k < 14 ? hdr[k] & hm : 0u) | (pay & pm & ~hm);
     }
     // L4 segment [base + 20, pay_end): everything past it is already zero
-    const bool l3 = f.base == 0;
+    const bool l3 = (UNI ? (uint32_t)__builtin_amdgcn_readfirstlane((int)f.base) : f.base) == 0;
     uint32_t sum = 0;
 #pragma unroll
     for (int k = 5; k < 16; ++k) {
@@ -501,9 +506,24 @@ __device__ __forceinline__ void build_small(const BuildParams& p, const Frame& f
         ck_at = f.base + 22u;
     }
     const uint32_t ck_le = (csum || f.proto == kIpIcmp) ? (~fold16(part)) & 0xFFFFu : 0u;
-    const uint32_t ck_dw = ck_at >> 2, ck_v = ck_le << ((ck_at & 2u) * 8u);
+    if constexpr (UNI) {  // the field's dword is the wave's: one OR into it
+        const uint32_t at = (uint32_t)__builtin_amdgcn_readfirstlane((int)ck_at);
+        const uint32_t ck_v = ck_le << ((at & 2u) * 8u);
+        switch (at >> 2) {
+            case 5: o[5] |= ck_v; break;
+            case 6: o[6] |= ck_v; break;
+            case 7: o[7] |= ck_v; break;
+            case 8: o[8] |= ck_v; break;
+            case 9: o[9] |= ck_v; break;
+            case 10: o[10] |= ck_v; break;
+            case 11: o[11] |= ck_v; break;
+            default: o[12] |= ck_v; break;
+        }
+    } else {
+        const uint32_t ck_dw = ck_at >> 2, ck_v = ck_le << ((ck_at & 2u) * 8u);
 #pragma unroll
-    for (int k = 5; k < 13; ++k) o[k] |= (uint32_t)k == ck_dw ? ck_v : 0u;
+        for (int k = 5; k < 13; ++k) o[k] |= (uint32_t)k == ck_dw ? ck_v : 0u;
+    }
 }
 
 // BuildUdpPkt / BuildTcpPkt / BuildIcmpPkt's length limits and the slot check (build-defined):
@@ -525,6 +545,9 @@ __device__ __forceinline__ uint32_t verdict(uint32_t d2, uint32_t d9, uint32_t s
 // descriptor's dwords from the lane that holds them (ds_bpermute). No LDS, no barrier.
 #ifndef HALO_TXB_SMALL  // 1: frames <= 64 B on the branch-free lane path (build_small)
 #define HALO_TXB_SMALL 1
+#endif
+#ifndef HALO_TXB_SMALL_UNIFORM  // 1: build_small's masks in scalar registers when the wave agrees
+#define HALO_TXB_SMALL_UNIFORM 1
 #endif
 #ifndef HALO_TXB_DESC_PREFETCH
 #define HALO_TXB_DESC_PREFETCH 1  // 64 B: 24.9 / 24.7 us against 25.5 / 25.0 without (profiles/r05/r5zx)
@@ -654,7 +677,14 @@ tx_build_kernel(const BuildParams p) {
                 const Frame f = decode(d, p.payload);
                 if (HALO_TXB_SMALL && f.flen <= 64u) {
                     uint32_t o[16];
-                    build_small(p, f, hv, p.desc + i, o);
+                    // (the lanes here: this tile's small frames; uniform over them in the common batch)
+                    // (flen <= 64: hdr_end, plen and base < 256; proto sets the checksum field)
+                    const uint32_t sig = f.hdr_end | (f.plen << 8) | (f.base << 16) | (f.proto << 24);
+                    const uint32_t sig0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)sig);
+                    if (HALO_TXB_SMALL_UNIFORM && __builtin_amdgcn_ballot_w64(sig != sig0) == 0)
+                        build_small<true>(p, f, hv, p.desc + i, o);
+                    else
+                        build_small<false>(p, f, hv, p.desc + i, o);
 #pragma unroll
                     for (int k = 0; k < 16; ++k) row[k] = o[k];
                     staged = (f.flen + 3u) >> 2;
