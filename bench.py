@@ -1070,6 +1070,8 @@ def queues_secondary(batches, netif, steps: int, warmup: int, d: Dist, headline_
 
     import torch
 
+    from halo_amd import protocol
+
     n = batches[0]["layout"]["n"]
     nb = len(batches)
     arr = lambda xs: (ctypes.c_void_p * len(xs))(*xs)  # noqa: E731
@@ -1080,9 +1082,22 @@ def queues_secondary(batches, netif, steps: int, warmup: int, d: Dist, headline_
                            arr([b["offsets_dw"].data_ptr() for b in batches]),
                            arr([b["lens"].data_ptr() for b in batches]), n, 1, ctypes.addressof(netif), 64,
                            arr([o.data_ptr() for o in outs]), q, steps=steps, warmup=warmup, d=d)
+        # each stream's record array holds the last batch that stream parsed: the same bytes as one
+        # ordinary launch over that batch
+        ok = True
+        ref = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=outs[0].device)
+        for j in range(q):
+            # (halo_bench_steps_queues numbers warm-up and timed steps from 0 each: step k -> stream
+            # k % q, batch k % nb)
+            timed = [kk for kk in range(steps) if kk % q == j]
+            last = timed[-1] if timed else max(kk for kk in range(warmup) if kk % q == j)
+            b = batches[last % nb]
+            protocol.parse_frames_batch(b["bytes"], b["offsets_dw"], b["lens"], netif=netif, max_len_hint=64, out=ref)
+            ok = ok and bool(torch.equal(ref, outs[j]))
         res[f"queues_{q}"] = {"mpps": round(n * steps / w / 1e6, 1), "ms_per_batch": round(k, 5),
-                              "vs_headline_per_batch": round(headline_ms / k, 4)}
-        del outs
+                              "vs_headline_per_batch": round(headline_ms / k, 4), "ok": ok}
+        assert ok, f"queues_{q}: records differ from a single launch"
+        del outs, ref
     res["what"] = ("config 2's one-batch launches with 2 / 4 in flight on as many streams (each its own record "
                    "array); ms_per_batch = event region / steps")
     return res
