@@ -1119,9 +1119,22 @@ def batch_stream_secondary(batches, netif, steps: int, warmup: int, d: Dist, hea
                         arr([b["offsets_dw"].data_ptr() for b in batches]), arr([b["lens"].data_ptr() for b in batches]),
                         n, k, 1, ctypes.addressof(netif), 64, arr([o.data_ptr() for o in outs]), None, steps=st,
                         warmup=max(2, warmup // k), d=d)
+    # the last launch's k record arrays against one ordinary launch per batch (launch t, slot j ->
+    # batch (t k + j) mod nb: halo_bench_multi_steps)
+    from halo_amd import protocol
+
+    ref = torch.empty((n, RESULT_BYTES), dtype=torch.uint8, device=outs[0].device)
+    ok = True
+    for j in range(k):
+        b = batches[((st - 1) * k + j) % nb]
+        protocol.parse_frames_batch(b["bytes"], b["offsets_dw"], b["lens"], netif=netif, max_len_hint=64, out=ref)
+        ok = ok and bool(torch.equal(ref, outs[j]))
+    assert ok, "batch stream: records differ from one launch per batch"
+    del ref
     fb = frame_bytes(batches[0])
     alg = k * (fb + n * (4 + 2 + RESULT_BYTES))
-    res = {"batches_per_launch": k, "frames_per_launch": k * n, "launches": st, "mpps": round(k * n * st / w / 1e6, 1),
+    res = {"batches_per_launch": k, "frames_per_launch": k * n, "launches": st, "ok": ok,
+           "mpps": round(k * n * st / w / 1e6, 1),
            "kernel_ms": round(km, 5), "ms_per_batch": round(km / k, 5),
            "vs_headline_per_batch": round(headline_ms / (km / k), 4),
            "roofline": roofline(alg, km, frame_bytes=k * fb), "alg_bytes_per_launch": alg,
