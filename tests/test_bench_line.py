@@ -124,6 +124,7 @@ def test_cpu_baseline_reports_threads_and_busy_cores():
     assert len(json.dumps(bench.compact_line({"cpu_baseline": res})["cpu_baseline"])) < 700
 
 
-def test_cgroup_quota_parser(tmp_path, monkeypatch):
+def test_cgroup_quota_parser():
+    """None (unlimited / unknown) or a positive CPU count, on whatever cgroup layout this host has."""
     q = bench.cgroup_cpu_quota()
     assert q is None or q > 0
