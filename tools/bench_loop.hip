@@ -132,6 +132,68 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_steps_queues(
     return rc;
 }
 
+// Tools only (tools/exp/split_steps.py): each step's batch split into `parts` index ranges launched
+// on as many streams at once (fork from the caller's stream by an event, join back by events), so a
+// single batch is fed by several HSA queues. Records are the same as one launch's.
+extern "C" __attribute__((visibility("default"))) int halo_bench_split_steps(
+    int nbatch, const uint8_t* const* bytes, const uint32_t* const* offsets_dw, const uint16_t* const* lens,
+    uint32_t n, uint32_t flags, const halo_rx_netif_t* netif, uint32_t hint, halo_rx_result_t* out, int parts,
+    int warmup, int steps, void* stream, float* region_ms, double* wall_s) {
+    if (nbatch <= 0 || parts <= 0 || parts > 8 || steps <= 0 || !region_ms || !wall_s) return HALO_E_INVAL;
+    hipStream_t s0 = static_cast<hipStream_t>(stream);
+    hipStream_t q[8] = {s0};
+    hipEvent_t fork = nullptr, join[8] = {}, e0 = nullptr, e1 = nullptr;
+    int rc = HALO_OK;
+    for (int k = 1; k < parts && rc == HALO_OK; ++k)
+        if (hipStreamCreateWithFlags(&q[k], hipStreamNonBlocking) != hipSuccess) rc = HALO_E_HIP;
+    if (rc == HALO_OK && hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) rc = HALO_E_HIP;
+    for (int k = 1; k < parts && rc == HALO_OK; ++k)
+        if (hipEventCreateWithFlags(&join[k], hipEventDisableTiming) != hipSuccess) rc = HALO_E_HIP;
+    if (rc == HALO_OK && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) rc = HALO_E_HIP;
+    const uint32_t per = ((n + parts - 1) / parts + 63u) & ~63u;  // whole 64-frame windows per part
+    auto launch = [&](int k) -> int {
+        const int b = k % nbatch;
+        int r = HALO_OK;
+        if (parts > 1) {
+            (void)hipEventRecord(fork, s0);
+            for (int j = 1; j < parts; ++j) (void)hipStreamWaitEvent(q[j], fork, 0);
+        }
+        for (int j = 0; j < parts && r == HALO_OK; ++j) {
+            const uint32_t lo = j * per, cnt = lo >= n ? 0u : (n - lo < per ? n - lo : per);
+            if (cnt)
+                r = halo_rx_parse_batch_device(bytes[b], offsets_dw[b] + lo, lens[b] + lo, cnt, flags, netif, hint,
+                                               out + lo, nullptr, q[j]);
+        }
+        for (int j = 1; j < parts; ++j) {
+            (void)hipEventRecord(join[j], q[j]);
+            (void)hipStreamWaitEvent(s0, join[j], 0);
+        }
+        return r;
+    };
+    for (int k = 0; k < warmup && rc == HALO_OK; ++k) rc = launch(k);
+    if (rc == HALO_OK && hipDeviceSynchronize() != hipSuccess) rc = HALO_E_HIP;
+    if (rc == HALO_OK) {
+        const auto t0 = std::chrono::steady_clock::now();
+        (void)hipEventRecord(e0, s0);
+        for (int k = 0; k < steps && rc == HALO_OK; ++k) rc = launch(k);
+        (void)hipEventRecord(e1, s0);
+        if (hipStreamSynchronize(s0) != hipSuccess && rc == HALO_OK) rc = HALO_E_HIP;
+        const auto t1 = std::chrono::steady_clock::now();
+        *wall_s = std::chrono::duration<double>(t1 - t0).count();
+        *region_ms = -1.0f;
+        (void)hipEventElapsedTime(region_ms, e0, e1);
+    }
+    (void)hipDeviceSynchronize();
+    for (int k = 1; k < parts; ++k) {
+        if (q[k]) (void)hipStreamDestroy(q[k]);
+        if (join[k]) (void)hipEventDestroy(join[k]);
+    }
+    if (fork) (void)hipEventDestroy(fork);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return rc;
+}
+
 template <typename F>
 static int timed_loop(F launch, int warmup, int steps, hipStream_t s, float* region_ms, double* wall_s) {
     if (steps <= 0 || !region_ms || !wall_s) return HALO_E_INVAL;
