@@ -316,6 +316,9 @@ def bench_lib():
         L.halo_bench_host_calls.restype = ctypes.c_int
         L.halo_bench_host_calls.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, i32, i32, vp,
                                             ctypes.POINTER(ctypes.c_uint32)]
+        L.halo_bench_cpu_calls.restype = ctypes.c_int
+        L.halo_bench_cpu_calls.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp, vp, i32, i32, vp,
+                                           ctypes.POINTER(ctypes.c_uint32)]
         L.halo_bench_gather_probe.restype = ctypes.c_int
         L.halo_bench_gather_probe.argtypes = [vp, vp, i32, u32, vp] + tail
         L.halo_bench_tx_layout_probe.restype = ctypes.c_int
@@ -1030,6 +1033,31 @@ def dropin_small_batch(dev, netif, with_cpu: bool = True) -> dict:
             curve[str(m)] = pt
         hb.close()
         res[path] = curve
+    # the CPU entry point (libhalo_rx_cpu.so, include/halo_rx_cpu.h) in the same native per-call loop
+    from halo_amd import _lib
+    from halo_amd import cpu as cpu_entry
+
+    fn = ctypes.cast(cpu_entry.lib.halo_rx_parse_batch_cpu, ctypes.c_void_p).value
+    curve = {}
+    for m in DROPIN_SIZES:
+        iters = 2000 if m <= 256 else 400
+        us = np.zeros(iters, np.float64)
+        bad = ctypes.c_uint32()
+        _lib.check("halo_bench_cpu_calls", bench_lib().halo_bench_cpu_calls(
+            fn, host.ctypes.data, offs.ctypes.data, lens.ctypes.data, m, 1, ctypes.addressof(netif), out.ctypes.data,
+            acts.ctypes.data, 50, iters, us.ctypes.data, ctypes.byref(bad)))
+        med = float(np.median(us))
+        curve[str(m)] = {"us_median": round(med, 3), "us_p10": round(float(np.percentile(us, 10)), 3),
+                         "us_p90": round(float(np.percentile(us, 90)), 3), "mpps": round(m / med, 3),
+                         "bad_calls": int(bad.value)}
+    res["cpu_entry"] = curve
+    ms = np.array(DROPIN_SIZES, np.float64)
+    t_res = np.array([res["resident"][str(m)]["us_median"] for m in DROPIN_SIZES])
+    t_cpu = np.array([curve[str(m)]["us_median"] for m in DROPIN_SIZES])
+    b, a = np.polyfit(ms, t_res, 1)
+    c = float(np.polyfit(ms, t_cpu, 1)[0])
+    res["cpu_entry_ns_per_frame"] = round(c * 1e3, 2)
+    res["cpu_entry_crossover_frames"] = round(float(a / (c - b)), 1) if c > b else None
     if with_cpu:
         from oracle import oracle as O
 
@@ -1392,7 +1420,7 @@ LINE_LIMIT = 7680  # bytes: the final stdout line stays under 8 KB, what the dri
 # percentiles) goes to the detail file only
 _KEEP_NUM = ("mpps", "mstrings_per_s", "mlookups_per_s", "mrecords_per_s", "gbit_s", "kernel_ms", "ms_per_batch",
              "us_per_batch", "ok", "speedup_vs_separate", "vs_headline", "vs_headline_per_batch", "failing_frac",
-             "crossover_frames", "cpu_port_ns_per_frame", "value", "unit", "ms_per_step")
+             "crossover_frames", "cpu_port_ns_per_frame", "cpu_entry_ns_per_frame", "cpu_entry_crossover_frames", "value", "unit", "ms_per_step")
 _KEEP_ROOF = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_session", "frac_frames_only",
               "peak_measured_read", "frac_of_measured", "size_matched_probe_ms", "frac_of_size_matched",
               "frac_of_gather_probe", "frac_of_load_pattern_probe", "frac_of_layout_matched")

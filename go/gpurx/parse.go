@@ -20,8 +20,9 @@ import (
 // C port of the reference's own parse — a GPU round trip per packet is ~350x slower than parsing it
 // on the calling core. These wrappers exist for ported code that needs the reference's signatures;
 // a forward hook that parses every forwarded packet belongs on Ctx.ParseFramesBatch over batches of
-// a few hundred frames or more (the crossover, §13.1). There is no CPU path. protocol.CheckSumEnable
-// is read at every call, as the reference reads it.
+// a few hundred frames or more (the crossover, §13.1), or on ParseFramesCPU (cpu.go), which gives
+// the same Results on the calling core. These wrappers never switch to the CPU by themselves.
+// protocol.CheckSumEnable is read at every call, as the reference reads it.
 
 // Device is the GPU the single-frame wrappers use (set before the first call).
 var Device = 0

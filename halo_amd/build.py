@@ -16,6 +16,9 @@ SOURCES = ["rx_parse.hip", "tx_fixup.hip", "tx_build.hip", "deep_nat.hip", "flow
 # measurement tooling (bench.py's native step loop), linked against the product library
 BENCH_SRC = os.path.join(ROOT, "tools", "bench_loop.hip")
 BENCH_OUT = os.path.join(ROOT, "tools", "libhalo_bench.so")
+# the CPU entry point of SURVEY §8b (include/halo_rx_cpu.h): host code only, its own library
+CPU_SRC = os.path.join(CSRC, "rx_cpu.cc")
+CPU_OUT = os.path.join(ROOT, "halo_amd", "lib", "libhalo_rx_cpu.so")
 HEADERS = ["halo_common.h", "halo_limits.h", "host_logic.h", "device_util.h", os.path.join("..", "..", "include", "halo_rx.h")]
 
 
@@ -61,6 +64,22 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return OUT
 
 
+def build_cpu(force: bool = False, verbose: bool = False) -> str:
+    """halo_amd/lib/libhalo_rx_cpu.so (g++): halo_rx_parse_batch_cpu. No HIP, no link to libhalo_rx."""
+    deps = [CPU_SRC, os.path.join(CSRC, "halo_limits.h"), os.path.join(ROOT, "include", "halo_rx.h"),
+            os.path.join(ROOT, "include", "halo_rx_cpu.h")]
+    if not force and os.path.exists(CPU_OUT) and os.path.getmtime(CPU_OUT) >= max(map(os.path.getmtime, deps)):
+        return CPU_OUT
+    os.makedirs(os.path.dirname(CPU_OUT), exist_ok=True)
+    cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-Wall", "-Wextra",
+           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, CPU_SRC, "-o", CPU_OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(CPU_OUT + ".tmp", CPU_OUT)
+    return CPU_OUT
+
+
 def build_bench(force: bool = False, verbose: bool = False) -> str:
     """tools/libhalo_bench.so: the native timed step loop used by bench.py."""
     lib = build(force=False, verbose=verbose)
@@ -82,4 +101,5 @@ def build_bench(force: bool = False, verbose: bool = False) -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_cpu(force="--force" in sys.argv, verbose=True))
     print(build_bench(force="--force" in sys.argv, verbose=True))

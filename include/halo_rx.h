@@ -28,7 +28,9 @@
  *   - The caller owns every buffer. No globals: `flags` replaces protocol.CheckSumEnable.
  *   - Calls are thread-safe per (device, stream).
  *   - There is no CPU fallback: without a gfx950 device every compute entry point
- *     returns HALO_E_NODEV / HALO_E_ARCH.
+ *     returns HALO_E_NODEV / HALO_E_ARCH. The CPU entry point SURVEY.md §8b also lists,
+ *     halo_rx_parse_batch_cpu, is a separate library a caller picks by name
+ *     (include/halo_rx_cpu.h, libhalo_rx_cpu.so); nothing here calls it.
  *
  * Frame layout in device memory (DESIGN.md "Data layout in HBM"):
  *   - ragged:  frame i starts at bytes + 4*offsets_dw[i] (4-byte aligned starts, as the

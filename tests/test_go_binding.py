@@ -64,8 +64,36 @@ int main(void) {
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
 
 
+def test_cpu_entry_preamble_compiles_links_and_runs(tmp_path):
+    """go/gpurx/cpu.go's preamble: halo_rx_cpu.h + -lhalo_rx_cpu, one all-zero frame (ETH_TYPE)."""
+    drv = tmp_path / "cpu.c"
+    drv.write_text(r'''
+#include <string.h>
+#include "halo_rx_cpu.h"
+int main(void) {
+    halo_rx_netif_t n;
+    memset(&n, 0, sizeof n);
+    uint8_t frame[64] = {0};
+    uint64_t off = 0;
+    uint16_t len = 64;
+    halo_rx_result_t r;
+    if (halo_rx_parse_batch_cpu(frame, &off, &len, 1, HALO_RX_CSUM_ENABLE | HALO_RX_L3_START, &n, &r, NULL) != HALO_OK)
+        return 2;
+    if (r.status != HALO_RX_IP_VER) return 3;
+    if (halo_rx_parse_batch_cpu(frame, &off, &len, 1, HALO_RX_CSUM_ENABLE, &n, &r, NULL) != HALO_OK) return 4;
+    return r.status == HALO_RX_ETH_TYPE ? 0 : 5;
+}
+''')
+    exe = tmp_path / "cpu"
+    cmd = ["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", f"-I{os.path.join(ROOT, 'include')}", str(drv),
+           f"-L{LIBDIR}", "-lhalo_rx_cpu", f"-Wl,-rpath,{LIBDIR}", "-o", str(exe)]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+
+
 def _header_names():
-    h = _src(HDR) + _src(os.path.join(GO, "gpurx", "gpurx_shim.h"))
+    h = _src(HDR) + _src(os.path.join(GO, "gpurx", "gpurx_shim.h")) + _src(os.path.join(ROOT, "include", "halo_rx_cpu.h"))
     names = set(re.findall(r"\b(halo_\w+|HALO_\w+|gpurx_\w+)\b", h))
     return names | {"uint8_t", "uint16_t", "uint32_t", "uint64_t", "int64_t", "int", "GoString"}
 

@@ -670,6 +670,32 @@ extern "C" __attribute__((visibility("default"))) int halo_bench_host_calls(
     return HALO_OK;
 }
 
+// The same per-call loop over the CPU entry point (include/halo_rx_cpu.h), passed as a function
+// pointer so that this library does not link libhalo_rx_cpu.so: halo_rx_parse_batch_cpu +
+// halo_rx_dispatch per call, on the calling core.
+typedef int (*halo_cpu_parse_fn)(const uint8_t*, const uint64_t*, const uint16_t*, uint32_t, uint32_t,
+                                 const halo_rx_netif_t*, halo_rx_result_t*, uint32_t*);
+extern "C" __attribute__((visibility("default"))) int halo_bench_cpu_calls(
+    void* parse_cpu, const uint8_t* bytes, const uint64_t* offs, const uint16_t* lens, uint32_t m, uint32_t flags,
+    const halo_rx_netif_t* netif, halo_rx_result_t* out, uint8_t* acts, int warmup, int iters, double* us,
+    uint32_t* bad) {
+    if (!parse_cpu || !netif || !out || !acts || !us || !bad || iters <= 0) return HALO_E_INVAL;
+    const auto fn = reinterpret_cast<halo_cpu_parse_fn>(parse_cpu);
+    *bad = 0;
+    for (int k = 0; k < warmup + iters; ++k) {
+        const auto t0 = std::chrono::steady_clock::now();
+        int rc = fn(bytes, offs, lens, m, flags, netif, out, nullptr);
+        if (!rc) rc = halo_rx_dispatch(out, m, netif, acts, nullptr);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc) return rc;
+        bool ok = true;
+        for (uint32_t i = 0; ok && i < m; ++i) ok = out[i].status == HALO_RX_OK && acts[i] == HALO_RX_ACT_LOCAL_UDP;
+        if (!ok) ++*bad;
+        if (k >= warmup) us[k - warmup] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+    }
+    return HALO_OK;
+}
+
 // The batch stream handed over k batches per launch (halo_rx_parse_batches_device): step t parses
 // batches (t * k + j) % nbatch, j < k, into outs[j].
 extern "C" __attribute__((visibility("default"))) int halo_bench_multi_steps(
