@@ -31,6 +31,19 @@ type BatchConfig struct {
 	// (~33-37 us for <= 256 frames instead of ~8 us, DESIGN.md §13.1), and no kernel stays on the
 	// GPU between batches.
 	Launched bool
+	// CPUBelow sends a batch (or LoChan drain) of fewer frames to the CPU entry point
+	// (gpurx.ParseBatchCPU, halo_rx_parse_batch_cpu): the same records on this goroutine's core,
+	// ~9 ns per frame against ~8 us per GPU round trip, so below ~3,800 frames it is the faster
+	// path (INTEGRATION.md §1a). 0 keeps every batch on the GPU.
+	CPUBelow int
+}
+
+// parse is ParseBatch on the GPU, or on the CPU entry point below cfg.CPUBelow frames.
+func (cfg *BatchConfig) parse(x *gpurx.Ctx, b *gpurx.Batch, netif *gpurx.NetIfCfg, l3 bool) error {
+	if b.Len() < cfg.CPUBelow {
+		return gpurx.ParseBatchCPU(b, netif, l3)
+	}
+	return x.ParseBatch(b, netif, l3)
 }
 
 // PacketHandleBatched replaces `go netIf.PacketHandle()` (engine.go:299) for a NetIf whose frames
@@ -74,7 +87,7 @@ func (i *NetIf) PacketHandleBatched(x *gpurx.Ctx, cfg BatchConfig) {
 			}
 		}
 		if b.Len() > 0 {
-			if err := x.ParseBatch(b, netif, false); err != nil {
+			if err := cfg.parse(x, b, netif, false); err != nil {
 				Log(fmt.Sprintf("gpurx parse error: %v\n", err))
 			} else {
 				for k := 0; k < b.Len(); k++ {
@@ -83,7 +96,7 @@ func (i *NetIf) PacketHandleBatched(x *gpurx.Ctx, cfg BatchConfig) {
 			}
 		}
 		if cfg.DrainEvery == 0 || n >= cfg.DrainEvery {
-			i.drainLoChanBatched(x, netif, cfg.Batch)
+			i.drainLoChanBatched(x, netif, &cfg)
 			n = 0
 		}
 	}
@@ -171,11 +184,13 @@ func (i *NetIf) deliverParsed(buf []byte, ipOff int, r *gpurx.Result) {
 }
 
 // drainLoChanBatched is PacketHandle's loopback drain (engine.go:353-381): until LoChan is empty,
-// take what is queued (at most `max` packets per GPU call), parse it with HALO_RX_L3_START and act
+// take what is queued (at most cfg.Batch packets per call; on the CPU entry point below
+// cfg.CPUBelow), parse it with HALO_RX_L3_START and act
 // per packet in order — ParseIpv4Pkt error: logged; not this NetIf's address: skipped; else the
 // local RxIcmp / RxUdp / RxTcp. Handlers that queue more loopback packets are drained in the same
 // call, as the reference's select loop drains them.
-func (i *NetIf) drainLoChanBatched(x *gpurx.Ctx, netif *gpurx.NetIfCfg, max int) {
+func (i *NetIf) drainLoChanBatched(x *gpurx.Ctx, netif *gpurx.NetIfCfg, cfg *BatchConfig) {
+	max := cfg.Batch
 	for {
 		var pkts [][]byte
 	take:
@@ -191,7 +206,7 @@ func (i *NetIf) drainLoChanBatched(x *gpurx.Ctx, netif *gpurx.NetIfCfg, max int)
 			return
 		}
 		b := gpurx.PackAligned(pkts)
-		if err := x.ParseBatch(b, netif, true); err != nil {
+		if err := cfg.parse(x, b, netif, true); err != nil {
 			Log(fmt.Sprintf("gpurx parse error: %v\n", err))
 			return
 		}

@@ -45,3 +45,13 @@ func ParseFramesCPU(buf []byte, off []uint64, lens []uint16, netif *NetIfCfg, l3
 		(*C.uint16_t)(unsafe.Pointer(&lens[0])), C.uint32_t(len(lens)), flags, &n,
 		(*C.halo_rx_result_t)(unsafe.Pointer(&out[0])), nil))
 }
+
+// ParseBatchCPU is Ctx.ParseBatch on the calling core: every frame of b through ParseFramesCPU
+// (l3: bare IPv4 packets), then Dispatch / DispatchLoopback into b.Res and b.Act.
+func ParseBatchCPU(b *Batch, netif *NetIfCfg, l3 bool) error {
+	n := b.Len()
+	if err := ParseFramesCPU(b.Buf, b.Off, b.Lens, netif, l3, b.Res[:n]); err != nil {
+		return err
+	}
+	return dispatch(l3, b.Res[:n], netif, b.Act[:n])
+}

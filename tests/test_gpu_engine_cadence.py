@@ -91,7 +91,7 @@ def _reference_order(sched):
     return h.log
 
 
-def _batched_order(sched, batch, drain_every):
+def _batched_order(sched, batch, drain_every, cpu_below=0):
     from halo_amd.engine import NetIf
 
     it = iter(sched)
@@ -101,7 +101,7 @@ def _batched_order(sched, batch, drain_every):
         polls[0] += 1
         return next(it, None)
 
-    netif = NetIf("eth0", "AA:AA:AA:AA:AA:AA", "192.168.100.100", rx)
+    netif = NetIf("eth0", "AA:AA:AA:AA:AA:AA", "192.168.100.100", rx, cpu_below=cpu_below)
     h = Handlers(netif.LoChan)
     for port in (7000, 7001, 7002):
         netif.RecvUdp(port, lambda s, p, port=port: h.udp(port, p))
@@ -124,6 +124,13 @@ def test_reference_cadence_reproduces_order(setup, batch):
     sched, want = setup
     assert len(want) > 500 and any(p == 7002 for p, _ in want)
     assert _batched_order(sched, batch, 99) == want
+
+
+@pytest.mark.parametrize("batch", [32, 4096])
+def test_mixed_cpu_gpu_routing_reproduces_order(setup, batch):
+    """Batches and drains below 40 frames on the CPU entry point, the rest on the GPU: the same order."""
+    sched, want = setup
+    assert _batched_order(sched, batch, 99, cpu_below=40) == want
 
 
 def test_every_batch_drain_differs(setup):
