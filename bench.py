@@ -1403,6 +1403,7 @@ def cpu_baseline(fr, seconds: float, rotate: int):
         pass
     shard = f"{n / 2 ** 20:g}M x {int(lay['lens'][0])}B UDP frames ({rotate} batches, the GPU line's rotation)"
     quota = cgroup_cpu_quota()
+    entry = cpu_entry_rate(host, lay, seconds=min(2.0, seconds / 2), threads=share)
     return {"value": round(one[0], 3), "unit": "Mpps", "cores": 1, "kind": "port",
             "sample": f"{shard}, {one[1]} passes in {one[2]:.1f}s, oracle/halo_rx_oracle.c -O2, one thread; "
                       f"cpu={model}",
@@ -1412,7 +1413,53 @@ def cpu_baseline(fr, seconds: float, rotate: int):
                              "note": "the same shard index-sharded over threads = len(sched_getaffinity); "
                                      "the process's cgroup CPU quota (cpu_quota_cores) caps what they get"},
             "multi_thread_share": {"value": round(sh[0], 3), "threads": share, "passes": sh[1], "cores_busy": sh[3],
-                                   "note": "the box's CPU share for one GPU (OMP_NUM_THREADS)"}}
+                                   "note": "the box's CPU share for one GPU (OMP_NUM_THREADS)"},
+            "cpu_entry": entry}
+
+
+def cpu_entry_rate(host, lay, seconds: float, threads: int) -> dict:
+    """The product's own CPU entry point (halo_rx_parse_batch_cpu, libhalo_rx_cpu.so) over the same
+    shard: one thread, and `threads` threads on contiguous index ranges (ctypes drops the GIL for
+    the call). Not the baseline (that is the port above); the fastest CPU path this build ships."""
+    import ctypes
+    import threading
+
+    import numpy as np
+
+    from halo_amd import cpu as cpu_entry
+    from halo_amd._lib import RESULT_DTYPE, NetIf
+
+    n = lay["n"]
+    offs = lay["offsets_dw"].astype(np.uint64) * 4
+    lens = np.ascontiguousarray(lay["lens"])
+    out = np.zeros(n, dtype=RESULT_DTYPE)
+    netif = NetIf.make()
+    L = cpu_entry.lib
+
+    def run(lo, hi):
+        rc = L.halo_rx_parse_batch_cpu(host.ctypes.data, offs.ctypes.data + 8 * lo, lens.ctypes.data + 2 * lo, hi - lo,
+                                       1, netif, out.ctypes.data + 32 * lo, None)
+        assert rc == 0, rc
+
+    res = {}
+    for t in sorted({1, threads}):
+        cuts = [n * k // t for k in range(t + 1)]
+        run(0, n)  # warm
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            ths = [threading.Thread(target=run, args=(cuts[k], cuts[k + 1])) for k in range(t)]
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        res[t] = round(passes * n / el / 1e6, 3)
+    ok = bool(np.all(out["status"] == 0))
+    return {"value": res[1], "unit": "Mpps", "threads": 1, "value_threads": res[threads], "threads_n": threads,
+            "ok": ok, "note": "halo_rx_parse_batch_cpu (include/halo_rx_cpu.h) over the same shard"}
 
 
 LINE_LIMIT = 7680  # bytes: the final stdout line stays under 8 KB, what the driver parses (VERDICT r5 #1)
@@ -1435,9 +1482,10 @@ def _compact_cpu(c: dict) -> dict:
     out = {k: c[k] for k in ("value", "unit", "cores", "kind") if k in c}
     if "sample" in c:
         out["sample"] = str(c["sample"])[:_SAMPLE_MAX]
-    for k in ("multi_thread", "multi_thread_share"):
+    for k in ("multi_thread", "multi_thread_share", "cpu_entry"):
         if isinstance(c.get(k), dict):
-            out[k] = {kk: c[k][kk] for kk in ("value", "threads", "cpus_in_affinity", "cpu_quota_cores", "cores_busy") if kk in c[k]}
+            out[k] = {kk: c[k][kk] for kk in ("value", "threads", "cpus_in_affinity", "cpu_quota_cores", "cores_busy",
+                                              "value_threads", "threads_n") if kk in c[k]}
     return out
 
 

@@ -121,7 +121,9 @@ def test_cpu_baseline_reports_threads_and_busy_cores():
         assert res[k]["value"] > 0 and res[k]["threads"] >= 1 and res[k]["cores_busy"] >= 0
     assert "cpu_quota_cores" in res["multi_thread"]
     assert "16 batches" in res["sample"]
-    assert len(json.dumps(bench.compact_line({"cpu_baseline": res})["cpu_baseline"])) < 700
+    ce = res["cpu_entry"]
+    assert ce["ok"] and ce["value"] > 0 and ce["value_threads"] > 0 and ce["threads"] == 1
+    assert len(json.dumps(bench.compact_line({"cpu_baseline": res})["cpu_baseline"])) < 800
 
 
 def test_cgroup_quota_parser():
