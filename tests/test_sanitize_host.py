@@ -51,3 +51,29 @@ def test_library_links_the_fuzzed_source():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert "host_logic.cc" in mod.SOURCES
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_cpu_entry_fuzz_asan_ubsan(tmp_path):
+    """The shipped CPU entry point (halo_amd/csrc/rx_cpu.cc, libhalo_rx_cpu.so) under ASan/UBSan
+    (tools/fuzz_cpu_entry.cc): the structured fuzz corpus with every frame in a heap block of exactly
+    its length, one frame per call and in odd-aligned batches, frames and LoChan packets, flags 0..3,
+    every record equal to the oracle's."""
+    inc = [f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(ROOT, 'halo_amd', 'csrc')}"]
+    objs = []
+    for src, cc, std in (("halo_amd/csrc/rx_cpu.cc", "g++", "-std=c++17"), ("tools/fuzz_cpu_entry.cc", "g++", "-std=c++17"),
+                         ("oracle/halo_rx_oracle.c", "gcc", "-std=c11"), ("oracle/halo_fuzz.c", "gcc", "-std=c11")):
+        o = tmp_path / (os.path.basename(src) + ".o")
+        subprocess.run([cc, std, *SAN, "-Wall", *inc, "-c", os.path.join(ROOT, src), "-o", str(o)], check=True)
+        objs.append(str(o))
+    exe = tmp_path / "fuzz_cpu_entry"
+    subprocess.run(["g++", "-fsanitize=address,undefined", *objs, "-lpthread", "-o", str(exe)], check=True)
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "verify_asan_link_order=0:detect_leaks=1:" + env.get("ASAN_OPTIONS", "")
+    r = subprocess.run([str(exe), "20000", "0xC9E"], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    m = re.search(r"cpu entry: (\d+) records checked.*statuses(.*)", r.stdout)
+    assert m, r.stdout
+    assert int(m.group(1)) == 2 * 2 * 4 * 20000
+    seen = {int(k): int(v) for k, v in (t.split(":") for t in m.group(2).split())}
+    assert sum(1 for v in seen.values() if v) >= 12  # every status the corpus reaches, frames and packets
