@@ -55,3 +55,17 @@ func ParseBatchCPU(b *Batch, netif *NetIfCfg, l3 bool) error {
 	}
 	return dispatch(l3, b.Res[:n], netif, b.Act[:n])
 }
+
+// parseOneCPU is parseOne (parse.go) on the calling core: one frame, or one bare IPv4 packet when
+// l3, with no NetIf (the Parse* wrappers read no dispatch flag). Lengths past 65535 are capped as
+// parseOne caps them: every such length gets the same ETH_LEN / IP_LEN verdict.
+func parseOneCPU(buf []byte, l3 bool) (Result, error) {
+	n := len(buf)
+	if n > 0xFFFF {
+		n = 0xFFFF
+	}
+	var r [1]Result
+	netif := &NetIfCfg{MacAddr: make([]byte, 6), IpAddr: make([]byte, 4)}
+	err := ParseFramesCPU(buf[:n], []uint64{0}, []uint16{uint16(n)}, netif, l3, r[:])
+	return r[0], err
+}

@@ -297,9 +297,12 @@ def icmp_ttl_deep_nat_batch(frames, offsets_dw, lens, *, nat=None, check_sum_ena
 # example/example.go:162-168) or code ported from the reference — each wrapper returns exactly the
 # tuple its Go function returns, with `err` the reference's error string (None on success). The
 # frame goes through the GPU like a batch of one (halo_rx_parse_batch_host, a per-process host
-# context whose resident consumer serves it: one request, no launch): there is no CPU path. Batches of frames belong on parse_frames_batch / engine.
+# context whose resident consumer serves it: one request, no launch) unless SINGLE_FRAME_CPU is set,
+# which sends it to the CPU entry point instead (halo_amd.cpu, include/halo_rx_cpu.h: the same record
+# on the calling core, no GPU round trip). Batches of frames belong on parse_frames_batch / engine.
 CheckSumEnable = True  # protocol.CheckSumEnable (protocol/utils.go:8) for the wrappers below
 DEVICE = 0             # the device the wrappers' host context uses
+SINGLE_FRAME_CPU = False  # the caller's choice, read at every call (go/gpurx SingleFrameCPU)
 
 
 class ReferencePanic(RuntimeError):
@@ -312,11 +315,19 @@ _ctx = {}
 
 
 def _parse_one(buf: bytes, l3: bool) -> np.void:
-    """One Ethernet frame (or, l3, one bare IPv4 packet) parsed on the GPU: its halo_rx_result_t.
+    """One Ethernet frame (or, l3, one bare IPv4 packet) parsed on the GPU (on the CPU entry point
+    with SINGLE_FRAME_CPU): its halo_rx_result_t.
     Lengths past 65535 are passed as 65535 (any length over the reference's caps gets the same
     ETH_LEN / IP_LEN verdict)."""
     import ctypes
 
+    if SINGLE_FRAME_CPU:
+        from . import cpu
+
+        n = min(len(buf), 0xFFFF)
+        data = np.frombuffer(bytes(buf[:n]), np.uint8) if n else np.zeros(4, np.uint8)
+        return cpu.parse_frames_cpu(data, np.zeros(1, np.uint64), np.array([n], np.uint16), netif=NetIf.make(),
+                                    check_sum_enable=CheckSumEnable, l3_start=l3)[0]
     if DEVICE not in _ctx:
         h = ctypes.c_void_p()
         _lib.check("halo_rx_host_ctx_create", _lib.lib.halo_rx_host_ctx_create(DEVICE, 64, 1 << 16, ctypes.byref(h)))
