@@ -53,6 +53,8 @@ def parse_frames_cpu(data: np.ndarray, offsets: np.ndarray, lens: np.ndarray, *,
     if hist is not None and (hist.dtype != np.uint32 or hist.shape[0] < HALO_RX_STATUS_COUNT
                              or not hist.flags.c_contiguous):
         raise ValueError("hist must be a contiguous u32 array of 14 counters")
+    if data.size == 0:  # every frame is empty: any valid address will do (the call needs a non-null one)
+        data = np.zeros(4, np.uint8)
     flags = (1 if check_sum_enable else 0) | (2 if jumbo else 0) | (0x10 if l3_start else 0)
     p = lambda a: None if a is None or a.size == 0 else a.ctypes.data  # noqa: E731
     check("halo_rx_parse_batch_cpu", lib.halo_rx_parse_batch_cpu(p(data), p(offsets), p(lens), n, flags, netif,

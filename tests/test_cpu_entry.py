@@ -140,6 +140,17 @@ def test_synthetic_batches_match_oracle(cpu, oracle_lib, size_mode, length, jumb
     assert_records_equal(got, want, None, f"synthetic {length} B")
 
 
+def test_empty_frames_and_empty_buffer(cpu):
+    """A batch whose frames are all empty (no data bytes at all) parses: ETH_LEN, or IP_LEN as LoChan
+    packets, and no byte is read."""
+    from halo_amd._lib import NetIf
+
+    for l3, want in ((False, 1), (True, 3)):
+        got = cpu.parse_frames_cpu(np.zeros(0, np.uint8), np.zeros(3, np.uint64), np.zeros(3, np.uint16),
+                                   netif=NetIf.make(), l3_start=l3)
+        assert list(got["status"]) == [want] * 3
+
+
 def test_argument_checks(cpu):
     from halo_amd import _lib
 

@@ -39,3 +39,14 @@ def test_cpu_routing_needs_no_device():
     netif = NetIf("eth0", "AA:AA:AA:AA:AA:AA", "192.168.100.100", lambda: next(frames, None), cpu_below=ALL_CPU)
     res, acts = netif.packet_handle_batch(batch=4096, drain_every=99)
     assert len(res) > 50 and netif._batcher is None
+
+
+def test_cpu_routing_empty_frames():
+    """EthRxFunc returning empty (non-nil) buffers: ParseEthFrm's length error, dropped (DROP_ETH)."""
+    from halo_amd import ACTION
+    from halo_amd.engine import NetIf
+
+    frames = iter([b"", b"", None])
+    netif = NetIf("eth0", "AA:AA:AA:AA:AA:AA", "192.168.100.100", lambda: next(frames, None), cpu_below=ALL_CPU)
+    res, acts = netif.packet_handle_batch(batch=16, drain_every=0)
+    assert list(res["status"]) == [1, 1] and list(acts) == [ACTION["DROP_ETH"]] * 2
