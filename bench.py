@@ -1469,10 +1469,11 @@ def cpu_entry_rate(host, lay, seconds: float, threads: int) -> dict:
             "ok": ok, "note": "halo_rx_parse_batch_cpu (include/halo_rx_cpu.h) over the same shard"}
 
 
+WIRE_OVERHEAD = 24  # bytes per frame on the wire beyond the L2 buffer: preamble + SFD 8, FCS 4, IFG 12
 LINE_LIMIT = 7680  # bytes: the final stdout line stays under 8 KB, what the driver parses
 # per-entry numbers the stdout line keeps; everything else (prose, probe tables, per-size curves'
 # percentiles) goes to the detail file only
-_KEEP_NUM = ("mpps", "mstrings_per_s", "mlookups_per_s", "mrecords_per_s", "gbit_s", "kernel_ms", "ms_per_batch",
+_KEEP_NUM = ("mpps", "mstrings_per_s", "mlookups_per_s", "mrecords_per_s", "gbit_s", "gbit_s_wire", "kernel_ms", "ms_per_batch",
              "us_per_batch", "ok", "speedup_vs_separate", "vs_headline", "vs_headline_per_batch", "failing_frac",
              "crossover_frames", "cpu_port_ns_per_frame", "cpu_entry_ns_per_frame", "cpu_entry_crossover_frames", "value", "unit", "ms_per_step")
 _KEEP_ROOF = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_session", "frac_frames_only",
@@ -1606,6 +1607,8 @@ def main():
     mpps = frames_total / wall / 1e6
     fbytes = frame_bytes(batches[0])
     gbit = fbytes * args.steps * d.world * 8 / wall / 1e9
+    # the same frames as wire bits: + 24 B each for preamble + SFD (8), FCS (4), inter-frame gap (12)
+    gbit_wire = (fbytes + WIRE_OVERHEAD * n) * args.steps * d.world * 8 / wall / 1e9
     alg = fbytes + n * (4 + 2 + RESULT_BYTES)  # frames + dword offset + u16 len + record
     # every rank checks its own shard on its own device after the timed region, and says which device
     ident = device_identity(gpu)
@@ -1630,6 +1633,7 @@ def main():
                    "frames_total": shard_frames * d.world,
                    "parallelism": f"index-sharded x{d.world}, no collective"},
         "gbit_s": round(gbit, 2),
+        "gbit_s_wire": round(gbit_wire, 2),
         "kernel_ms": round(max(per_rank_kms), 5),
         "per_rank_kernel_ms": [round(k, 5) for k in per_rank_kms],
         "kernel": "rx_lane_kernel<0, 0> (lane per frame, ragged, no fused pass)",
@@ -1776,7 +1780,9 @@ def main():
             meta = 0 if strided_len else 6
             a2 = fb + nn * (meta + RESULT_BYTES)
             sec[name] = {"frames": nn, "mpps": round(nn * steps / w2 / 1e6, 1),
-                         "gbit_s": round(fb * steps * 8 / w2 / 1e9, 1), "kernel_ms": round(k2, 4),
+                         "gbit_s": round(fb * steps * 8 / w2 / 1e9, 1),
+                         "gbit_s_wire": round((fb + WIRE_OVERHEAD * nn) * steps * 8 / w2 / 1e9, 1),
+                         "kernel_ms": round(k2, 4),
                          "roofline": roofline(a2, k2, load_traffic(name), frame_bytes=fb)}
             if "imix" in name:
                 sec[name]["mix"] = ("sizes 64/570/1500 B at 7:4:1; protocols UDP 50 / TCP 40 / ICMP 10 % "
