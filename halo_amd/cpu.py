@@ -12,7 +12,7 @@ import os
 
 import numpy as np
 
-from ._lib import LIB_DIR, RESULT_DTYPE, HALO_RX_STATUS_COUNT, NetIf, check
+from ._lib import HALO_RX_RECORD_COMPACT, HALO_RX_STATUS_COUNT, LIB_DIR, RECORD16_DTYPE, RESULT_DTYPE, NetIf, check
 
 CPU_LIB_PATH = os.path.join(LIB_DIR, "libhalo_rx_cpu.so")
 
@@ -34,10 +34,11 @@ lib = _load()
 
 def parse_frames_cpu(data: np.ndarray, offsets: np.ndarray, lens: np.ndarray, *, netif: NetIf,
                      check_sum_enable: bool = True, jumbo: bool = False, l3_start: bool = False,
-                     out: np.ndarray | None = None, hist: np.ndarray | None = None) -> np.ndarray:
+                     compact: bool = False, out: np.ndarray | None = None,
+                     hist: np.ndarray | None = None) -> np.ndarray:
     """Parse + verify n frames in host memory (frame i: lens[i] bytes at data[offsets[i]:]) on the
-    calling core; returns the n RESULT_DTYPE records (into `out` when given). `hist` (u32[14]) is
-    incremented per status."""
+    calling core; returns the n RESULT_DTYPE records, or RECORD16_DTYPE ones with `compact` (into
+    `out` when given). `hist` (u32[14]) is incremented per status."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint16)
@@ -46,16 +47,18 @@ def parse_frames_cpu(data: np.ndarray, offsets: np.ndarray, lens: np.ndarray, *,
         raise ValueError("offsets and lens differ in length")
     if n and int((offsets + lens).max()) > data.nbytes:
         raise ValueError("a frame reaches past the end of data")
+    rec = RECORD16_DTYPE if compact else RESULT_DTYPE
     if out is None:
-        out = np.empty(n, dtype=RESULT_DTYPE)
-    if out.dtype != RESULT_DTYPE or out.shape[0] < n or not out.flags.c_contiguous:
-        raise ValueError("out must be a contiguous RESULT_DTYPE array of n records")
+        out = np.empty(n, dtype=rec)
+    if out.dtype != rec or out.shape[0] < n or not out.flags.c_contiguous:
+        raise ValueError(f"out must be a contiguous array of n {'RECORD16' if compact else 'RESULT'}_DTYPE records")
     if hist is not None and (hist.dtype != np.uint32 or hist.shape[0] < HALO_RX_STATUS_COUNT
                              or not hist.flags.c_contiguous):
         raise ValueError("hist must be a contiguous u32 array of 14 counters")
     if data.size == 0:  # every frame is empty: any valid address will do (the call needs a non-null one)
         data = np.zeros(4, np.uint8)
-    flags = (1 if check_sum_enable else 0) | (2 if jumbo else 0) | (0x10 if l3_start else 0)
+    flags = ((1 if check_sum_enable else 0) | (2 if jumbo else 0) | (0x10 if l3_start else 0)
+             | (HALO_RX_RECORD_COMPACT if compact else 0))
     p = lambda a: None if a is None or a.size == 0 else a.ctypes.data  # noqa: E731
     check("halo_rx_parse_batch_cpu", lib.halo_rx_parse_batch_cpu(p(data), p(offsets), p(lens), n, flags, netif,
                                                                  p(out), p(hist)))

@@ -217,15 +217,34 @@ inline void parse_one(const uint8_t* f, uint32_t L, const Own& own, halo_rx_resu
     }
 }
 
-template <bool L3>
+// The 16-byte record of a full one (HALO_RX_RECORD_COMPACT, include/halo_rx.h): the EtherType as
+// its class in flags bits 4-5, as rx_parse.hip's frame_store packs it.
+inline halo_rx_record16_t compact(const halo_rx_result_t& r) {
+    halo_rx_record16_t c;
+    const uint32_t et_class = r.ethertype == kEthArp ? HALO_RX_F_ET_ARP
+                            : r.ethertype == kEthIpv6 ? HALO_RX_F_ET_IPV6
+                            : r.ethertype == kEthIeee8023 ? HALO_RX_F_ET_8023 : HALO_RX_F_ET_IPV4;
+    c.status = r.status;
+    c.flags = (uint8_t)(r.flags | et_class);
+    c.ip_proto = r.ip_proto;
+    c.l4_aux = r.l4_aux;
+    c.src_ip = r.src_ip;
+    c.dst_ip = r.dst_ip;
+    c.sport = r.sport;
+    c.dport = r.dport;
+    return c;
+}
+
+template <bool L3, bool COMPACT>
 void parse_all(const uint8_t* bytes, const uint64_t* offsets, const uint16_t* lens, uint32_t n, const Own& own,
-               halo_rx_result_t* out, uint32_t* hist) {
+               void* out, uint32_t* hist) {
     constexpr uint32_t kAhead = 8;  // frames prefetched ahead of the one being parsed
     for (uint32_t i = 0; i < n; ++i) {
         if (i + kAhead < n) __builtin_prefetch(bytes + offsets[i + kAhead]);
         halo_rx_result_t r;
         parse_one<L3>(bytes + offsets[i], lens[i], own, r);
-        out[i] = r;
+        if (COMPACT) static_cast<halo_rx_record16_t*>(out)[i] = compact(r);
+        else static_cast<halo_rx_result_t*>(out)[i] = r;
         if (hist) ++hist[r.status];
     }
 }
@@ -236,9 +255,9 @@ extern "C" HALO_API int halo_rx_parse_batch_cpu(const uint8_t* bytes, const uint
                                                 uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
                                                 halo_rx_result_t* out, uint32_t* status_hist) {
     if (!netif) return HALO_E_INVAL;
-    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_UNIFORM_LEN | HALO_RX_L3_START |
-                  HALO_RX_VARIANT_MASK))
-        return HALO_E_INVAL;  // HALO_RX_RECORD_COMPACT included: full records only, as the host path
+    if (flags & ~(HALO_RX_CSUM_ENABLE | HALO_RX_JUMBO_EXT | HALO_RX_RECORD_COMPACT | HALO_RX_UNIFORM_LEN |
+                  HALO_RX_L3_START | HALO_RX_VARIANT_MASK))
+        return HALO_E_INVAL;
     if (n == 0) return HALO_OK;
     if (!bytes || !offsets || !lens || !out) return HALO_E_INVAL;
     Own own;
@@ -247,8 +266,11 @@ extern "C" HALO_API int halo_rx_parse_batch_cpu(const uint8_t* bytes, const uint
     own.ip = netif->ip;
     own.csum = (flags & HALO_RX_CSUM_ENABLE) != 0;
     own.jumbo = (flags & HALO_RX_JUMBO_EXT) != 0;
-    if (flags & HALO_RX_L3_START) parse_all<true>(bytes, offsets, lens, n, own, out, status_hist);
-    else parse_all<false>(bytes, offsets, lens, n, own, out, status_hist);
+    const bool l3 = (flags & HALO_RX_L3_START) != 0, c16 = (flags & HALO_RX_RECORD_COMPACT) != 0;
+    if (l3 && c16) parse_all<true, true>(bytes, offsets, lens, n, own, out, status_hist);
+    else if (l3) parse_all<true, false>(bytes, offsets, lens, n, own, out, status_hist);
+    else if (c16) parse_all<false, true>(bytes, offsets, lens, n, own, out, status_hist);
+    else parse_all<false, false>(bytes, offsets, lens, n, own, out, status_hist);
     return HALO_OK;
 }
 

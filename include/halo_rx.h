@@ -76,7 +76,8 @@ extern "C" {
 #define HALO_RX_JUMBO_EXT 0x2u   /* build-defined extension: lift the 1514/1500/1480 caps   */
                                  /* to 9014/9000/8980 (MTU 9000); arithmetic unchanged      */
 #define HALO_RX_RECORD_COMPACT 0x4u /* write halo_rx_record16_t (16 B) instead of            */
-                                    /* halo_rx_result_t (32 B); device entry points only     */
+                                    /* halo_rx_result_t (32 B); device entry points and      */
+                                    /* halo_rx_parse_batch_cpu (include/halo_rx_cpu.h) only  */
 #define HALO_RX_UNIFORM_LEN 0x8u    /* ragged batch whose frames all have length max_len_hint */
                                     /* (a speed hint: picks the uniform-length kernel table)  */
 /* Every buffer starts at its IPv4 header: the packets of a NetIf's LoChan, which

@@ -26,14 +26,14 @@ extern "C" {
 #endif
 
 /* Frames in host memory: frame i is lens[i] bytes at bytes + offsets[i] (any alignment).
- * `out` receives n halo_rx_result_t records; `status_hist`, if not NULL, receives
+ * `out` receives n halo_rx_result_t records, or n halo_rx_record16_t with HALO_RX_RECORD_COMPACT
+ * (the device entry points' compact records, byte for byte); `status_hist`, if not NULL, receives
  * HALO_RX_STATUS_COUNT u32 counters that are INCREMENTED. Flags: HALO_RX_CSUM_ENABLE,
- * HALO_RX_JUMBO_EXT, HALO_RX_L3_START; HALO_RX_UNIFORM_LEN and the variant bits are accepted and
- * ignored (they only pick kernels); HALO_RX_RECORD_COMPACT is refused, as by
- * halo_rx_parse_batch_host. Synchronous, on the calling thread; thread-safe (no state). No byte
- * outside [offsets[i], offsets[i] + lens[i]) is read, and no byte of a frame that fails
- * ParseEthFrm's length check (ParseIpv4Pkt's, with HALO_RX_L3_START). n = 0: HALO_OK with null
- * arrays; otherwise a null pointer or unknown flag bit is HALO_E_INVAL.                      */
+ * HALO_RX_JUMBO_EXT, HALO_RX_L3_START, HALO_RX_RECORD_COMPACT; HALO_RX_UNIFORM_LEN and the variant
+ * bits are accepted and ignored (they only pick kernels). Synchronous, on the calling thread;
+ * thread-safe (no state). No byte outside [offsets[i], offsets[i] + lens[i]) is read, and no byte
+ * of a frame that fails ParseEthFrm's length check (ParseIpv4Pkt's, with HALO_RX_L3_START).
+ * n = 0: HALO_OK with null arrays; otherwise a null pointer or unknown flag bit is HALO_E_INVAL.  */
 HALO_API int halo_rx_parse_batch_cpu(const uint8_t* bytes, const uint64_t* offsets, const uint16_t* lens,
                                      uint32_t n, uint32_t flags, const halo_rx_netif_t* netif,
                                      halo_rx_result_t* out, uint32_t* status_hist);

@@ -110,6 +110,22 @@ def test_fuzz_corpus_matches_oracle(cpu, oracle_lib, fuzz, flags):
     assert_records_equal(got2, want, None, f"fuzz unaligned flags={flags}")
 
 
+@pytest.mark.parametrize("flags", [0, 1, 3])
+def test_fuzz_corpus_compact_records(cpu, oracle_lib, fuzz, flags):
+    """HALO_RX_RECORD_COMPACT: each 16-byte record is the packing (compact_of) of the full record,
+    for Ethernet frames and LoChan packets; the histogram is unchanged."""
+    from halo_amd._lib import NetIf, compact_of
+    from tests.helpers import strip_ethernet
+
+    for l3, (data, offs, lens) in ((False, fuzz), (True, strip_ethernet(*fuzz))):
+        kw = dict(netif=NetIf.make(), check_sum_enable=bool(flags & 1), jumbo=bool(flags & 2), l3_start=l3)
+        full = cpu.parse_frames_cpu(data, _byte_offsets(offs), lens, **kw)
+        h16 = np.zeros(14, np.uint32)
+        c16 = cpu.parse_frames_cpu(data, _byte_offsets(offs), lens, compact=True, hist=h16, **kw)
+        assert c16.tobytes() == compact_of(full).tobytes(), (l3, flags)
+        assert np.array_equal(h16, np.bincount(full["status"], minlength=14))
+
+
 @pytest.mark.parametrize("flags", [1, 3])
 def test_fuzz_corpus_as_lochan_packets_matches_oracle(cpu, oracle_lib, fuzz, flags):
     from halo_amd._lib import NetIf
@@ -165,8 +181,6 @@ def test_argument_checks(cpu):
     assert L.halo_rx_parse_batch_cpu(None, offs.ctypes.data, lens.ctypes.data, 1, 1, ni, out.ctypes.data,
                                      None) == _lib.HALO_E_INVAL
     assert L.halo_rx_parse_batch_cpu(*a, 1, 1, ni, None, None) == _lib.HALO_E_INVAL
-    assert L.halo_rx_parse_batch_cpu(*a, 1, 1 | _lib.HALO_RX_RECORD_COMPACT, ni, out.ctypes.data,
-                                     None) == _lib.HALO_E_INVAL
     assert L.halo_rx_parse_batch_cpu(*a, 1, 1 | 0x20, ni, out.ctypes.data, None) == _lib.HALO_E_INVAL
     # kernel-choice bits are accepted and change nothing
     assert L.halo_rx_parse_batch_cpu(*a, 1, 1 | _lib.HALO_RX_UNIFORM_LEN | _lib.variant_flags(16), ni,

@@ -25,7 +25,7 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _gpu(dev, data, offs_dw, lens, flags):
+def _gpu(dev, data, offs_dw, lens, flags, compact=False):
     import torch
 
     from halo_amd import _lib
@@ -35,20 +35,21 @@ def _gpu(dev, data, offs_dw, lens, flags):
     d = torch.from_numpy(data).to(dev)
     o = torch.from_numpy(offs_dw.view(np.int32)).to(dev)
     ln = torch.from_numpy(lens.view(np.int16)).to(dev)
-    out = torch.full((n, 32), 0xEE, dtype=torch.uint8, device=dev)
+    out = torch.full((n, 16 if compact else 32), 0xEE, dtype=torch.uint8, device=dev)
     _lib.check("halo_rx_parse_batch_device", _lib.lib.halo_rx_parse_batch_device(
-        d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, flags, NetIf.make(), 0, out.data_ptr(), None,
-        torch.cuda.current_stream().cuda_stream))
+        d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, flags | (_lib.HALO_RX_RECORD_COMPACT if compact else 0),
+        NetIf.make(), 0, out.data_ptr(), None, torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
-    return out.cpu().numpy().view(RESULT_DTYPE).reshape(n)
+    return out.cpu().numpy().view(_lib.RECORD16_DTYPE if compact else RESULT_DTYPE).reshape(n)
 
 
-def _cpu(data, offs_dw, lens, flags):
+def _cpu(data, offs_dw, lens, flags, compact=False):
     from halo_amd import cpu
     from halo_amd._lib import NetIf
 
     return cpu.parse_frames_cpu(data, offs_dw.astype(np.uint64) * 4, lens, netif=NetIf.make(),
-                                check_sum_enable=bool(flags & 1), jumbo=bool(flags & 2), l3_start=bool(flags & 0x10))
+                                check_sum_enable=bool(flags & 1), jumbo=bool(flags & 2), l3_start=bool(flags & 0x10),
+                                compact=compact)
 
 
 @pytest.fixture(scope="module")
@@ -61,6 +62,14 @@ def test_fuzz_cpu_entry_equals_gpu(dev, fuzz, flags):
     data, offs, lens = fuzz
     assert_records_equal(_cpu(data, offs, lens, flags), _gpu(dev, data, offs, lens, flags), None,
                          f"fuzz flags={flags}")
+
+
+@pytest.mark.parametrize("flags", [0, 1, 3])
+def test_fuzz_compact_cpu_entry_equals_gpu(dev, fuzz, flags):
+    """HALO_RX_RECORD_COMPACT on both sides: the 16-byte records match byte for byte."""
+    data, offs, lens = fuzz
+    got, want = _cpu(data, offs, lens, flags, compact=True), _gpu(dev, data, offs, lens, flags, compact=True)
+    assert got.tobytes() == want.tobytes(), np.nonzero(got != want)[0][:8]
 
 
 @pytest.mark.parametrize("flags", [1, 3])
