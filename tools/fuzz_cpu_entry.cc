@@ -3,8 +3,8 @@
 // fuzz corpus (oracle/halo_fuzz.c: every size class 0..9100 B, header-targeted mutations) with every
 // frame copied into a heap block of EXACTLY its length, so any read past a frame's last byte is an
 // ASan report, parsed one frame per call and in batches at odd offsets, as Ethernet frames and as
-// LoChan packets (the frame minus its first 14 bytes), under flags 0..3; every record is compared
-// with the oracle's for the same bytes.
+// LoChan packets (the frame minus its first 14 bytes), under flags 0..3, full and compact records;
+// every record is compared with the oracle's for the same bytes.
 // usage: fuzz_cpu_entry <frames> <seed>
 #include <stdint.h>
 #include <stdio.h>
@@ -78,6 +78,21 @@ int main(int argc, char** argv) {
                 ++counts[got[i].status];
             }
             if (hg != hw) return fail("histogram", 0, flags);
+            // compact records from the same exact-size blocks: the packing of the full ones
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint64_t zero = 0;
+                halo_rx_record16_t c;
+                if (halo_rx_parse_batch_cpu(blocks[i], &zero, &ln[i], 1, f | HALO_RX_RECORD_COMPACT, &ni,
+                                            reinterpret_cast<halo_rx_result_t*>(&c), nullptr) != HALO_OK)
+                    return 5;
+                const halo_rx_result_t& w = want[i];
+                const uint8_t et = w.ethertype == 0x0806 ? HALO_RX_F_ET_ARP : w.ethertype == 0x86DD ? HALO_RX_F_ET_IPV6
+                                 : w.ethertype == 0x05DC ? HALO_RX_F_ET_8023 : HALO_RX_F_ET_IPV4;
+                if (c.status != w.status || c.flags != (uint8_t)(w.flags | et) || c.ip_proto != w.ip_proto ||
+                    c.l4_aux != w.l4_aux || c.src_ip != w.src_ip || c.dst_ip != w.dst_ip || c.sport != w.sport ||
+                    c.dport != w.dport)
+                    return fail(l3 ? "compact L3" : "compact", i, flags);
+            }
             // batches of 1..97 frames repacked back to back at an odd base (no alignment at all)
             uint32_t i = 0;
             while (i < n) {
